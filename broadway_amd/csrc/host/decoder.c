@@ -1,0 +1,503 @@
+/* Host decoder control -- see decoder.h. */
+#include "decoder.h"
+#include "../common/tables.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <stdio.h>
+static int dbg_enabled(void) { static int e = -1; if (e < 0) e = getenv("H264MI_DEBUG") != NULL; return e; }
+#define DEC_FAIL(code) (dbg_enabled() ? (fprintf(stderr, "h264mi: %s:%d -> %d\n", __FILE__, __LINE__, (code)), (code)) : (code))
+#define SPS_FORCE (MAX_SPS + 1)
+#define PPS_FORCE (MAX_PPS + 1)
+
+int h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be)
+{
+    h264_tables_init();
+    memset(d, 0, sizeof(*d));
+    d->active_sps = -1;
+    d->active_pps = -1;
+    d->old_sps_id = -1;
+    d->no_reorder_app = no_output_reordering;
+    d->be = be;
+    d->aub_first_call = 1;
+    d->cur_slot = -1;
+    return 0;
+}
+
+void h264dec_release(H264Dec *d)
+{
+    if (d->pb_ready) picbuild_free(&d->pb);
+    free(d->rbsp);
+    free(d->out_frames);
+    if (d->be.destroy) d->be.destroy(d->be.ctx);
+    memset(d, 0, sizeof(*d));
+}
+
+const Sps *h264dec_active_sps(const H264Dec *d)
+{
+    if (d->active_sps < 0 || d->active_sps >= MAX_SPS) return NULL;
+    return &d->sps[d->active_sps];
+}
+
+int h264dec_valid_param_sets(const H264Dec *d)
+{
+    for (int i = 0; i < MAX_PPS; i++)
+        if (d->pps[i].valid && d->sps[d->pps[i].sps_id].valid) return 1;
+    return 0;
+}
+
+/* ---- byte stream: reference byte_stream.c:80-236 semantics ----------- */
+static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_t **nal,
+                       uint32_t *nal_len, uint32_t *read_bytes)
+{
+    uint32_t init = 0, size, zeros = 0;
+    int emul = 0;
+    if (len > 3 && bs[0] == 0 && bs[1] == 0 && (bs[2] & 0xFE) == 0) {
+        uint32_t cnt = 2;
+        zeros = 2;
+        const uint8_t *p = bs + 2;
+        for (;;) {
+            uint8_t b = *p++;
+            cnt++;
+            if (cnt == len) { *read_bytes = len; return -1; }
+            if (!b) zeros++;
+            else if (b == 1 && zeros >= 2) break;
+            else zeros = 0;
+        }
+        init = cnt;
+        zeros = 0;
+        int invalid = 0;
+        for (;;) {
+            uint8_t b = *p++;
+            cnt++;
+            if (!b) zeros++;
+            if (b == 1 && zeros >= 2) {
+                size = cnt - init - zeros - 1;
+                zeros -= zeros < 3 ? zeros : 3;
+                break;
+            } else if (b) {
+                if (zeros >= 3) invalid = 1;
+                zeros = 0;
+            }
+            if (cnt == len) { size = cnt - init - zeros; break; }
+        }
+        *read_bytes = size + init + zeros;
+        if (invalid) return -1;
+        emul = 1;
+    } else {
+        size = len;
+        *read_bytes = len;
+        emul = 1;
+    }
+    const uint8_t *src = bs + init;
+    if (d->rbsp_cap < size + 8) {
+        size_t nc = size + 64 + size / 2;
+        uint8_t *r = (uint8_t *)realloc(d->rbsp, nc);
+        if (!r) return -1;
+        d->rbsp = r;
+        d->rbsp_cap = nc;
+    }
+    uint32_t w = 0;
+    if (emul) {
+        int zc = 0;
+        for (uint32_t i = 0; i < size; i++) {
+            uint8_t b = src[i];
+            if (zc == 2 && b == 3) {
+                if (i == size - 1 || src[i + 1] > 3) return -1;
+                zc = 0;
+                continue;
+            }
+            if (zc == 2 && b <= 2) return -1;
+            zc = b == 0 ? zc + 1 : 0;
+            d->rbsp[w++] = b;
+        }
+    } else {
+        memcpy(d->rbsp, src, size);
+        w = size;
+    }
+    *nal = d->rbsp;
+    *nal_len = w;
+    return 0;
+}
+
+/* ---- picture order count, H.264 §8.2.1 -------------------------------- */
+static int decode_poc(H264Dec *d, const Sps *sps, const SliceHdr *sh)
+{
+    PocState *s = &d->poc;
+    int idr = sh->nal_type == NAL_IDR;
+    int max_fn = 1 << sps->log2_max_frame_num;
+    int poc = 0;
+    if (sps->poc_type == 0) {
+        if (idr) { s->prev_msb = 0; s->prev_lsb = 0; }
+        else if (s->prev_mmco5) { s->prev_msb = 0; s->prev_lsb = 0; }
+        int max_lsb = 1 << sps->log2_max_poc_lsb;
+        int msb;
+        if (sh->poc_lsb < s->prev_lsb && s->prev_lsb - sh->poc_lsb >= max_lsb / 2) msb = s->prev_msb + max_lsb;
+        else if (sh->poc_lsb > s->prev_lsb && sh->poc_lsb - s->prev_lsb > max_lsb / 2) msb = s->prev_msb - max_lsb;
+        else msb = s->prev_msb;
+        int top = msb + sh->poc_lsb;
+        int bot = top + sh->delta_poc_bottom;
+        poc = top < bot ? top : bot;
+        if (sh->nal_ref_idc) { s->prev_msb = msb; s->prev_lsb = sh->poc_lsb; }
+    } else {
+        int fno;
+        if (idr) fno = 0;
+        else if (s->prev_mmco5) fno = s->prev_frame_num > sh->frame_num ? max_fn : 0;
+        else if (s->prev_frame_num > sh->frame_num) fno = s->prev_frame_num_offset + max_fn;
+        else fno = s->prev_frame_num_offset;
+        if (sps->poc_type == 2) {
+            if (idr) poc = 0;
+            else if (!sh->nal_ref_idc) poc = 2 * (fno + sh->frame_num) - 1;
+            else poc = 2 * (fno + sh->frame_num);
+        } else {
+            int abs_fn = sps->num_ref_frames_in_poc_cycle ? fno + sh->frame_num : 0;
+            if (!sh->nal_ref_idc && abs_fn > 0) abs_fn--;
+            int exp = 0;
+            if (abs_fn > 0) {
+                int delta_cycle = 0;
+                for (int i = 0; i < sps->num_ref_frames_in_poc_cycle; i++) delta_cycle += sps->offset_for_ref_frame[i];
+                int cyc = (abs_fn - 1) / sps->num_ref_frames_in_poc_cycle;
+                int in_cyc = (abs_fn - 1) % sps->num_ref_frames_in_poc_cycle;
+                exp = cyc * delta_cycle;
+                for (int i = 0; i <= in_cyc; i++) exp += sps->offset_for_ref_frame[i];
+            }
+            if (!sh->nal_ref_idc) exp += sps->offset_for_non_ref_pic;
+            int top = exp + sh->delta_poc[0];
+            int bot = top + sps->offset_for_top_to_bottom + sh->delta_poc[1];
+            poc = top < bot ? top : bot;
+        }
+        s->prev_frame_num_offset = fno;
+        s->prev_frame_num = sh->frame_num;
+    }
+    s->prev_mmco5 = 0;
+    for (int i = 0; i < sh->nmmco; i++) if (sh->mmco[i].op == 5) s->prev_mmco5 = 1;
+    if (s->prev_mmco5) {
+        /* tempPicOrderCnt handling (§8.2.1): the picture is treated as POC 0 */
+        s->prev_frame_num_offset = 0;
+        s->prev_frame_num = 0;
+        if (sps->poc_type == 0) { s->prev_msb = 0; s->prev_lsb = 0; }
+        poc = 0;
+    }
+    return poc;
+}
+
+/* ---- access unit boundary (reference storage.c:632-760) --------------- */
+static int check_au_boundary(H264Dec *d, const NalHdr *nal, const BitReader *br, int *boundary)
+{
+    *boundary = 0;
+    if ((nal->type > 5 && nal->type < 12) || (nal->type > 12 && nal->type <= 18)) {
+        *boundary = 1;
+        return 0;
+    }
+    if (nal->type != NAL_SLICE && nal->type != NAL_IDR) return 0;
+    if (d->aub_first_call) { *boundary = 1; d->aub_first_call = 0; }
+    int pps_id;
+    if (peek_slice_pps_id(br, &pps_id)) return DEC_FAIL(DEC_ERROR);
+    const Pps *pps = &d->pps[pps_id];
+    if (!pps->valid || !d->sps[pps->sps_id].valid ||
+        (d->active_sps >= 0 && d->active_sps < MAX_SPS && pps->sps_id != d->active_sps && nal->type != NAL_IDR))
+        return DEC_FAIL(DEC_PARAM_SET_ERROR);
+    const Sps *sps = &d->sps[pps->sps_id];
+    if (d->prev_nal.ref_idc != nal->ref_idc && (d->prev_nal.ref_idc == 0 || nal->ref_idc == 0)) *boundary = 1;
+    if ((d->prev_nal.type == NAL_IDR) != (nal->type == NAL_IDR)) *boundary = 1;
+    BitReader b = *br;
+    br_ue(&b); br_ue(&b); br_ue(&b);
+    int fn = (int)br_u(&b, sps->log2_max_frame_num);
+    if (b.err) return DEC_FAIL(DEC_ERROR);
+    if (d->aub_prev_frame_num != fn) { d->aub_prev_frame_num = fn; *boundary = 1; }
+    if (nal->type == NAL_IDR) {
+        int id = (int)br_ue(&b);
+        if (d->prev_nal.type == NAL_IDR && d->aub_prev_idr_id != id) *boundary = 1;
+        d->aub_prev_idr_id = id;
+    }
+    if (sps->poc_type == 0) {
+        int lsb = (int)br_u(&b, sps->log2_max_poc_lsb);
+        if (d->aub_prev_poc_lsb != lsb) { d->aub_prev_poc_lsb = lsb; *boundary = 1; }
+        if (pps->bottom_field_poc_present) {
+            int db = br_se(&b);
+            if (d->aub_prev_dpoc_bottom != db) { d->aub_prev_dpoc_bottom = db; *boundary = 1; }
+        }
+    } else if (sps->poc_type == 1 && !sps->delta_pic_order_always_zero) {
+        int d0 = br_se(&b), d1 = pps->bottom_field_poc_present ? br_se(&b) : 0;
+        if (d->aub_prev_dpoc[0] != d0) { d->aub_prev_dpoc[0] = d0; *boundary = 1; }
+        if (d->aub_prev_dpoc[1] != d1) { d->aub_prev_dpoc[1] = d1; *boundary = 1; }
+    }
+    d->prev_nal = *nal;          /* storage.c:774 (nuPrev aliases prevNalUnit) */
+    return b.err ? DEC_FAIL(DEC_ERROR) : 0;
+}
+
+/* ---- parameter-set activation (reference storage.c:298-420) ----------- */
+static int ensure_picbuild(H264Dec *d, const Sps *sps)
+{
+    if (d->pb_ready && d->pb.w == sps->w_mbs && d->pb.h == sps->h_mbs) return 0;
+    if (d->pb_ready) picbuild_free(&d->pb);
+    d->pb_ready = 0;
+    if (picbuild_init(&d->pb, sps->w_mbs, sps->h_mbs)) return -1;
+    d->pb_ready = 1;
+    return 0;
+}
+
+static int activate(H264Dec *d, int pps_id, int is_idr)
+{
+    const Pps *pps = &d->pps[pps_id];
+    if (!pps->valid || !d->sps[pps->sps_id].valid) return DEC_FAIL(DEC_PARAM_SET_ERROR);
+    if (pps->entropy_coding || pps->weighted_pred) return DEC_FAIL(DEC_PARAM_SET_ERROR);
+    if (d->active_pps == -1) {
+        d->active_pps = pps_id;
+        d->active_sps = pps->sps_id;
+        d->pending_activation = 1;
+    } else if (d->pending_activation) {
+        d->pending_activation = 0;
+        const Sps *sps = &d->sps[d->active_sps];
+        if (ensure_picbuild(d, sps)) return DEC_MEMALLOC_ERROR;
+        int no_reorder = d->no_reorder_app || sps->poc_type == 2 ||
+                         (sps->vui_present && sps->bitstream_restriction && !sps->num_reorder_frames);
+        dpb_init(&d->dpb, sps->max_dpb, sps->num_ref_frames, 1 << sps->log2_max_frame_num, no_reorder);
+        d->nslots = d->dpb.npic;
+        d->frame_bytes = (size_t)sps->w_mbs * sps->h_mbs * 384;
+        free(d->out_frames);
+        d->out_frames = (uint8_t *)malloc(d->frame_bytes * (size_t)d->nslots);
+        if (!d->out_frames) return DEC_MEMALLOC_ERROR;
+        if (d->be.configure(d->be.ctx, sps->w_mbs, sps->h_mbs, d->nslots)) return DEC_MEMALLOC_ERROR;
+    } else if (pps_id != d->active_pps) {
+        if (pps->sps_id != d->active_sps) {
+            if (!is_idr) return DEC_FAIL(DEC_PARAM_SET_ERROR);
+            d->active_pps = pps_id;
+            d->active_sps = pps->sps_id;
+            d->pending_activation = 1;
+        } else {
+            d->active_pps = pps_id;
+        }
+    }
+    return 0;
+}
+
+static void store_sps(H264Dec *d, const Sps *s)
+{
+    int id = s->id;
+    if (d->sps[id].valid && id == d->active_sps) {
+        if (!sps_equal(s, &d->sps[id])) {
+            d->active_sps = SPS_FORCE;
+            d->active_pps = PPS_FORCE;
+        } else {
+            return;
+        }
+    }
+    d->sps[id] = *s;
+}
+
+static void store_pps(H264Dec *d, const Pps *p)
+{
+    int id = p->id;
+    if (d->pps[id].valid && id == d->active_pps && p->sps_id != d->active_sps)
+        d->active_pps = PPS_FORCE;
+    d->pps[id] = *p;
+}
+
+/* ---- error concealment of missing MBs (simplified) ------ */
+static int conceal_picture(H264Dec *d, int is_p, const int *ref_slot)
+{
+    PicBuild *pb = &d->pb;
+    int n = 0;
+    for (int i = 0; i < pb->nmbs; i++) {
+        if (pb->pc.mb[i].slice != SLICE_NONE) continue;
+        MbRec *r = &pb->rec[i];
+        memset(r, 0, sizeof(*r));
+        memset(&pb->pc.mb[i], 0, sizeof(MbInfo));
+        pb->pc.mb[i].slice = 0xFFFE;
+        if (is_p && ref_slot && ref_slot[0] >= 0) {
+            r->type = MBT_SKIP;
+            for (int k = 0; k < 4; k++) r->ref[k] = (uint8_t)ref_slot[0];
+        } else {
+            /* mid-grey I_PCM */
+            int16_t *c = NULL;
+            if (pb->ncoef + 12 <= pb->cap) { c = pb->coef + (size_t)pb->ncoef * 16; pb->ncoef += 12; }
+            if (!c) return -1;
+            memset(c, 128, 384);
+            r->type = MBT_IPCM;
+            r->coef = pb->ncoef - 12;
+        }
+        r->slice = 0xFFFE;
+        n++;
+    }
+    return n;
+}
+
+static int finish_picture(H264Dec *d, int concealed_mbs)
+{
+    const Sps *sps = &d->sps[d->active_sps];
+    if (d->be.decode(d->be.ctx, &d->pb, d->cur_slot)) return DEC_FAIL(DEC_ERROR);
+    d->pics_decoded++;
+    d->alg_ref_bytes += d->pb.alg_ref_bytes;
+    d->coded_blocks += d->pb.n_coded_blocks;
+    int poc = decode_poc(d, sps, &d->sh);
+    if (d->valid_slice_in_au) {
+        int is_idr = d->prev_nal.type == NAL_IDR;
+        dpb_mark(&d->dpb, &d->sh, d->prev_nal.ref_idc != 0, d->sh.frame_num, poc, is_idr,
+                 d->cur_pic_id, concealed_mbs);
+    }
+    d->pic_started = 0;
+    d->valid_slice_in_au = 0;
+    return DEC_PIC_RDY;
+}
+
+int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id, uint32_t *read_bytes)
+{
+    const uint8_t *nal;
+    uint32_t nal_len;
+    if (extract_nal(d, buf, len, &nal, &nal_len, read_bytes)) return DEC_FAIL(DEC_ERROR);
+    if (d->prev_buf_not_finished && buf == d->prev_buf_ptr) *read_bytes = d->prev_bytes;
+    d->prev_bytes = *read_bytes;
+    d->prev_buf_ptr = buf;
+    d->prev_buf_not_finished = 0;
+    if (nal_len < 1) return DEC_FAIL(DEC_ERROR);
+    if (nal[0] & 0x80) return DEC_FAIL(DEC_ERROR);
+    NalHdr nh = {(nal[0] >> 5) & 3, nal[0] & 31};
+    if ((nh.type == NAL_IDR && nh.ref_idc == 0) ||
+        ((nh.type == NAL_SPS || nh.type == NAL_PPS) && nh.ref_idc == 0)) return DEC_FAIL(DEC_ERROR);
+    BitReader br;
+    br_init(&br, nal + 1, nal_len - 1);
+    if (nh.type == 0 || nh.type >= 13) return DEC_RDY;
+
+    int boundary = 0;
+    int r = check_au_boundary(d, &nh, &br, &boundary);
+    if (r) return r;
+    if (boundary) {
+        if (d->pic_started && d->active_sps >= 0 && d->active_sps < MAX_SPS) {
+            if (d->pending_activation) return DEC_FAIL(DEC_ERROR);
+            int ref_slot[MAX_REFS];
+            int is_p = 1;
+            if (!d->valid_slice_in_au) {
+                d->cur_slot = dpb_alloc_current(&d->dpb);
+                if (d->cur_slot < 0) return DEC_FAIL(DEC_ERROR);
+                picbuild_reset(&d->pb, 0);
+            } else {
+                is_p = d->sh.slice_type == 0;
+            }
+            SliceHdr tmp = d->sh;
+            tmp.slice_type = 0;
+            tmp.ref_mod_flag = 0;
+            if (tmp.num_ref_idx_active < 1) tmp.num_ref_idx_active = 1;
+            dpb_build_list(&d->dpb, &tmp, ref_slot);
+            int n = conceal_picture(d, is_p, ref_slot);
+            if (n < 0) return DEC_FAIL(DEC_ERROR);
+            d->num_concealed += n;
+            *read_bytes = 0;
+            d->prev_buf_not_finished = 1;
+            return finish_picture(d, d->num_concealed);
+        }
+        d->valid_slice_in_au = 0;
+        d->skip_redundant = 0;
+    }
+
+    switch (nh.type) {
+    case NAL_SPS: {
+        Sps s;
+        if (parse_sps(&br, &s)) return DEC_FAIL(DEC_ERROR);
+        store_sps(d, &s);
+        return DEC_RDY;
+    }
+    case NAL_PPS: {
+        Pps p;
+        if (parse_pps(&br, d->sps, &p)) return DEC_FAIL(DEC_ERROR);
+        store_pps(d, &p);
+        return DEC_RDY;
+    }
+    case NAL_SLICE:
+    case NAL_IDR: {
+        if (d->skip_redundant) return DEC_RDY;
+        d->pic_started = 1;
+        int is_idr = nh.type == NAL_IDR;
+        if (!d->valid_slice_in_au) {
+            d->num_concealed = 0;
+            d->cur_pic_id = (int)pic_id;
+            int pps_id;
+            if (peek_slice_pps_id(&br, &pps_id)) return DEC_FAIL(DEC_ERROR);
+            int old = d->active_sps;
+            int rr = activate(d, pps_id, is_idr);
+            if (rr) {
+                d->active_pps = -1; d->active_sps = -1; d->pending_activation = 0;
+                return rr;
+            }
+            if (old != d->active_sps) {
+                const Sps *nsps = &d->sps[d->active_sps];
+                const Sps *osps = (d->old_sps_id >= 0 && d->old_sps_id < MAX_SPS) ? &d->sps[d->old_sps_id] : NULL;
+                *read_bytes = 0;
+                d->prev_buf_not_finished = 1;
+                int no_out_prior = 1;
+                if (is_idr) {
+                    SliceHdr t;
+                    BitReader b2 = br;
+                    if (!parse_slice_header(&b2, &nh, nsps, &d->pps[d->active_pps], &t)) no_out_prior = t.no_output_prior;
+                }
+                if (no_out_prior || d->dpb.no_reorder || !osps || osps->w_mbs != nsps->w_mbs ||
+                    osps->h_mbs != nsps->h_mbs || osps->max_dpb != nsps->max_dpb)
+                    d->dpb.flushed = 0;
+                else
+                    dpb_flush(&d->dpb);
+                d->old_sps_id = d->active_sps;
+                return DEC_HDRS_RDY;
+            }
+        }
+        if (d->pending_activation) return DEC_FAIL(DEC_ERROR);
+        const Sps *sps = &d->sps[d->active_sps];
+        const Pps *pps = &d->pps[d->active_pps];
+        SliceHdr sh;
+        if (parse_slice_header(&br, &nh, sps, pps, &sh)) return DEC_FAIL(DEC_ERROR);
+        if (sh.pps_id != d->active_pps) {
+            /* a later slice of the picture may name another PPS of the same SPS */
+            if (!d->pps[sh.pps_id].valid || d->pps[sh.pps_id].sps_id != d->active_sps) return DEC_FAIL(DEC_ERROR);
+            pps = &d->pps[sh.pps_id];
+        }
+        if (!d->valid_slice_in_au) {
+            if (!is_idr && dpb_check_gaps(&d->dpb, sh.frame_num, nh.ref_idc != 0, sps->gaps_allowed))
+                return DEC_FAIL(DEC_ERROR);
+            d->cur_slot = dpb_alloc_current(&d->dpb);
+            if (d->cur_slot < 0) return DEC_FAIL(DEC_ERROR);
+            picbuild_reset(&d->pb, pps->cip);
+        }
+        d->sh = sh;
+        d->valid_slice_in_au = 1;
+        d->prev_nal = nh;
+        int ref_slot[MAX_REFS];
+        if (dpb_build_list(&d->dpb, &sh, ref_slot)) return DEC_FAIL(DEC_ERROR);
+        if (sh.slice_type == 0 && ref_slot[0] < 0) return DEC_FAIL(DEC_ERROR);
+        d->pb.pc.cip = pps->cip;
+        if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot, (uint16_t)(sh.first_mb & 0xFFFF))) {
+            /* the reference un-marks the slice and conceals at the next AU
+             * boundary (slice_data.c:302-358); drop the slice's MBs */
+            for (int i = 0; i < d->pb.nmbs; i++)
+                if (d->pb.pc.mb[i].slice == (uint16_t)(sh.first_mb & 0xFFFF)) {
+                    d->pb.pc.mb[i].slice = SLICE_NONE;
+                    d->pb.ndecoded--;
+                }
+            return DEC_FAIL(DEC_ERROR);
+        }
+        if (d->pb.ndecoded == d->pb.nmbs) {
+            d->skip_redundant = 1;
+            return finish_picture(d, d->num_concealed);
+        }
+        return DEC_RDY;
+    }
+    default:
+        return DEC_RDY;
+    }
+}
+
+void h264dec_flush(H264Dec *d)
+{
+    if (d->dpb.npic) dpb_flush(&d->dpb);
+}
+
+const uint8_t *h264dec_next_output(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr, uint32_t *err_mbs)
+{
+    const DpbOut *o = dpb_next_output(&d->dpb);
+    if (!o) return NULL;
+    uint8_t *dst = d->out_frames + d->frame_bytes * (size_t)o->slot;
+    if (d->be.read(d->be.ctx, o->slot, dst)) return NULL;
+    if (pic_id) *pic_id = (uint32_t)o->pic_id;
+    if (is_idr) *is_idr = (uint32_t)o->is_idr;
+    if (err_mbs) *err_mbs = (uint32_t)o->err_mbs;
+    return dst;
+}

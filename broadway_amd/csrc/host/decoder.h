@@ -1,0 +1,94 @@
+/* Host decoder control: one instance per bitstream.  Per NAL unit it does
+ * what the reference's h264bsdDecode (h264bsd_decoder.c:162-560) does --
+ * NAL extraction, parameter-set storage/activation, access-unit boundary
+ * detection, slice header + slice data parse into an MB-record batch, DPB
+ * bookkeeping -- but instead of reconstructing on the CPU it hands each
+ * complete picture to a reconstruction backend (HIP kernels in the product
+ * library; the CPU oracle only in tests). */
+#ifndef H264MI_DECODER_H
+#define H264MI_DECODER_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "syntax.h"
+#include "dpb.h"
+#include "picbuild.h"
+
+/* Reconstruction backend interface (the device boundary). */
+typedef struct H264Backend {
+    void *ctx;
+    /* (re)allocate frame slots for a w x h (MBs) stream with nslots frames */
+    int  (*configure)(void *ctx, int w_mbs, int h_mbs, int nslots);
+    /* reconstruct + deblock the picture described by pb into slot cur_slot
+     * (may run asynchronously; records are consumed before returning) */
+    int  (*decode)(void *ctx, const PicBuild *pb, int cur_slot);
+    /* copy slot as planar I420 (w*16 * h*16 * 3/2 bytes) to host memory */
+    int  (*read)(void *ctx, int slot, uint8_t *dst);
+    /* copy one slot into another (error concealment of lost pictures) */
+    int  (*copy)(void *ctx, int dst_slot, int src_slot);
+    void (*destroy)(void *ctx);
+} H264Backend;
+
+enum {
+    DEC_RDY = 0, DEC_PIC_RDY = 1, DEC_HDRS_RDY = 2, DEC_ERROR = 3,
+    DEC_PARAM_SET_ERROR = 4, DEC_MEMALLOC_ERROR = 5,
+};
+
+typedef struct PocState {
+    int prev_msb, prev_lsb;
+    int prev_frame_num_offset, prev_frame_num;
+    int prev_mmco5;
+} PocState;
+
+typedef struct H264Dec {
+    Sps  sps[MAX_SPS];
+    Pps  pps[MAX_PPS];
+    int  active_sps, active_pps;   /* -1: none; MAX+1: forced re-activation */
+    int  pending_activation;
+    int  old_sps_id;
+    int  no_reorder_app;
+    Dpb  dpb;
+    PicBuild pb;
+    int  pb_ready;
+    H264Backend be;
+    /* picture state */
+    int  pic_started, valid_slice_in_au, skip_redundant;
+    SliceHdr sh;                   /* header of the last decoded slice */
+    NalHdr   prev_nal;
+    int  cur_pic_id;
+    int  cur_slot;
+    int  num_concealed;
+    PocState poc;
+    /* access-unit boundary state (reference storage_t.aub) */
+    int  aub_first_call;
+    int  aub_prev_frame_num, aub_prev_idr_id, aub_prev_poc_lsb, aub_prev_dpoc_bottom;
+    int  aub_prev_dpoc[2];
+    /* re-entry on an unfinished buffer (decoder.c:184-206) */
+    int  prev_buf_not_finished;
+    const uint8_t *prev_buf_ptr;
+    uint32_t prev_bytes;
+    uint8_t *rbsp;
+    size_t   rbsp_cap;
+    int  intra_conceal;
+    /* host-side output frames (one per slot), filled by backend->read */
+    uint8_t *out_frames;
+    size_t   frame_bytes;
+    int      nslots;
+    /* statistics */
+    uint64_t pics_decoded, alg_ref_bytes, coded_blocks;
+} H264Dec;
+
+int  h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be);
+void h264dec_release(H264Dec *d);
+/* decode the next NAL unit found at buf[0..len); *read_bytes = consumed */
+int  h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id,
+                    uint32_t *read_bytes);
+/* flush for end of stream */
+void h264dec_flush(H264Dec *d);
+/* next output picture; returns host pointer to I420 data or NULL */
+const uint8_t *h264dec_next_output(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr,
+                                   uint32_t *err_mbs);
+int  h264dec_valid_param_sets(const H264Dec *d);
+const Sps *h264dec_active_sps(const H264Dec *d);
+
+#endif

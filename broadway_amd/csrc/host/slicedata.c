@@ -1,0 +1,373 @@
+/* slice_data() / macroblock_layer() parsing into MbRec batches (H.264
+ * §7.3.4-7.3.5, semantics §7.4.5).  Replaces the parse half of the
+ * reference: h264bsdDecodeSliceData (slice_data.c:85-235),
+ * h264bsdDecodeMacroblockLayer / DecodeMbPred / DecodeSubMbPred /
+ * DecodeResidual (macroblock_layer.c:133-869) and the host-side metadata of
+ * h264bsdDecodeMacroblock (:964-1134: QP update, I_PCM), MV prediction
+ * (inter_prediction.c:499-1031) and Intra4x4PredMode derivation
+ * (intra_prediction.c:1885-1936). */
+#include "picbuild.h"
+#include "../common/cavlc.h"
+#include "../common/tables.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+int picbuild_init(PicBuild *pb, int w_mbs, int h_mbs)
+{
+    memset(pb, 0, sizeof(*pb));
+    pb->w = w_mbs; pb->h = h_mbs; pb->nmbs = w_mbs * h_mbs;
+    pb->rec = (MbRec *)calloc((size_t)pb->nmbs, sizeof(MbRec));
+    pb->pc.mb = (MbInfo *)calloc((size_t)pb->nmbs, sizeof(MbInfo));
+    pb->cap = (uint32_t)pb->nmbs * 8 + 64;
+    pb->coef = (int16_t *)malloc((size_t)pb->cap * 32);
+    pb->pc.w = w_mbs; pb->pc.h = h_mbs;
+    if (!pb->rec || !pb->pc.mb || !pb->coef) { picbuild_free(pb); return -1; }
+    return 0;
+}
+
+void picbuild_free(PicBuild *pb)
+{
+    free(pb->rec); free(pb->pc.mb); free(pb->coef);
+    pb->rec = NULL; pb->pc.mb = NULL; pb->coef = NULL;
+}
+
+void picbuild_reset(PicBuild *pb, int cip)
+{
+    for (int i = 0; i < pb->nmbs; i++) pb->pc.mb[i].slice = SLICE_NONE;
+    pb->pc.cip = cip;
+    pb->ncoef = 0;
+    pb->ndecoded = 0;
+    pb->nslices = 0;
+    pb->is_p = 0;
+    pb->alg_ref_bytes = 0;
+    pb->n_inter = pb->n_intra = pb->n_coded_blocks = 0;
+}
+
+static int16_t *coef_alloc(PicBuild *pb, uint32_t nblk)
+{
+    if (pb->ncoef + nblk > pb->cap) {
+        uint32_t nc = pb->cap * 2;
+        while (nc < pb->ncoef + nblk) nc *= 2;
+        int16_t *p = (int16_t *)realloc(pb->coef, (size_t)nc * 32);
+        if (!p) return NULL;
+        pb->coef = p;
+        pb->cap = nc;
+    }
+    int16_t *r = pb->coef + (size_t)pb->ncoef * 16;
+    pb->ncoef += nblk;
+    return r;
+}
+
+static int clip3(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* algorithmic reference-fetch bytes of one partition (SURVEY.md §8d R_alg) */
+static uint32_t part_bytes(int w, int h, const int16_t *mv)
+{
+    int fx = mv[0] & 3, fy = mv[1] & 3, cx = mv[0] & 7, cy = mv[1] & 7;
+    uint32_t l = (uint32_t)((w + (fx ? 5 : 0)) * (h + (fy ? 5 : 0)));
+    uint32_t c = (uint32_t)((w / 2 + (cx ? 1 : 0)) * (h / 2 + (cy ? 1 : 0)));
+    return l + 2 * c;
+}
+
+/* fields common to every record: availability, deblocking parameters */
+static void finish_rec(PicBuild *pb, int cur, const SliceHdr *sh, const Pps *pps, uint16_t tag)
+{
+    MbRec *r = &pb->rec[cur];
+    const PicCtx *pc = &pb->pc;
+    uint8_t av = 0;
+    for (int n = 0; n < 4; n++) {
+        int a = mbctx_neighbour(pc, cur, n);
+        if (a >= 0 && !(pc->cip && !mb_is_intra(&pc->mb[a]))) av |= (uint8_t)(1 << n);
+    }
+    if (sh->dbf_idc != 1) {
+        av |= DB_INNER;
+        int col = cur % pb->w;
+        if (col > 0 && (sh->dbf_idc != 2 || pc->mb[cur - 1].slice == tag)) av |= DB_LEFT;
+        if (cur >= pb->w && (sh->dbf_idc != 2 || pc->mb[cur - pb->w].slice == tag)) av |= DB_TOP;
+    }
+    r->avail = av;
+    r->offA = (int8_t)(sh->off_a_div2 * 2);
+    r->offB = (int8_t)(sh->off_b_div2 * 2);
+    r->qpc = kQpChroma[clip3(0, 51, r->qp + pps->chroma_qp_offset)];
+    r->slice = tag;
+    r->dbf = 0;
+    r->rsv0 = 0;
+}
+
+static void decode_skip(PicBuild *pb, int cur, int qp, const int *ref_slot)
+{
+    MbInfo *m = &pb->pc.mb[cur];
+    MbRec *r = &pb->rec[cur];
+    int16_t mv[2];
+    m->type = MBT_SKIP;
+    m->qp = (uint8_t)qp;
+    memset(m->refidx, 0, sizeof(m->refidx));
+    mbctx_mv_skip(&pb->pc, cur, mv);
+    for (int b = 0; b < 16; b++) { m->mv[b][0] = mv[0]; m->mv[b][1] = mv[1]; }
+    memset(r, 0, sizeof(*r));
+    r->type = MBT_SKIP;
+    r->qp = (uint8_t)qp;
+    for (int i = 0; i < 4; i++) r->ref[i] = (uint8_t)ref_slot[0];
+    memcpy(r->mv, m->mv, sizeof(r->mv));
+    r->coef = pb->ncoef;
+    pb->alg_ref_bytes += part_bytes(16, 16, mv);
+    pb->n_inter++;
+}
+
+static int parse_inter_pred(PicBuild *pb, BitReader *br, int cur, int kind, int nref, const int *ref_slot)
+{
+    MbInfo *m = &pb->pc.mb[cur];
+    MbRec *r = &pb->rec[cur];
+    int refs[4] = {0, 0, 0, 0};
+    int mvd[16][2];
+    int nmvd = 0;
+    uint32_t done = 0;
+    if (kind < 3) {
+        int npart = kind == 0 ? 1 : 2;
+        for (int i = 0; i < npart; i++) {
+            if (nref > 1) {
+                uint32_t v = br_te(br, (uint32_t)(nref - 1));
+                if ((int)v >= nref) return -1;
+                refs[i] = (int)v;
+            }
+        }
+        for (int i = 0; i < npart; i++) { mvd[i][0] = br_se(br); mvd[i][1] = br_se(br); }
+        for (int i = 0; i < npart; i++) {
+            int x4 = 0, y4 = 0, w4 = 4, h4 = 4, shape = PSHAPE_NORMAL;
+            if (kind == 1) { y4 = 2 * i; h4 = 2; shape = PSHAPE_16x8; }
+            if (kind == 2) { x4 = 2 * i; w4 = 2; shape = PSHAPE_8x16; }
+            for (int b8 = 0; b8 < 4; b8++) {
+                int bx = (b8 & 1) * 2, by = (b8 >> 1) * 2;
+                if (bx >= x4 && bx < x4 + w4 && by >= y4 && by < y4 + h4) m->refidx[b8] = (int8_t)refs[i];
+            }
+            int16_t mvp[2];
+            mbctx_mvp(&pb->pc, cur, x4, y4, w4, h4, refs[i], shape, i, done, mvp);
+            int16_t mv[2] = {(int16_t)(mvp[0] + mvd[i][0]), (int16_t)(mvp[1] + mvd[i][1])};
+            for (int y = y4; y < y4 + h4; y++)
+                for (int x = x4; x < x4 + w4; x++) {
+                    int b = blk_index(x, y);
+                    m->mv[b][0] = mv[0]; m->mv[b][1] = mv[1];
+                    done |= 1u << b;
+                }
+            pb->alg_ref_bytes += part_bytes(w4 * 4, h4 * 4, mv);
+        }
+    } else {
+        int sub[4];
+        for (int i = 0; i < 4; i++) {
+            uint32_t v = br_ue(br);
+            if (v > 3) return -1;
+            sub[i] = (int)v;
+        }
+        if (kind == 3 && nref > 1)
+            for (int i = 0; i < 4; i++) {
+                uint32_t v = br_te(br, (uint32_t)(nref - 1));
+                if ((int)v >= nref) return -1;
+                refs[i] = (int)v;
+            }
+        for (int i = 0; i < 4; i++) m->refidx[i] = (int8_t)refs[i];
+        static const int nsp[4] = {1, 2, 2, 4};
+        for (int i = 0; i < 4; i++)
+            for (int s = 0; s < nsp[sub[i]]; s++) { mvd[nmvd][0] = br_se(br); mvd[nmvd][1] = br_se(br); nmvd++; }
+        int k = 0;
+        for (int i = 0; i < 4; i++) {
+            int ox = (i & 1) * 2, oy = (i >> 1) * 2;
+            for (int s = 0; s < nsp[sub[i]]; s++, k++) {
+                int x4 = ox, y4 = oy, w4 = 2, h4 = 2;
+                if (sub[i] == 1) { y4 += s; h4 = 1; }
+                if (sub[i] == 2) { x4 += s; w4 = 1; }
+                if (sub[i] == 3) { x4 += s & 1; y4 += s >> 1; w4 = h4 = 1; }
+                int16_t mvp[2];
+                mbctx_mvp(&pb->pc, cur, x4, y4, w4, h4, refs[i], PSHAPE_NORMAL, 0, done, mvp);
+                int16_t mv[2] = {(int16_t)(mvp[0] + mvd[k][0]), (int16_t)(mvp[1] + mvd[k][1])};
+                for (int y = y4; y < y4 + h4; y++)
+                    for (int x = x4; x < x4 + w4; x++) {
+                        int b = blk_index(x, y);
+                        m->mv[b][0] = mv[0]; m->mv[b][1] = mv[1];
+                        done |= 1u << b;
+                    }
+                pb->alg_ref_bytes += part_bytes(w4 * 4, h4 * 4, mv);
+            }
+        }
+    }
+    for (int i = 0; i < 4; i++) {
+        int s = ref_slot[m->refidx[i]];
+        if (s < 0) return -1;                      /* reference picture missing */
+        r->ref[i] = (uint8_t)s;
+    }
+    memcpy(r->mv, m->mv, sizeof(r->mv));
+    return br->err ? -1 : 0;
+}
+
+static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, const Pps *pps,
+                    const int *ref_slot, int *qp)
+{
+    MbInfo *m = &pb->pc.mb[cur];
+    MbRec *r = &pb->rec[cur];
+    int is_p = sh->slice_type == 0;
+    uint32_t mbt = br_ue(br);
+    int inter = 0;
+    memset(r, 0, sizeof(*r));
+    memset(m->refidx, -1, sizeof(m->refidx));
+    if (is_p) {
+        if (mbt < 5) inter = 1; else mbt -= 5;
+    }
+    if (!inter && mbt > 25) return -1;
+
+    if (!inter && mbt == 25) {                       /* I_PCM, §7.3.5 */
+        m->type = MBT_IPCM;
+        while (!br_byte_aligned(br)) if (br_u1(br)) return -1;
+        int16_t *dst = coef_alloc(pb, 12);
+        if (!dst) return -1;
+        uint8_t *d8 = (uint8_t *)dst;
+        for (int i = 0; i < 384; i++) d8[i] = (uint8_t)br_u(br, 8);
+        r->type = MBT_IPCM;
+        r->coef = pb->ncoef - 12;
+        r->cbits = 0;
+        m->qp = 0;                                   /* macroblock_layer.c:1003 */
+        memset(m->tc, 16, sizeof(m->tc));
+        memset(m->tcc, 16, sizeof(m->tcc));
+        r->qp = 0;
+        pb->n_intra++;
+        return br->err ? -1 : 0;
+    }
+
+    int cbp = 0, is_i16 = 0;
+    if (inter) {
+        m->type = MBT_INTER;
+        r->type = MBT_INTER;
+        if (parse_inter_pred(pb, br, cur, (int)mbt, sh->num_ref_idx_active, ref_slot)) return -1;
+        pb->n_inter++;
+    } else if (mbt == 0) {                           /* I_NxN (Intra 4x4) */
+        m->type = MBT_I4x4;
+        r->type = MBT_I4x4;
+        for (int b = 0; b < 16; b++) {
+            int pred = mbctx_pred_i4mode(&pb->pc, cur, b);
+            int mode;
+            if (br_u1(br)) mode = pred;
+            else {
+                int rem = (int)br_u(br, 3);
+                mode = rem < pred ? rem : rem + 1;
+            }
+            m->i4mode[b] = (int8_t)mode;
+            r->i4[b >> 1] |= (uint8_t)(mode << ((b & 1) * 4));
+        }
+        uint32_t cm = br_ue(br);
+        if (cm > 3) return -1;
+        r->pred = (uint8_t)(cm << 4);
+        pb->n_intra++;
+    } else {                                          /* I_16x16 */
+        m->type = MBT_I16;
+        r->type = MBT_I16;
+        is_i16 = 1;
+        int t = (int)mbt - 1;
+        cbp = ((t / 4) % 3) << 4 | (mbt >= 13 ? 15 : 0);
+        uint32_t cm = br_ue(br);
+        if (cm > 3) return -1;
+        r->pred = (uint8_t)((t % 4) | (cm << 4));
+        pb->n_intra++;
+    }
+    if (!is_i16) {
+        uint32_t code = br_ue(br);
+        if (code > 47) return -1;
+        cbp = inter ? kCbpInter[code] : kCbpIntra[code];
+    }
+    if (cbp || is_i16) {
+        int d = br_se(br);
+        if (d < -26 || d > 25) return -1;
+        *qp = (*qp + d + 52) % 52;
+    }
+    m->qp = (uint8_t)*qp;
+    r->qp = (uint8_t)*qp;
+
+    /* residual(), §7.3.5.3 */
+    int16_t blk[27][16];
+    uint32_t cbits = 0;
+    if (is_i16) {
+        int tc = cavlc_decode_block(br, mbctx_nc_luma(&pb->pc, cur, 0), 16, blk[24]);
+        if (tc < 0) return -1;
+        if (tc) cbits |= 1u << 24;
+    }
+    for (int b = 0; b < 16; b++) {
+        if (cbp & (1 << (b >> 2))) {
+            int nc = mbctx_nc_luma(&pb->pc, cur, b);
+            int tc;
+            if (is_i16) { blk[b][0] = 0; tc = cavlc_decode_block(br, nc, 15, blk[b] + 1); }
+            else tc = cavlc_decode_block(br, nc, 16, blk[b]);
+            if (tc < 0) return -1;
+            m->tc[b] = (uint8_t)tc;
+            if (tc) cbits |= 1u << b;
+        } else {
+            m->tc[b] = 0;
+        }
+    }
+    int cc = cbp >> 4;
+    if (cc) {
+        for (int comp = 0; comp < 2; comp++) {
+            int tc = cavlc_decode_block(br, -1, 4, blk[25 + comp]);
+            if (tc < 0) return -1;
+            if (tc) cbits |= 1u << (25 + comp);
+        }
+    }
+    for (int comp = 0; comp < 2; comp++)
+        for (int b = 0; b < 4; b++) {
+            int idx = 16 + comp * 4 + b;
+            if (cc & 2) {
+                blk[idx][0] = 0;
+                int tc = cavlc_decode_block(br, mbctx_nc_chroma(&pb->pc, cur, comp, b), 15, blk[idx] + 1);
+                if (tc < 0) return -1;
+                m->tcc[comp * 4 + b] = (uint8_t)tc;
+                if (tc) cbits |= 1u << idx;
+            } else {
+                m->tcc[comp * 4 + b] = 0;
+            }
+        }
+    int nblk = __builtin_popcount(cbits);
+    int16_t *dst = coef_alloc(pb, (uint32_t)nblk);
+    if (!dst) return -1;
+    r->coef = pb->ncoef - (uint32_t)nblk;
+    r->cbits = cbits;
+    for (int bit = 0; bit < 27; bit++)
+        if (cbits & (1u << bit)) { memcpy(dst, blk[bit], 32); dst += 16; }
+    pb->n_coded_blocks += (uint32_t)nblk;
+    return br->err ? -1 : 0;
+}
+
+int parse_slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps *pps,
+                     const int *ref_slot, uint16_t tag)
+{
+    int cur = sh->first_mb;
+    int qp = sh->slice_qp;
+    int is_p = sh->slice_type == 0;
+    int more = 1;
+    if (is_p) pb->is_p = 1;
+    pb->nslices++;
+    while (more) {
+        if (is_p) {
+            uint32_t run = br_ue(br);
+            if (br->err || run > (uint32_t)(pb->nmbs - cur)) return -1;
+            for (uint32_t i = 0; i < run; i++, cur++) {
+                if (pb->pc.mb[cur].slice != SLICE_NONE) return -1;
+                memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
+                pb->pc.mb[cur].slice = tag;
+                decode_skip(pb, cur, qp, ref_slot);
+                finish_rec(pb, cur, sh, pps, tag);
+                pb->ndecoded++;
+            }
+            if (run > 0) {
+                more = br_more_rbsp_data(br);
+                if (!more) break;
+            }
+        }
+        if (cur >= pb->nmbs) return -1;
+        if (pb->pc.mb[cur].slice != SLICE_NONE) return -1;
+        memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
+        pb->pc.mb[cur].slice = tag;
+        if (parse_mb(pb, br, cur, sh, pps, ref_slot, &qp)) return -1;
+        finish_rec(pb, cur, sh, pps, tag);
+        pb->ndecoded++;
+        cur++;
+        more = br_more_rbsp_data(br);
+    }
+    return br->err ? -1 : 0;
+}
