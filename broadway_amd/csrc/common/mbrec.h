@@ -1,84 +1,5 @@
-/* Packed per-macroblock reconstruction record: the host->device data contract.
- *
- * One MbRec per macroblock, 96 bytes, produced by the host parser (CAVLC +
- * MB-layer parse, MV prediction, intra-mode derivation) and consumed by the
- * HIP reconstruction kernels and by the CPU oracle.  It is the device-side
- * restatement of what the reference keeps in mbStorage_t / macroblockLayer_t
- * (h264bsd_macroblock_layer.h:141-188) after h264bsdDecodeMacroblockLayer and
- * the MV/mode derivation have run:
- *   - mv[16]        <- mbStorage_t.mv[16] (z-scan order, quarter-pel)
- *   - ref[4]        <- mbStorage_t.refAddr[4] as a DPB *slot* index
- *   - i4[8]         <- mbStorage_t.intra4x4PredMode[16] (4 bits each)
- *   - cbits/coef    <- residual_t.level/totalCoeff: only coded blocks travel,
- *                      each as 16 int16 levels in scan order
- *   - qp            <- mbStorage_t.qpY (0 for I_PCM, macroblock_layer.c:1003)
- *   - dbf/offA/offB <- mbStorage_t.disableDeblockingFilterIdc/filterOffsetA/B
- *   - slice         <- mbStorage_t.sliceId
- *
- * Coefficient blocks (int16[16] each) referenced by a record are stored
- * contiguously starting at block index `coef`, one block per set bit of
- * `cbits` in increasing bit order:
- *   bits  0..15  luma 4x4 blocks (z-scan); for I16x16 these are AC blocks
- *                (scan position 0 unused); a bit is set iff TotalCoeff > 0
- *   bits 16..19  Cb AC 4x4 blocks, bits 20..23 Cr AC (scan pos 0 unused)
- *   bit  24      I16x16 luma DC (16 levels, scan order)
- *   bit  25      Cb DC (levels 0..3), bit 26 Cr DC (levels 0..3)
- * I_PCM: cbits = 0 and 12 blocks at `coef` hold the 384 raw samples
- * (256 luma raster, 64 Cb, 64 Cr) as bytes.
- */
-#ifndef H264MI_MBREC_H
-#define H264MI_MBREC_H
-
-#include <stdint.h>
-
-enum {
-    MBT_INTER = 0,      /* P_L0_* and P_8x8 (any partitioning) */
-    MBT_SKIP  = 1,      /* P_Skip */
-    MBT_I4x4  = 2,
-    MBT_I16   = 3,
-    MBT_IPCM  = 4,
-};
-
-/* avail bits: intra-prediction availability of neighbour MBs (slice +
- * constrained_intra_pred applied, h264bsdIsNeighbourAvailable +
- * intra_prediction.c:643-654) */
-enum {
-    AV_A = 1, AV_B = 2, AV_C = 4, AV_D = 8,
-    /* deblocking: filterLeftMbEdgeFlag / filterTopMbEdgeFlag
-     * (deblocking.c:288-319) */
-    DB_LEFT = 16, DB_TOP = 32, DB_INNER = 64,
-};
-
-typedef struct MbRec {
-    uint8_t  type;      /* MBT_* */
-    uint8_t  qp;        /* QPY (I_PCM: 0) */
-    uint8_t  qpc;       /* QPc = QpChroma[clip3(0,51,QPY+chroma_qp_index_offset)] */
-    uint8_t  avail;     /* AV_* | DB_* */
-    uint8_t  pred;      /* I16: mode (bits 0-1); chroma mode bits 4-5 */
-    uint8_t  dbf;       /* unused (reserved) */
-    int8_t   offA;      /* FilterOffsetA = slice_alpha_c0_offset_div2 << 1 */
-    int8_t   offB;      /* FilterOffsetB */
-    uint32_t cbits;     /* coded-block mask, see above */
-    uint32_t coef;      /* first coefficient block index */
-    uint8_t  i4[8];     /* Intra4x4PredMode, 4 bits per block, z-scan */
-    uint8_t  ref[4];    /* DPB slot per 8x8 partition (inter only) */
-    int16_t  mv[16][2]; /* per 4x4 block, z-scan, quarter-pel (x, y) */
-    uint16_t slice;     /* slice id within the picture */
-    uint16_t rsv0;
-} MbRec;
-
-#ifdef __cplusplus
-static_assert(sizeof(MbRec) == 96, "MbRec must stay 96 bytes");
-#else
-_Static_assert(sizeof(MbRec) == 96, "MbRec must stay 96 bytes");
-#endif
-
-/* Per-picture descriptor, one per picture in a launch batch */
-typedef struct PicDesc {
-    uint32_t rec_base;      /* first MbRec index of this picture in the batch */
-    uint32_t frame_base;    /* index of this stream's slot 0 in the frame pool */
-    uint32_t cur_slot;      /* slot being reconstructed */
-    uint32_t flags;         /* bit0: P picture (has inter MBs) */
-} PicDesc;
-
+/* The MB-record format is part of the public C-ABI: include/h264mi_records.h */
+#ifndef H264MI_MBREC_INDIRECT_H
+#define H264MI_MBREC_INDIRECT_H
+#include "../../../include/h264mi_records.h"
 #endif

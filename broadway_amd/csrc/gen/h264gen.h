@@ -50,6 +50,8 @@ void h264gen_default_params(GenParams *p, int w_mbs, int h_mbs);
 int  h264gen_preset(GenParams *p, int config, uint64_t seed);
 /* generate a stream; *out is malloc'ed, caller frees with h264gen_free */
 int  h264gen_generate(const GenParams *p, uint8_t **out, size_t *out_len);
+/* CAVLC encode/decode round trip self-test; returns mismatches */
+int  h264gen_cavlc_selftest(int iters, uint64_t seed);
 void h264gen_free(void *ptr);
 
 #ifdef __cplusplus

@@ -1,0 +1,319 @@
+// h264mi engine: HBM-resident frame slots, record upload, kernel launches.
+// One engine serves `nstreams` independent bitstreams of one picture size
+// (streams shard across GPUs with no collective; within a GPU
+// one launch reconstructs one picture from each stream of the batch).
+#include "recon_kernels.hip"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../../../include/h264mi.h"
+
+#define HIPCHECK(x)                                                                    \
+    do {                                                                               \
+        hipError_t err_ = (x);                                                         \
+        if (err_ != hipSuccess) {                                                      \
+            fprintf(stderr, "h264mi: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(err_), \
+                    __FILE__, __LINE__);                                               \
+            return -1;                                                                 \
+        }                                                                              \
+    } while (0)
+
+struct h264mi_engine {
+    int dev;
+    int w, h, nmbs, nstreams, nslots;
+    size_t frame_bytes;
+    uint8_t *d_frames;
+    uint8_t *d_edges;
+    MbRec *d_rec;
+    int16_t *d_coef;
+    size_t coef_cap;          // blocks
+    PicDesc *d_pics;
+    unsigned *d_err;
+    MbRec *h_rec;             // pinned staging
+    int16_t *h_coef;
+    size_t h_coef_cap;
+    PicDesc *h_pics;
+    unsigned *h_err;
+    hipStream_t st;
+    hipEvent_t ev_staged, ev0, ev1, ev2;
+    int ndiag, diag_len;
+    uint32_t err_accum;
+    int timing;
+};
+
+static int diag_geometry(int w, int h, int *ndiag, int *len)
+{
+    *ndiag = w + 2 * (h - 1);
+    int mx = 0;
+    for (int t = 0; t < *ndiag; t++) {
+        int lo = t - (w - 1) + 1;
+        lo = lo > 0 ? lo >> 1 : 0;
+        int hi = t / 2 < h - 1 ? t / 2 : h - 1;
+        int n = hi - lo + 1;
+        if (n > mx) mx = n;
+    }
+    *len = mx;
+    return 0;
+}
+
+extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
+{
+    if (w_mbs < 1 || h_mbs < 1 || nstreams < 1 || nslots < 1) return NULL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
+        fprintf(stderr, "h264mi: no HIP device %d (count %d)\n", device, ndev);
+        return NULL;
+    }
+    if (hipSetDevice(device) != hipSuccess) return NULL;
+    h264mi_engine *e = (h264mi_engine *)calloc(1, sizeof(h264mi_engine));
+    if (!e) return NULL;
+    e->dev = device;
+    e->w = w_mbs; e->h = h_mbs; e->nmbs = w_mbs * h_mbs;
+    e->nstreams = nstreams; e->nslots = nslots;
+    e->frame_bytes = (size_t)e->nmbs * 384;
+    diag_geometry(w_mbs, h_mbs, &e->ndiag, &e->diag_len);
+    e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
+    e->h_coef_cap = e->coef_cap;
+    e->timing = getenv("H264MI_TIMING") != NULL;
+    bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
+              hipMalloc(&e->d_edges, (size_t)nstreams * e->nmbs * 64) == hipSuccess &&
+              hipMalloc(&e->d_rec, sizeof(MbRec) * nstreams * e->nmbs) == hipSuccess &&
+              hipMalloc(&e->d_coef, e->coef_cap * 32) == hipSuccess &&
+              hipMalloc(&e->d_pics, sizeof(PicDesc) * nstreams) == hipSuccess &&
+              hipMalloc(&e->d_err, sizeof(unsigned) * nstreams) == hipSuccess &&
+              hipHostMalloc(&e->h_rec, sizeof(MbRec) * nstreams * e->nmbs, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&e->h_coef, e->h_coef_cap * 32, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&e->h_pics, sizeof(PicDesc) * nstreams, hipHostMallocDefault) == hipSuccess &&
+              hipHostMalloc(&e->h_err, sizeof(unsigned) * nstreams, hipHostMallocDefault) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess &&
+              hipEventCreate(&e->ev2) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "h264mi: engine allocation failed\n");
+        h264mi_engine_destroy(e);
+        return NULL;
+    }
+    (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * nslots * nstreams, e->st);
+    (void)hipMemsetAsync(e->d_edges, 0, (size_t)nstreams * e->nmbs * 64, e->st);
+    (void)hipEventRecord(e->ev_staged, e->st);
+    (void)hipStreamSynchronize(e->st);
+    return e;
+}
+
+extern "C" void h264mi_engine_destroy(h264mi_engine *e)
+{
+    if (!e) return;
+    if (e->st) (void)hipStreamSynchronize(e->st);
+    (void)hipFree(e->d_frames); (void)hipFree(e->d_edges); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
+    (void)hipFree(e->d_pics); (void)hipFree(e->d_err);
+    (void)hipHostFree(e->h_rec); (void)hipHostFree(e->h_coef); (void)hipHostFree(e->h_pics); (void)hipHostFree(e->h_err);
+    if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->ev2) (void)hipEventDestroy(e->ev2);
+    if (e->st) (void)hipStreamDestroy(e->st);
+    free(e);
+}
+
+static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
+                        const PicDesc *d_pics)
+{
+    ReconArgs a;
+    a.frames = e->d_frames;
+    a.frame_bytes = e->frame_bytes;
+    a.rec = d_rec;
+    a.coef = d_coef;
+    a.edges = e->d_edges;
+    a.pics = d_pics;
+    a.npics = npics;
+    a.w = e->w; a.h = e->h;
+    a.diag = 0;
+    a.diag_len = e->diag_len;
+    a.err = e->d_err;
+    HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * npics, e->st));
+    if (e->timing) (void)hipEventRecord(e->ev0, e->st);
+    hipLaunchKernelGGL(k_inter, dim3(npics * e->nmbs), dim3(64), 0, e->st, a);
+    HIPCHECK(hipGetLastError());
+    if (e->timing) (void)hipEventRecord(e->ev1, e->st);
+    for (int t = 0; t < e->ndiag; t++) {
+        a.diag = t;
+        hipLaunchKernelGGL(k_wave, dim3(npics * e->diag_len), dim3(64), 0, e->st, a);
+    }
+    HIPCHECK(hipGetLastError());
+    if (e->timing) (void)hipEventRecord(e->ev2, e->st);
+    HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
+    return 0;
+}
+
+extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
+                                    const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef)
+{
+    if (!e || npics < 1 || npics > e->nstreams) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    // staging buffers are reused: wait until the previous upload consumed them
+    HIPCHECK(hipEventSynchronize(e->ev_staged));
+    for (int i = 0; i < npics; i++) e->err_accum += 0;
+    size_t total = 0;
+    for (int i = 0; i < npics; i++) total += ncoef[i];
+    if (total + 16 > e->coef_cap) {
+        HIPCHECK(hipStreamSynchronize(e->st));
+        (void)hipFree(e->d_coef);
+        (void)hipHostFree(e->h_coef);
+        e->coef_cap = e->h_coef_cap = total + total / 2 + 1024;
+        HIPCHECK(hipMalloc(&e->d_coef, e->coef_cap * 32));
+        HIPCHECK(hipHostMalloc(&e->h_coef, e->h_coef_cap * 32, hipHostMallocDefault));
+    }
+    size_t cbase = 0;
+    for (int i = 0; i < npics; i++) {
+        if (stream[i] < 0 || stream[i] >= e->nstreams || cur_slot[i] < 0 || cur_slot[i] >= e->nslots) return -1;
+        memcpy(e->h_rec + (size_t)i * e->nmbs, recs[i], sizeof(MbRec) * e->nmbs);
+        if (ncoef[i]) memcpy(e->h_coef + cbase * 16, coefs[i], (size_t)ncoef[i] * 32);
+        PicDesc &pd = e->h_pics[i];
+        pd.rec_base = (uint32_t)(i * e->nmbs);
+        pd.frame_base = (uint32_t)(stream[i] * e->nslots);
+        pd.cur_slot = (uint32_t)cur_slot[i];
+        pd.flags = 0;
+        pd.coef_base = (uint32_t)cbase;
+        pd.rsv[0] = pd.rsv[1] = pd.rsv[2] = 0;
+        cbase += ncoef[i];
+    }
+    HIPCHECK(hipMemcpyAsync(e->d_rec, e->h_rec, sizeof(MbRec) * e->nmbs * npics, hipMemcpyHostToDevice, e->st));
+    if (cbase) HIPCHECK(hipMemcpyAsync(e->d_coef, e->h_coef, cbase * 32, hipMemcpyHostToDevice, e->st));
+    HIPCHECK(hipMemcpyAsync(e->d_pics, e->h_pics, sizeof(PicDesc) * npics, hipMemcpyHostToDevice, e->st));
+    HIPCHECK(hipEventRecord(e->ev_staged, e->st));
+    return launch_batch(e, npics, e->d_rec, e->d_coef, e->d_pics);
+}
+
+extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
+                                           const void *d_pics)
+{
+    if (!e || npics < 1 || npics > e->nstreams) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics);
+}
+
+extern "C" int h264mi_engine_sync(h264mi_engine *e)
+{
+    if (!e) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    HIPCHECK(hipStreamSynchronize(e->st));
+    for (int i = 0; i < e->nstreams; i++) e->err_accum += e->h_err[i] ? 1 : 0;
+    memset(e->h_err, 0, sizeof(unsigned) * e->nstreams);
+    return 0;
+}
+
+extern "C" uint32_t h264mi_engine_errors(h264mi_engine *e)
+{
+    if (!e) return 0;
+    uint32_t v = e->err_accum;
+    e->err_accum = 0;
+    return v;
+}
+
+extern "C" int h264mi_engine_last_timing(h264mi_engine *e, float *us2)
+{
+    if (!e || !e->timing) return -1;
+    float ms0 = 0, ms1 = 0;
+    HIPCHECK(hipEventSynchronize(e->ev2));
+    HIPCHECK(hipEventElapsedTime(&ms0, e->ev0, e->ev1));
+    HIPCHECK(hipEventElapsedTime(&ms1, e->ev1, e->ev2));
+    us2[0] = ms0 * 1000.f;
+    us2[1] = ms1 * 1000.f;
+    return 0;
+}
+
+extern "C" int h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst)
+{
+    if (!e || stream < 0 || stream >= e->nstreams || slot < 0 || slot >= e->nslots) return -1;
+    if (h264mi_engine_sync(e)) return -1;
+    HIPCHECK(hipMemcpy(dst, e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot), e->frame_bytes,
+                       hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot)
+{
+    if (!e) return NULL;
+    return e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot);
+}
+
+extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? e->frame_bytes : 0; }
+
+extern "C" void *h264mi_device_alloc(size_t bytes)
+{
+    void *p = NULL;
+    if (hipMalloc(&p, bytes) != hipSuccess) return NULL;
+    return p;
+}
+
+extern "C" int h264mi_device_free(void *p) { return hipFree(p) == hipSuccess ? 0 : -1; }
+
+extern "C" int h264mi_copy_h2d(void *dst, const void *src, size_t bytes)
+{
+    return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
+// -------- H264Backend adapter for the single-stream host decoder ----------
+#include "../host/decoder.h"
+
+struct HipBackendCtx {
+    int device;
+    h264mi_engine *e;
+};
+
+static int hb_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    if (c->e) h264mi_engine_destroy(c->e);
+    c->e = h264mi_engine_create(c->device, w_mbs, h_mbs, 1, nslots);
+    return c->e ? 0 : -1;
+}
+
+static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    int stream = 0;
+    const void *recs[1] = {pb->rec};
+    const int16_t *coefs[1] = {pb->coef};
+    uint32_t nc[1] = {pb->ncoef};
+    return h264mi_engine_decode(c->e, 1, &stream, &cur_slot, recs, coefs, nc);
+}
+
+static int hb_read(void *vctx, int slot, uint8_t *dst)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    return h264mi_engine_read(c->e, 0, slot, dst);
+}
+
+static int hb_copy(void *vctx, int dst, int src)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    if (h264mi_engine_sync(c->e)) return -1;
+    HIPCHECK(hipMemcpy(h264mi_engine_frame_ptr(c->e, 0, dst), h264mi_engine_frame_ptr(c->e, 0, src),
+                       h264mi_engine_frame_bytes(c->e), hipMemcpyDeviceToDevice));
+    return 0;
+}
+
+static void hb_destroy(void *vctx)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    if (c->e) h264mi_engine_destroy(c->e);
+    free(c);
+}
+
+extern "C" H264Backend h264mi_hip_backend_create(int device)
+{
+    H264Backend be;
+    memset(&be, 0, sizeof(be));
+    HipBackendCtx *c = (HipBackendCtx *)calloc(1, sizeof(HipBackendCtx));
+    c->device = device;
+    be.ctx = c;
+    be.configure = hb_configure;
+    be.decode = hb_decode;
+    be.read = hb_read;
+    be.copy = hb_copy;
+    be.destroy = hb_destroy;
+    return be;
+}

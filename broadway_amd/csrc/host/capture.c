@@ -1,0 +1,164 @@
+/* MB-record capture: run the host parser over a whole stream and keep every
+ * picture's MB-record batch (records, coefficient blocks, target slot) in
+ * host memory instead of reconstructing it.  This is the "pre-parsed record
+ * batch" producer of SURVEY.md §8d (kernel-only timing uploads these to HBM
+ * once) and the record source for kernel-level parity tests. */
+#include "../../../include/h264mi.h"
+#include "decoder.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct CapPic {
+    size_t   rec_off;
+    size_t   coef_off;       /* in 16-coefficient blocks */
+    uint32_t ncoef;
+    int      cur_slot;
+    uint64_t alg_ref_bytes;
+    uint32_t n_inter, n_intra, n_coded;
+} CapPic;
+
+struct h264mi_capture {
+    int w, h, nslots;
+    MbRec *recs;
+    size_t nrec, rec_cap;
+    int16_t *coefs;
+    size_t ncoef, coef_cap;
+    CapPic *pics;
+    int npics, pic_cap;
+    int errors;
+    int reconfigured;
+};
+
+static int cap_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
+{
+    struct h264mi_capture *c = (struct h264mi_capture *)vctx;
+    if (c->w && (c->w != w_mbs || c->h != h_mbs)) c->reconfigured = 1;
+    c->w = w_mbs; c->h = h_mbs;
+    if (nslots > c->nslots) c->nslots = nslots;
+    return 0;
+}
+
+static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
+{
+    struct h264mi_capture *c = (struct h264mi_capture *)vctx;
+    if (c->npics == c->pic_cap) {
+        c->pic_cap = c->pic_cap ? c->pic_cap * 2 : 64;
+        CapPic *np = (CapPic *)realloc(c->pics, sizeof(CapPic) * (size_t)c->pic_cap);
+        if (!np) return -1;
+        c->pics = np;
+    }
+    size_t nmbs = (size_t)pb->nmbs;
+    if (c->nrec + nmbs > c->rec_cap) {
+        size_t nc = c->rec_cap ? c->rec_cap * 2 : nmbs * 16;
+        while (nc < c->nrec + nmbs) nc *= 2;
+        MbRec *nr = (MbRec *)realloc(c->recs, sizeof(MbRec) * nc);
+        if (!nr) return -1;
+        c->recs = nr;
+        c->rec_cap = nc;
+    }
+    if (c->ncoef + pb->ncoef > c->coef_cap) {
+        size_t nc = c->coef_cap ? c->coef_cap * 2 : (size_t)pb->ncoef * 16 + 1024;
+        while (nc < c->ncoef + pb->ncoef) nc *= 2;
+        int16_t *ncf = (int16_t *)realloc(c->coefs, nc * 32);
+        if (!ncf) return -1;
+        c->coefs = ncf;
+        c->coef_cap = nc;
+    }
+    CapPic *p = &c->pics[c->npics++];
+    p->rec_off = c->nrec;
+    p->coef_off = c->ncoef;
+    p->ncoef = pb->ncoef;
+    p->cur_slot = cur_slot;
+    p->alg_ref_bytes = pb->alg_ref_bytes;
+    p->n_inter = pb->n_inter;
+    p->n_intra = pb->n_intra;
+    p->n_coded = pb->n_coded_blocks;
+    memcpy(c->recs + c->nrec, pb->rec, sizeof(MbRec) * nmbs);
+    if (pb->ncoef) memcpy(c->coefs + c->ncoef * 16, pb->coef, (size_t)pb->ncoef * 32);
+    c->nrec += nmbs;
+    c->ncoef += pb->ncoef;
+    return 0;
+}
+
+static int cap_read(void *vctx, int slot, uint8_t *dst)
+{
+    struct h264mi_capture *c = (struct h264mi_capture *)vctx;
+    (void)slot;
+    memset(dst, 0, (size_t)c->w * c->h * 384);
+    return 0;
+}
+
+static int cap_copy(void *vctx, int dst, int src) { (void)vctx; (void)dst; (void)src; return 0; }
+static void cap_destroy(void *vctx) { (void)vctx; }
+
+h264mi_capture *h264mi_capture_stream(const uint8_t *buf, size_t len, int no_reorder)
+{
+    h264mi_capture *c = (h264mi_capture *)calloc(1, sizeof(*c));
+    H264Dec *d = (H264Dec *)calloc(1, sizeof(H264Dec));
+    if (!c || !d) { free(c); free(d); return NULL; }
+    H264Backend be;
+    memset(&be, 0, sizeof(be));
+    be.ctx = c;
+    be.configure = cap_configure;
+    be.decode = cap_decode;
+    be.read = cap_read;
+    be.copy = cap_copy;
+    be.destroy = cap_destroy;
+    h264dec_init(d, no_reorder, be);
+    const uint8_t *p = buf;
+    uint32_t left = (uint32_t)len, pic_id = 0;
+    while (left > 0) {
+        uint32_t rb = 0;
+        int r = h264dec_decode(d, p, left, pic_id, &rb);
+        if (r == DEC_PIC_RDY) pic_id++;
+        if (r == DEC_ERROR || r == DEC_PARAM_SET_ERROR) c->errors++;
+        if (r == DEC_PIC_RDY || r == DEC_HDRS_RDY)
+            while (h264dec_next_output(d, NULL, NULL, NULL)) {}
+        if (rb > left) rb = left;
+        p += rb;
+        left -= rb;
+    }
+    h264dec_release(d);
+    free(d);
+    return c;
+}
+
+int h264mi_capture_info(const h264mi_capture *c, int *w_mbs, int *h_mbs, int *nslots, int *npics, int *errors)
+{
+    if (!c) return -1;
+    if (w_mbs) *w_mbs = c->w;
+    if (h_mbs) *h_mbs = c->h;
+    if (nslots) *nslots = c->nslots;
+    if (npics) *npics = c->npics;
+    if (errors) *errors = c->errors + (c->reconfigured ? 1 : 0);
+    return 0;
+}
+
+int h264mi_capture_picture(const h264mi_capture *c, int i, const void **rec, const int16_t **coef,
+                           uint32_t *ncoef, int *cur_slot, uint64_t *alg_ref_bytes)
+{
+    if (!c || i < 0 || i >= c->npics) return -1;
+    const CapPic *p = &c->pics[i];
+    if (rec) *rec = c->recs + p->rec_off;
+    if (coef) *coef = c->coefs + p->coef_off * 16;
+    if (ncoef) *ncoef = p->ncoef;
+    if (cur_slot) *cur_slot = p->cur_slot;
+    if (alg_ref_bytes) *alg_ref_bytes = p->alg_ref_bytes;
+    return 0;
+}
+
+int h264mi_capture_stats(const h264mi_capture *c, int i, uint32_t *n_inter, uint32_t *n_intra, uint32_t *n_coded)
+{
+    if (!c || i < 0 || i >= c->npics) return -1;
+    const CapPic *p = &c->pics[i];
+    *n_inter = p->n_inter; *n_intra = p->n_intra; *n_coded = p->n_coded;
+    return 0;
+}
+
+void h264mi_capture_free(h264mi_capture *c)
+{
+    if (!c) return;
+    free(c->recs); free(c->coefs); free(c->pics);
+    free(c);
+}

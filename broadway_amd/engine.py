@@ -1,0 +1,129 @@
+"""Batched multi-stream reconstruction on one MI355X (the throughput path).
+
+``Capture`` runs the product host parser over a whole stream and keeps each
+picture's MB-record batch (include/h264mi_records.h).  ``Engine`` owns the
+HBM frame slots of S streams and reconstructs one picture of each stream per
+launch sequence (k_inter + one k_wave per MB anti-diagonal).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Sequence
+
+import numpy as np
+
+from . import _lib
+
+MBREC_BYTES = 96
+PICDESC_BYTES = 32
+
+
+@dataclass
+class CapturedPicture:
+    rec: int            # host address of w*h MbRec
+    coef: int           # host address of ncoef coefficient blocks
+    ncoef: int
+    cur_slot: int
+    alg_ref_bytes: int
+    n_inter: int
+    n_intra: int
+    n_coded: int
+
+
+class Capture:
+    def __init__(self, stream: bytes, no_reorder: bool = False):
+        self._L = _lib.mi()
+        self._buf = C.create_string_buffer(stream, len(stream))
+        self._h = self._L.h264mi_capture_stream(C.cast(self._buf, C.c_void_p), len(stream), int(no_reorder))
+        if not self._h:
+            raise RuntimeError("capture failed")
+        w, h, ns, npics, err = (C.c_int() for _ in range(5))
+        self._L.h264mi_capture_info(self._h, C.byref(w), C.byref(h), C.byref(ns), C.byref(npics), C.byref(err))
+        self.w_mbs, self.h_mbs, self.nslots = w.value, h.value, ns.value
+        self.npics, self.errors = npics.value, err.value
+        self.pictures: List[CapturedPicture] = [self._picture(i) for i in range(self.npics)]
+
+    def _picture(self, i: int) -> CapturedPicture:
+        rec, coef = C.c_void_p(), C.c_void_p()
+        nc, slot = C.c_uint32(), C.c_int()
+        alg = C.c_uint64()
+        self._L.h264mi_capture_picture(self._h, i, C.byref(rec), C.byref(coef), C.byref(nc), C.byref(slot),
+                                       C.byref(alg))
+        a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
+        self._L.h264mi_capture_stats(self._h, i, C.byref(a), C.byref(b), C.byref(c))
+        return CapturedPicture(rec.value or 0, coef.value or 0, nc.value, slot.value, alg.value,
+                               a.value, b.value, c.value)
+
+    def records_bytes(self, i: int) -> bytes:
+        p = self.pictures[i]
+        return C.string_at(p.rec, self.w_mbs * self.h_mbs * MBREC_BYTES)
+
+    def coef_bytes(self, i: int) -> bytes:
+        p = self.pictures[i]
+        return C.string_at(p.coef, p.ncoef * 32) if p.ncoef else b""
+
+    def close(self):
+        if self._h:
+            self._L.h264mi_capture_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Engine:
+    def __init__(self, w_mbs: int, h_mbs: int, nstreams: int, nslots: int, device: int = 0):
+        self._L = _lib.mi()
+        self.w_mbs, self.h_mbs, self.nstreams, self.nslots = w_mbs, h_mbs, nstreams, nslots
+        self._h = self._L.h264mi_engine_create(device, w_mbs, h_mbs, nstreams, nslots)
+        if not self._h:
+            raise RuntimeError("h264mi_engine_create failed (no HIP device?)")
+        self.frame_bytes = self._L.h264mi_engine_frame_bytes(self._h)
+
+    def decode(self, streams: Sequence[int], pics: Sequence[CapturedPicture]) -> None:
+        n = len(pics)
+        st = (C.c_int * n)(*streams)
+        sl = (C.c_int * n)(*[p.cur_slot for p in pics])
+        recs = (C.c_void_p * n)(*[p.rec for p in pics])
+        coefs = (C.c_void_p * n)(*[p.coef for p in pics])
+        nc = (C.c_uint32 * n)(*[p.ncoef for p in pics])
+        if self._L.h264mi_engine_decode(self._h, n, st, sl, recs, coefs, nc) != 0:
+            raise RuntimeError("h264mi_engine_decode failed")
+
+    def decode_device(self, npics: int, d_recs: int, d_coef: int, d_pics: int) -> None:
+        if self._L.h264mi_engine_decode_device(self._h, npics, d_recs, d_coef, d_pics) != 0:
+            raise RuntimeError("h264mi_engine_decode_device failed")
+
+    def read(self, stream: int, slot: int) -> np.ndarray:
+        out = np.empty(self.frame_bytes, dtype=np.uint8)
+        if self._L.h264mi_engine_read(self._h, stream, slot, out.ctypes.data) != 0:
+            raise RuntimeError("h264mi_engine_read failed")
+        return out
+
+    def sync(self) -> None:
+        if self._L.h264mi_engine_sync(self._h) != 0:
+            raise RuntimeError("h264mi_engine_sync failed")
+
+    def errors(self) -> int:
+        return int(self._L.h264mi_engine_errors(self._h))
+
+    def last_timing_us(self):
+        v = (C.c_float * 2)()
+        if self._L.h264mi_engine_last_timing(self._h, v) != 0:
+            return None
+        return float(v[0]), float(v[1])
+
+    def close(self):
+        if self._h:
+            self._L.h264mi_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,168 @@
+/* h264mi -- MI355X-native H.264 Baseline macroblock-reconstruction engine.
+ *
+ * C-ABI of libh264mi.so (plain pointers and sizes only).  Three layers:
+ *
+ * 1. The Broadway decoder API (drop-in for Decoder/inc/H264SwDecApi.h):
+ *    H264SwDecInit / Decode / NextPicture / GetInfo / Release /
+ *    GetAPIVersion with the same structures, return codes and call
+ *    protocol.  Replaces reference H264SwDecApi.c:124-569.
+ * 2. The wasm/JS glue API (drop-in for Decoder/src/Decoder.c:44-185):
+ *    broadwayInit / broadwayCreateStream / broadwayPlayStream / broadwayExit /
+ *    broadwayGetMajorVersion / broadwayGetMinorVersion, calling back into
+ *    broadwayOnHeadersDecoded / broadwayOnPictureDecoded, which the embedder
+ *    registers with broadwaySetCallbacks (the emscripten library.js:1-13
+ *    bridge becomes a function-pointer registration).
+ * 3. The batched engine API used for multi-stream throughput (one picture
+ *    from each of S streams per launch): h264mi_engine_*.
+ *    This is the hot path the reference has no equivalent for; its unit of
+ *    work is the MB-record batch of include/h264mi_records.h.
+ */
+#ifndef H264MI_H
+#define H264MI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------- */
+/* 1. H264SwDec API  (reference Decoder/inc/H264SwDecApi.h:53-173)         */
+/* ---------------------------------------------------------------------- */
+typedef uint8_t  u8;
+typedef uint32_t u32;
+typedef int32_t  i32;
+
+typedef enum {
+    H264SWDEC_OK = 0,
+    H264SWDEC_STRM_PROCESSED = 1,
+    H264SWDEC_PIC_RDY,
+    H264SWDEC_PIC_RDY_BUFF_NOT_EMPTY,
+    H264SWDEC_HDRS_RDY_BUFF_NOT_EMPTY,
+    H264SWDEC_PARAM_ERR = -1,
+    H264SWDEC_STRM_ERR = -2,
+    H264SWDEC_NOT_INITIALIZED = -3,
+    H264SWDEC_MEMFAIL = -4,
+    H264SWDEC_INITFAIL = -5,
+    H264SWDEC_HDRS_NOT_RDY = -6,
+    H264SWDEC_EVALUATION_LIMIT_EXCEEDED = -7
+} H264SwDecRet;
+
+typedef void *H264SwDecInst;
+
+typedef struct {
+    u8  *pStream;
+    u32  dataLen;
+    u32  picId;
+    u32  intraConcealmentMethod;
+} H264SwDecInput;
+
+typedef struct {
+    u8  *pStrmCurrPos;
+} H264SwDecOutput;
+
+typedef struct {
+    u32 *pOutputPicture;     /* planar I420, picWidth*picHeight*3/2 bytes */
+    u32 picId;
+    u32 isIdrPicture;
+    u32 nbrOfErrMBs;
+} H264SwDecPicture;
+
+typedef struct {
+    u32 cropLeftOffset;
+    u32 cropOutWidth;
+    u32 cropTopOffset;
+    u32 cropOutHeight;
+} CropParams;
+
+typedef struct {
+    u32 profile;
+    u32 picWidth;            /* MB-aligned, pixels */
+    u32 picHeight;
+    u32 videoRange;
+    u32 matrixCoefficients;
+    u32 parWidth;
+    u32 parHeight;
+    u32 croppingFlag;
+    CropParams cropParams;
+} H264SwDecInfo;
+
+typedef struct {
+    u32 major;
+    u32 minor;
+} H264SwDecApiVersion;
+
+H264SwDecRet H264SwDecInit(H264SwDecInst *decInst, u32 noOutputReordering);   /* H264SwDecApi.c:124 */
+H264SwDecRet H264SwDecDecode(H264SwDecInst decInst, H264SwDecInput *pInput,
+                             H264SwDecOutput *pOutput);                          /* :338 */
+H264SwDecRet H264SwDecNextPicture(H264SwDecInst decInst, H264SwDecPicture *pOutput,
+                                  u32 endOfStream);                              /* :524 */
+H264SwDecRet H264SwDecGetInfo(H264SwDecInst decInst, H264SwDecInfo *pDecInfo);  /* :204 */
+void H264SwDecRelease(H264SwDecInst decInst);                                    /* :259 */
+H264SwDecApiVersion H264SwDecGetAPIVersion(void);                                /* :487 */
+
+/* ---------------------------------------------------------------------- */
+/* 2. Broadway glue (reference Decoder/src/Decoder.c:44-185, make.py:39)   */
+/* ---------------------------------------------------------------------- */
+typedef void (*broadway_headers_cb)(void *user);
+typedef void (*broadway_picture_cb)(void *user, u8 *buffer, u32 width, u32 height);
+
+void broadwaySetCallbacks(broadway_headers_cb on_headers, broadway_picture_cb on_picture, void *user);
+u32  broadwayInit(void);                    /* Decoder.c:178 */
+u8  *broadwayCreateStream(u32 length);      /* Decoder.c:58  */
+void broadwayPlayStream(u32 length);        /* Decoder.c:67  */
+void broadwayExit(void);                    /* Decoder.c:88  */
+u32  broadwayGetMajorVersion(void);         /* Decoder.c:164 */
+u32  broadwayGetMinorVersion(void);         /* Decoder.c:169 */
+
+/* ---------------------------------------------------------------------- */
+/* 3. Batched reconstruction engine (MI355X hot path)                      */
+/* ---------------------------------------------------------------------- */
+typedef struct h264mi_engine h264mi_engine;
+
+/* Reconstruction engine for `nstreams` independent streams of one size
+ * (w_mbs x h_mbs macroblocks), each with `nslots` frame slots in HBM. */
+h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots);
+void h264mi_engine_destroy(h264mi_engine *e);
+
+/* Reconstruct one picture per listed stream (host-resident record batches):
+ * recs[i] -> w*h MbRec (96 B each), coefs[i] -> ncoef[i] int16x16 blocks. */
+int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
+                         const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef);
+
+/* Device-resident variant (records already in HBM; kernel-only timing):
+ * d_recs = npics*w*h MbRec in batch order with coefficient offsets relative
+ * to d_coef, d_pics = npics PicDesc. */
+int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
+                                const void *d_pics);
+
+int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */
+int  h264mi_engine_sync(h264mi_engine *e);
+/* residual range errors seen since the last call (reference transform.c:181) */
+uint32_t h264mi_engine_errors(h264mi_engine *e);
+/* average duration (us) of the last batch's kernels: [0] k_inter, [1] k_wave sum */
+int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
+void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);          /* device pointer */
+size_t h264mi_engine_frame_bytes(h264mi_engine *e);
+
+/* MB-record capture: run the host parser over a whole Annex-B stream and keep
+ * every picture's record batch (the §8d "pre-parsed MB-record batches"). */
+typedef struct h264mi_capture h264mi_capture;
+h264mi_capture *h264mi_capture_stream(const uint8_t *buf, size_t len, int no_reorder);
+int  h264mi_capture_info(const h264mi_capture *c, int *w_mbs, int *h_mbs, int *nslots, int *npics, int *errors);
+int  h264mi_capture_picture(const h264mi_capture *c, int i, const void **rec, const int16_t **coef,
+                            uint32_t *ncoef, int *cur_slot, uint64_t *alg_ref_bytes);
+int  h264mi_capture_stats(const h264mi_capture *c, int i, uint32_t *n_inter, uint32_t *n_intra, uint32_t *n_coded);
+void h264mi_capture_free(h264mi_capture *c);
+
+/* Device memory helpers for the device-resident path (HIP device pointers) */
+void *h264mi_device_alloc(size_t bytes);
+int   h264mi_device_free(void *p);
+int   h264mi_copy_h2d(void *dst, const void *src, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

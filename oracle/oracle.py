@@ -1,0 +1,109 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY (checker / CPU baseline, never product).
+
+Python binding of oracle/_build/liboracle.so: the plain-C restatement of the
+reference reconstruction (oracle/recon_cpu.c) driven by the product host
+parser, plus the reference decoder binary oracle/_ref/refdec (built here from
+/root/reference by oracle/Makefile.ref, used to make golden fixtures).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+import os
+import subprocess
+import tempfile
+from typing import List, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+REFDEC = os.path.join(HERE, "_ref", "refdec")
+
+_L = None
+
+
+def lib() -> C.CDLL:
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", HERE])
+        L = C.CDLL(LIB)
+        L.oracle_decode_stream.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_double)]
+        L.oracle_decode_stream.restype = C.c_void_p
+        L.oracle_result_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                         C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_size_t)]
+        L.oracle_result_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        L.oracle_result_free.argtypes = [C.c_void_p]
+        L.oracle_replay_create.argtypes = [C.c_int, C.c_int, C.c_int]
+        L.oracle_replay_create.restype = C.c_void_p
+        L.oracle_replay_picture.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.oracle_replay_picture.restype = C.c_int
+        L.oracle_replay_frame.argtypes = [C.c_void_p, C.c_int]
+        L.oracle_replay_frame.restype = C.c_void_p
+        L.oracle_replay_free.argtypes = [C.c_void_p]
+        _L = L
+    return _L
+
+
+def decode(stream: bytes, no_reorder: bool = False) -> Tuple[List[bytes], int, int, int, float]:
+    """Decode a whole Annex-B stream on the CPU (DecTestBench semantics incl.
+    the end-of-stream flush).  Returns (frames, errors, width, height, seconds)."""
+    L = lib()
+    buf = C.create_string_buffer(stream, len(stream))
+    secs = C.c_double()
+    res = L.oracle_decode_stream(C.cast(buf, C.c_void_p), len(stream), int(no_reorder), C.byref(secs))
+    n, e, w, h, nb = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
+    L.oracle_result_info(res, C.byref(n), C.byref(e), C.byref(w), C.byref(h), C.byref(nb))
+    data = np.empty(nb.value, dtype=np.uint8)
+    L.oracle_result_copy(res, data.ctypes.data, nb.value)
+    L.oracle_result_free(res)
+    fb = w.value * h.value * 3 // 2
+    frames = [data[i * fb:(i + 1) * fb].tobytes() for i in range(n.value)] if fb else []
+    return frames, e.value, w.value, h.value, secs.value
+
+
+class Replay:
+    """CPU reconstruction of captured MB-record pictures into frame slots."""
+
+    def __init__(self, w_mbs: int, h_mbs: int, nslots: int):
+        self.w, self.h, self.nslots = w_mbs, h_mbs, nslots
+        self._c = lib().oracle_replay_create(w_mbs, h_mbs, nslots)
+
+    def picture(self, rec_addr: int, coef_addr: int, cur_slot: int) -> int:
+        return lib().oracle_replay_picture(self._c, rec_addr, coef_addr, self.w, self.h, cur_slot)
+
+    def frame(self, slot: int) -> bytes:
+        p = lib().oracle_replay_frame(self._c, slot)
+        return C.string_at(p, self.w * self.h * 384)
+
+    def __del__(self):
+        try:
+            lib().oracle_replay_free(self._c)
+        except Exception:
+            pass
+
+
+def md5(b: bytes) -> str:
+    return hashlib.md5(b).hexdigest()
+
+
+def refdec_frames(stream: bytes, no_reorder: bool = False) -> List[bytes]:
+    """Decode with the reference C decoder (only in the build container)."""
+    if not os.path.exists(REFDEC):
+        raise FileNotFoundError(REFDEC)
+    with tempfile.TemporaryDirectory() as td:
+        src = os.path.join(td, "in.h264")
+        yuv = os.path.join(td, "out.yuv")
+        with open(src, "wb") as f:
+            f.write(stream)
+        args = [REFDEC, "-O" + yuv] + (["-R"] if no_reorder else []) + [src]
+        out = subprocess.run(args, capture_output=True, text=True)
+        w = h = None
+        for line in out.stdout.splitlines():
+            if line.startswith("Width"):
+                parts = line.split()
+                w, h = int(parts[1]), int(parts[3])
+        data = open(yuv, "rb").read() if os.path.exists(yuv) else b""
+    fb = w * h * 3 // 2 if w else 0
+    return [data[i:i + fb] for i in range(0, len(data), fb)] if fb else []

@@ -1,0 +1,107 @@
+/* ORACLE -- TEST INFRASTRUCTURE ONLY.
+ * ctypes-friendly entry points of liboracle.so for tests/ and bench.py's
+ * cpu_baseline leg.  Decodes a whole Annex-B buffer the way the reference
+ * testbench does (DecTestBench.c:230-410: drain NextPicture after every
+ * PIC_RDY, flush at end) with the CPU restatement of the reconstruction. */
+#include "recon_cpu.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+typedef struct OracleOut {
+    uint8_t *data;
+    size_t   len, cap;
+    int      npics, errors;
+    int      w, h;
+} OracleOut;
+
+static void out_append(OracleOut *o, const uint8_t *p, size_t n)
+{
+    if (o->len + n > o->cap) {
+        size_t nc = o->cap ? o->cap * 2 : (n * 8);
+        while (nc < o->len + n) nc *= 2;
+        o->data = (uint8_t *)realloc(o->data, nc);
+        o->cap = nc;
+    }
+    memcpy(o->data + o->len, p, n);
+    o->len += n;
+}
+
+static void drain(H264Dec *d, OracleOut *o)
+{
+    const uint8_t *pic;
+    uint32_t id, idr, em;
+    while ((pic = h264dec_next_output(d, &id, &idr, &em)) != NULL) {
+        out_append(o, pic, d->frame_bytes);
+        o->npics++;
+        o->errors += (int)em;
+    }
+}
+
+/* Decode buf; returns an opaque result (frames concatenated, I420 MB-aligned). */
+void *oracle_decode_stream(const uint8_t *buf, size_t len, int no_reorder, double *seconds)
+{
+    OracleOut *o = (OracleOut *)calloc(1, sizeof(OracleOut));
+    H264Dec *d = (H264Dec *)calloc(1, sizeof(H264Dec));
+    if (!o || !d) { free(o); free(d); return NULL; }
+    h264dec_init(d, no_reorder, oracle_backend_create());
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    const uint8_t *p = buf;
+    uint32_t left = (uint32_t)len, pic_id = 0;
+    while (left > 0) {
+        uint32_t rb = 0;
+        int r = h264dec_decode(d, p, left, pic_id, &rb);
+        if (r == DEC_PIC_RDY) pic_id++;
+        if (r == DEC_ERROR || r == DEC_PARAM_SET_ERROR) o->errors++;
+        if (r == DEC_PIC_RDY || r == DEC_HDRS_RDY) drain(d, o);
+        if (rb > left) rb = left;
+        p += rb;
+        left -= rb;
+    }
+    h264dec_flush(d);
+    drain(d, o);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    const Sps *s = h264dec_active_sps(d);
+    if (s) { o->w = s->w_mbs * 16; o->h = s->h_mbs * 16; }
+    h264dec_release(d);
+    free(d);
+    return o;
+}
+
+int oracle_result_info(void *res, int *npics, int *errors, int *w, int *h, size_t *bytes)
+{
+    OracleOut *o = (OracleOut *)res;
+    if (!o) return -1;
+    *npics = o->npics; *errors = o->errors; *w = o->w; *h = o->h; *bytes = o->len;
+    return 0;
+}
+
+int oracle_result_copy(void *res, uint8_t *dst, size_t cap)
+{
+    OracleOut *o = (OracleOut *)res;
+    if (!o || cap < o->len) return -1;
+    memcpy(dst, o->data, o->len);
+    return 0;
+}
+
+void oracle_result_free(void *res)
+{
+    OracleOut *o = (OracleOut *)res;
+    if (!o) return;
+    free(o->data);
+    free(o);
+}
+
+/* Reconstruct a sequence of captured MB-record pictures (as produced by the
+ * product's h264mi_capture_*) into CPU frame slots, for record-level parity
+ * checks of the HIP kernels.  frames_out receives nslots*w*h*384 bytes. */
+void *oracle_replay_create(int w_mbs, int h_mbs, int nslots) { return oracle_ctx_create(w_mbs, h_mbs, nslots); }
+int oracle_replay_picture(void *ctx, const void *rec, const int16_t *coef, int w_mbs, int h_mbs, int cur_slot)
+{
+    return oracle_recon_picture(ctx, (const MbRec *)rec, coef, w_mbs, h_mbs, cur_slot);
+}
+const uint8_t *oracle_replay_frame(void *ctx, int slot) { return oracle_ctx_frame(ctx, slot); }
+void oracle_replay_free(void *ctx) { oracle_ctx_destroy(ctx); }
