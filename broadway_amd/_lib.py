@@ -90,10 +90,19 @@ H264SWDEC_HDRS_NOT_RDY = -6
 
 
 def mi() -> C.CDLL:
-    """libh264mi.so with prototypes set."""
+    """libh264mi.so with prototypes set.
+
+    PyTorch-ROCm ships its own libamdhip64.so (same SONAME libamdhip64.so.7 as
+    /opt/rocm's).  If torch is importable it is imported first so that
+    libh264mi.so binds to that already-loaded runtime and the process holds a
+    single HIP runtime (torch.cuda.synchronize() then sees our stream work)."""
     global _mi
     if _mi is not None:
         return _mi
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = _load("libh264mi.so")
     vp, i32, u32, sz = C.c_void_p, C.c_int, C.c_uint32, C.c_size_t
     L.H264SwDecInit.argtypes = [C.POINTER(vp), u32]
@@ -135,6 +144,12 @@ def mi() -> C.CDLL:
     L.h264mi_engine_errors.restype = u32
     L.h264mi_engine_last_timing.argtypes = [vp, C.POINTER(C.c_float)]
     L.h264mi_engine_last_timing.restype = i32
+    L.h264mi_engine_set_timing.argtypes = [vp, i32]
+    L.h264mi_engine_set_timing.restype = i32
+    L.h264mi_engine_timing_report.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i32)]
+    L.h264mi_engine_timing_report.restype = i32
+    L.h264mi_engine_profile.argtypes = [vp, i32, C.POINTER(C.c_uint64), sz]
+    L.h264mi_engine_profile.restype = i32
     L.h264mi_engine_frame_ptr.argtypes = [vp, i32, i32]
     L.h264mi_engine_frame_ptr.restype = vp
     L.h264mi_engine_frame_bytes.argtypes = [vp]

@@ -24,7 +24,12 @@ struct h264mi_engine {
     int w, h, nmbs, nstreams, nslots;
     size_t frame_bytes;
     uint8_t *d_frames;
-    uint8_t *d_edges;
+    unsigned long long *d_mbx;    // k_rows row mailboxes: 32 granules (256 B) per batch MB
+    unsigned epoch;
+    unsigned long long *d_prof;   // optional k_rows phase clocks
+    size_t prof_cap;
+    uint8_t *d_dbrec;         // 64 B per batch MB
+    int16_t *d_res;           // 384 x int16 per batch MB (intra residual)
     MbRec *d_rec;
     int16_t *d_coef;
     size_t coef_cap;          // blocks
@@ -37,29 +42,16 @@ struct h264mi_engine {
     unsigned *h_err;
     hipStream_t st;
     hipEvent_t ev_staged, ev0, ev1, ev2;
-    int ndiag, diag_len;
     uint32_t err_accum;
     int timing;
+    // per-batch kernel timing (h264mi_engine_set_timing): event triples
+    hipEvent_t *tev;
+    int tev_cap, tev_n;
 };
-
-static int diag_geometry(int w, int h, int *ndiag, int *len)
-{
-    *ndiag = w + 2 * (h - 1);
-    int mx = 0;
-    for (int t = 0; t < *ndiag; t++) {
-        int lo = t - (w - 1) + 1;
-        lo = lo > 0 ? lo >> 1 : 0;
-        int hi = t / 2 < h - 1 ? t / 2 : h - 1;
-        int n = hi - lo + 1;
-        if (n > mx) mx = n;
-    }
-    *len = mx;
-    return 0;
-}
 
 extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
 {
-    if (w_mbs < 1 || h_mbs < 1 || nstreams < 1 || nslots < 1) return NULL;
+    if (w_mbs < 1 || h_mbs < 1 || h_mbs > 1024 || nstreams < 1 || nslots < 1) return NULL;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) {
         fprintf(stderr, "h264mi: no HIP device %d (count %d)\n", device, ndev);
@@ -72,12 +64,13 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->w = w_mbs; e->h = h_mbs; e->nmbs = w_mbs * h_mbs;
     e->nstreams = nstreams; e->nslots = nslots;
     e->frame_bytes = (size_t)e->nmbs * 384;
-    diag_geometry(w_mbs, h_mbs, &e->ndiag, &e->diag_len);
     e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
     e->h_coef_cap = e->coef_cap;
     e->timing = getenv("H264MI_TIMING") != NULL;
     bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
-              hipMalloc(&e->d_edges, (size_t)nstreams * e->nmbs * 64) == hipSuccess &&
+              hipMalloc(&e->d_mbx, (size_t)nstreams * e->nmbs * 256) == hipSuccess &&
+              hipMalloc(&e->d_dbrec, (size_t)nstreams * e->nmbs * 64) == hipSuccess &&
+              hipMalloc(&e->d_res, (size_t)nstreams * e->nmbs * 768) == hipSuccess &&
               hipMalloc(&e->d_rec, sizeof(MbRec) * nstreams * e->nmbs) == hipSuccess &&
               hipMalloc(&e->d_coef, e->coef_cap * 32) == hipSuccess &&
               hipMalloc(&e->d_pics, sizeof(PicDesc) * nstreams) == hipSuccess &&
@@ -96,7 +89,8 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         return NULL;
     }
     (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * nslots * nstreams, e->st);
-    (void)hipMemsetAsync(e->d_edges, 0, (size_t)nstreams * e->nmbs * 64, e->st);
+    (void)hipMemsetAsync(e->d_mbx, 0, (size_t)nstreams * e->nmbs * 256, e->st);
+    e->epoch = 0;
     (void)hipEventRecord(e->ev_staged, e->st);
     (void)hipStreamSynchronize(e->st);
     return e;
@@ -106,13 +100,14 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
 {
     if (!e) return;
     if (e->st) (void)hipStreamSynchronize(e->st);
-    (void)hipFree(e->d_frames); (void)hipFree(e->d_edges); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
+    (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_mbx); (void)hipFree(e->d_dbrec); (void)hipFree(e->d_res); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
     (void)hipFree(e->d_pics); (void)hipFree(e->d_err);
     (void)hipHostFree(e->h_rec); (void)hipHostFree(e->h_coef); (void)hipHostFree(e->h_pics); (void)hipHostFree(e->h_err);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
+    h264mi_engine_set_timing(e, 0);
     if (e->st) (void)hipStreamDestroy(e->st);
     free(e);
 }
@@ -125,24 +120,33 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.frame_bytes = e->frame_bytes;
     a.rec = d_rec;
     a.coef = d_coef;
-    a.edges = e->d_edges;
+    a.mbx = e->d_mbx;
+    if (++e->epoch == 0) {                    // granule tags: never 0 (the cleared state)
+        HIPCHECK(hipMemsetAsync(e->d_mbx, 0, (size_t)e->nstreams * e->nmbs * 256, e->st));
+        e->epoch = 1;
+    }
+    a.epoch = e->epoch;
+    a.prof = e->d_prof;
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;
-    a.diag = 0;
-    a.diag_len = e->diag_len;
+    a.dbrec = e->d_dbrec;
+    a.res = e->d_res;
     a.err = e->d_err;
     HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * npics, e->st));
-    if (e->timing) (void)hipEventRecord(e->ev0, e->st);
-    hipLaunchKernelGGL(k_inter, dim3(npics * e->nmbs), dim3(64), 0, e->st, a);
-    HIPCHECK(hipGetLastError());
-    if (e->timing) (void)hipEventRecord(e->ev1, e->st);
-    for (int t = 0; t < e->ndiag; t++) {
-        a.diag = t;
-        hipLaunchKernelGGL(k_wave, dim3(npics * e->diag_len), dim3(64), 0, e->st, a);
+    hipEvent_t t0 = e->ev0, t1 = e->ev1, t2 = e->ev2;
+    if (e->tev && e->tev_n < e->tev_cap) {
+        t0 = e->tev[3 * e->tev_n]; t1 = e->tev[3 * e->tev_n + 1]; t2 = e->tev[3 * e->tev_n + 2];
+        e->tev_n++;
     }
+    const bool rec = e->timing || e->tev;
+    if (rec) (void)hipEventRecord(t0, e->st);
+    hipLaunchKernelGGL(k_mb, dim3(npics * e->nmbs), dim3(64), 0, e->st, a);
     HIPCHECK(hipGetLastError());
-    if (e->timing) (void)hipEventRecord(e->ev2, e->st);
+    if (rec) (void)hipEventRecord(t1, e->st);
+    hipLaunchKernelGGL(k_rows, dim3(npics * e->h), dim3(64), 0, e->st, a);
+    HIPCHECK(hipGetLastError());
+    if (rec) (void)hipEventRecord(t2, e->st);
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
     return 0;
 }
@@ -221,6 +225,64 @@ extern "C" int h264mi_engine_last_timing(h264mi_engine *e, float *us2)
     HIPCHECK(hipEventElapsedTime(&ms1, e->ev1, e->ev2));
     us2[0] = ms0 * 1000.f;
     us2[1] = ms1 * 1000.f;
+    return 0;
+}
+
+extern "C" int h264mi_engine_set_timing(h264mi_engine *e, int max_batches)
+{
+    if (!e) return -1;
+    if (e->tev) {
+        for (int i = 0; i < 3 * e->tev_cap; i++) (void)hipEventDestroy(e->tev[i]);
+        free(e->tev);
+        e->tev = NULL;
+    }
+    e->tev_cap = e->tev_n = 0;
+    if (max_batches <= 0) return 0;
+    e->tev = (hipEvent_t *)calloc((size_t)max_batches * 3, sizeof(hipEvent_t));
+    if (!e->tev) return -1;
+    for (int i = 0; i < 3 * max_batches; i++) HIPCHECK(hipEventCreate(&e->tev[i]));
+    e->tev_cap = max_batches;
+    return 0;
+}
+
+extern "C" int h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches)
+{
+    if (!e || !e->tev) return -1;
+    HIPCHECK(hipStreamSynchronize(e->st));
+    double a = 0, b = 0;
+    for (int i = 0; i < e->tev_n; i++) {
+        float m0 = 0, m1 = 0;
+        HIPCHECK(hipEventElapsedTime(&m0, e->tev[3 * i], e->tev[3 * i + 1]));
+        HIPCHECK(hipEventElapsedTime(&m1, e->tev[3 * i + 1], e->tev[3 * i + 2]));
+        a += m0 * 1000.0;
+        b += m1 * 1000.0;
+    }
+    *inter_us = a;
+    *wave_us = b;
+    *nbatches = e->tev_n;
+    e->tev_n = 0;
+    return 0;
+}
+
+extern "C" int h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long long *out, size_t n)
+{
+    if (!e) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    if (out && e->d_prof) {
+        HIPCHECK(hipStreamSynchronize(e->st));
+        HIPCHECK(hipMemcpy(out, e->d_prof, sizeof(unsigned long long) * (n < e->prof_cap ? n : e->prof_cap),
+                           hipMemcpyDeviceToHost));
+    }
+    if (enable && !e->d_prof) {
+        e->prof_cap = (size_t)e->nstreams * e->h * 8 + (size_t)e->nstreams * e->nmbs * 4;
+        HIPCHECK(hipMalloc(&e->d_prof, sizeof(unsigned long long) * e->prof_cap));
+        HIPCHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * e->prof_cap));
+    } else if (!enable && e->d_prof) {
+        HIPCHECK(hipStreamSynchronize(e->st));
+        (void)hipFree(e->d_prof);
+        e->d_prof = NULL;
+        e->prof_cap = 0;
+    }
     return 0;
 }
 

@@ -1,25 +1,25 @@
 // H.264 Baseline macroblock reconstruction + in-loop deblocking for gfx950.
 //
 // Two kernels per picture batch (one picture from each of S streams):
-//   k_inter  -- every inter MB (P_L0_*, P_8x8, P_Skip) of every picture in the
-//               batch, fully parallel: residual (dequant + 4x4 IDCT), 6-tap
-//               luma / bilinear chroma motion compensation from HBM-resident
-//               reference slots staged through LDS, clip-add, write-out, and a
-//               copy of the MB's unfiltered bottom row / right column into the
-//               edge buffer (intra neighbours read those after deblocking has
-//               started).  Reference: h264bsdInterPrediction
-//               (inter_prediction.c:364-487), h264bsdPredictSamples
-//               (reconstruct.c:1819-1941), h264bsdWriteOutputBlocks
-//               (image.c:171-343).
-//   k_wave   -- one launch per MB anti-diagonal t = c + 2r (dependencies
-//               (r,c-1), (r-1,c), (r-1,c+1)); for each MB on it: intra
-//               reconstruction (I4x4 10-step sub-wavefront, I16x16, chroma,
-//               I_PCM) from the edge buffers, then the MB's deblocking
-//               (bS per 4x4 edge segment, thresholds, luma/chroma filters) in
-//               the reference's raster-equivalent order.  Reference:
-//               h264bsdIntraPrediction (intra_prediction.c:475-988),
-//               h264bsdFilterPicture (deblocking.c:574-1736).
-// One 64-lane wave per macroblock in both kernels.
+//   k_mb    -- every MB of every picture in the batch, fully parallel, one
+//              64-lane wave per MB: deblocking record (bS of the 32 4x4 edge
+//              segments + alpha/beta/indexA per edge class), residual
+//              (dequant + 4x4 IDCT + luma/chroma DC transforms) and, for inter
+//              MBs, 6-tap luma / bilinear chroma motion compensation from the
+//              HBM-resident reference slots staged through LDS, clip-add and
+//              write-out.  Reference: h264bsdProcessBlock/LumaDc/ChromaDc
+//              (transform.c:94-398), h264bsdInterPrediction
+//              (inter_prediction.c:364-487), h264bsdPredictSamples
+//              (reconstruct.c:1819-1941), h264bsdWriteOutputBlocks
+//              (image.c:171-343), GetBoundaryStrengths / thresholds
+//              (deblocking.c:1134-1532).
+//   k_rows  -- one 16-wave workgroup per picture: MB rows pipelined across the
+//              waves with LDS progress counters (MB (r,c) waits for (r-1,c+1)),
+//              intra reconstruction (I4x4 10-step sub-wavefront, I16x16,
+//              chroma, I_PCM) from unfiltered neighbour samples, then the MB's
+//              deblocking in the reference's raster-equivalent order.
+//              Reference: h264bsdIntraPrediction (intra_prediction.c:475-988),
+//              h264bsdFilterPicture (deblocking.c:574-1736).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../../include/h264mi_records.h"
@@ -31,13 +31,15 @@ struct ReconArgs {
     unsigned long long frame_bytes;
     const MbRec *rec;         // batch records (pictures back to back)
     const int16_t *coef;      // batch coefficient blocks
-    uint8_t *edges;           // 64 B per MB of the batch
     const PicDesc *pics;
     int npics;
     int w, h;                 // picture size in MBs
-    int diag;                 // k_wave: anti-diagonal index
-    int diag_len;             // k_wave: max MBs on a diagonal
-    unsigned int *err;        // residual range errors (per picture)
+    uint8_t *dbrec;           // 64 B deblocking record per MB of the batch
+    int16_t *res;             // 384 residual samples per MB (intra MBs only)
+    unsigned int *err;        // per picture: bit0 residual range error, bit1 wait timeout
+    unsigned long long *mbx;  // row mailboxes: 32 tagged granules per MB of the batch (k_rows)
+    unsigned int epoch;       // launch counter != 0: granule tag (no reset between launches)
+    unsigned long long *prof; // optional k_rows phase clocks: 8 per (row, picture) workgroup
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -60,6 +62,15 @@ __constant__ uint8_t cTc0[52][3] = {
     {2, 3, 4}, {2, 3, 4}, {3, 3, 5}, {3, 4, 6}, {3, 4, 6}, {4, 5, 7}, {4, 5, 8},
     {4, 6, 9}, {5, 7, 10}, {6, 8, 11}, {6, 8, 13}, {7, 10, 14}, {8, 11, 16},
     {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+// ordering of LDS traffic between the lanes of one wave (waves of k_rows
+// work independently; k_mb workgroups are a single wave)
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return min(max(v, lo), hi); }
@@ -113,7 +124,7 @@ __device__ void mb_residual(const MbRec &r, const int16_t *__restrict__ coef, in
         }
         dc[lane] = f;
     }
-    __syncthreads();
+    wave_sync();
     if (lane < 24) {
         const bool luma = lane < 16;
         const int qp = luma ? r.qp : r.qpc;
@@ -179,7 +190,7 @@ __device__ void mb_residual(const MbRec &r, const int16_t *__restrict__ coef, in
             for (int i = 0; i < 16; i++) res[256 + comp * 64 + (by + (i >> 2)) * 8 + bx + (i & 3)] = (int16_t)o[i];
         }
     }
-    __syncthreads();
+    wave_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -233,123 +244,24 @@ __device__ __forceinline__ void luma_row4(const uint8_t *win, int yy, int fx, in
 #undef H1
 }
 
-__device__ __forceinline__ void write_edges(uint8_t *e, const uint8_t *ty, int ystride, const uint8_t *tu,
-                                            const uint8_t *tv, int cstride, int lane)
-{
-    // e[0..15] Y bottom row, [16..23] Cb bottom, [24..31] Cr bottom,
-    // [32..47] Y right col, [48..55] Cb right col, [56..63] Cr right col
-    uint8_t v;
-    if (lane < 16) v = ty[15 * ystride + lane];
-    else if (lane < 24) v = tu[7 * cstride + lane - 16];
-    else if (lane < 32) v = tv[7 * cstride + lane - 24];
-    else if (lane < 48) v = ty[(lane - 32) * ystride + 15];
-    else if (lane < 56) v = tu[(lane - 48) * cstride + 7];
-    else v = tv[(lane - 56) * cstride + 7];
-    e[lane] = v;
-}
-
-__global__ __launch_bounds__(64) void k_inter(ReconArgs a)
-{
-    const int nmbs = a.w * a.h;
-    const int gmb = blockIdx.x;                  // MB index within the batch
-    const int p = gmb / nmbs;
-    const int mb = gmb - p * nmbs;
-    if (p >= a.npics) return;
-    const PicDesc pd = a.pics[p];
-    const MbRec &r = a.rec[pd.rec_base + mb];
-    if (r.type > MBT_SKIP) return;               // intra: done by k_wave
-    const int lane = threadIdx.x;
-
-    __shared__ int16_t s_res[384];
-    __shared__ int32_t s_dc[24];
-    __shared__ uint8_t s_win[16 * 81];
-    __shared__ uint8_t s_cwin[2][16][9];
-    __shared__ uint8_t s_out[384];
-    __shared__ int s_err;
-    if (lane == 0) s_err = 0;
-
-    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
-    const int mbx = mb % a.w, mby = mb / a.w;
-    const uint8_t *frames = a.frames;
-
-    if (r.cbits) {
-        int e = 0;
-        mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, s_dc, lane, &e);
-        if (e) s_err = 1;
-    } else {
-        for (int i = lane; i < 384; i += WAVE) s_res[i] = 0;
-    }
-
-    // stage luma windows: 16 blocks x 9x9
-    for (int idx = lane; idx < 16 * 81; idx += WAVE) {
-        const int b = idx / 81, rem = idx - b * 81;
-        const int wy = rem / 9, wx = rem - wy * 9;
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int x = clip3(0, W16 - 1, mbx * 16 + blk_x(b) * 4 + (mvx >> 2) - 2 + wx);
-        const int y = clip3(0, H16 - 1, mby * 16 + blk_y(b) * 4 + (mvy >> 2) - 2 + wy);
-        s_win[idx] = ref[y * W16 + x];
-    }
-    // chroma windows: 16 blocks x 2 comps x 3x3
-    for (int idx = lane; idx < 16 * 2 * 9; idx += WAVE) {
-        const int b = idx / 18, rem = idx - b * 18;
-        const int comp = rem / 9, k = rem - comp * 9;
-        const int wy = k / 3, wx = k - wy * 3;
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes +
-                             (unsigned long long)W16 * H16 + (unsigned long long)comp * CW * CH;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int x = clip3(0, CW - 1, mbx * 8 + blk_x(b) * 2 + (mvx >> 3) + wx);
-        const int y = clip3(0, CH - 1, mby * 8 + blk_y(b) * 2 + (mvy >> 3) + wy);
-        s_cwin[comp][b][k] = ref[y * CW + x];
-    }
-    __syncthreads();
-
-    {   // luma: lane -> (block, row)
-        const int b = lane >> 2, yy = lane & 3;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        int o[4];
-        luma_row4(s_win + b * 81, yy, mvx & 3, mvy & 3, o);
-        const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
-#pragma unroll
-        for (int x = 0; x < 4; x++) s_out[by * 16 + bx + x] = (uint8_t)clip255(o[x] + s_res[by * 16 + bx + x]);
-    }
-    {   // chroma: lane -> (block, comp, row), 2 samples
-        const int b = lane >> 2, comp = (lane >> 1) & 1, yy = lane & 1;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int fx = mvx & 7, fy = mvy & 7;
-        const uint8_t *w = s_cwin[comp][b];
-        const int cx = blk_x(b) * 2, cy = blk_y(b) * 2 + yy;
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            const int A = w[yy * 3 + x], B = w[yy * 3 + x + 1], C = w[(yy + 1) * 3 + x], D = w[(yy + 1) * 3 + x + 1];
-            const int v = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
-            s_out[256 + comp * 64 + cy * 8 + cx + x] = (uint8_t)clip255(v + s_res[256 + comp * 64 + cy * 8 + cx + x]);
-        }
-    }
-    __syncthreads();
-
-    // write-out: luma 16 rows x 4 dwords, chroma 2 x 8 rows x 2 dwords
-    uint8_t *cur = a.frames + (unsigned long long)(pd.frame_base + pd.cur_slot) * a.frame_bytes;
-    {
-        const int row = lane >> 2, q = lane & 3;
-        *(uint32_t *)(cur + (size_t)(mby * 16 + row) * W16 + mbx * 16 + q * 4) = *(const uint32_t *)(s_out + row * 16 + q * 4);
-    }
-    if (lane < 32) {
-        const int comp = lane >> 4, row = (lane >> 1) & 7, q = lane & 1;
-        uint8_t *cp = cur + (size_t)W16 * H16 + (size_t)comp * CW * CH;
-        *(uint32_t *)(cp + (size_t)(mby * 8 + row) * CW + mbx * 8 + q * 4) =
-            *(const uint32_t *)(s_out + 256 + comp * 64 + row * 8 + q * 4);
-    }
-    write_edges(a.edges + (size_t)(pd.rec_base + mb) * 64, s_out, 16, s_out + 256, s_out + 320, 8, lane);
-    if (lane == 0 && s_err) atomicOr(a.err + p, 1u);
-}
-
 // ---------------------------------------------------------------------------
 // intra prediction (intra_prediction.c) into an LDS tile with a 1-sample halo
 // ---------------------------------------------------------------------------
 // luma tile: 17 rows x 24 cols; (row 0) = y=-1, (col 0) = x=-1; cols 17..20 = top-right
 #define TY_STRIDE 24
 #define TC_STRIDE 12
+
+// LDS offset (relative to the block's first sample) of virtual sample Sx[k]
+__device__ __forceinline__ int sx_off(int k, int S, bool avTR)
+{
+    if (k == 4) return -S - 1;                       // p[-1,-1]
+    if (k > 4) {                                     // p[k-5,-1], top-right replicated
+        int t = k - 5;
+        if (t > 3 && !avTR) t = 3;
+        return -S + t;
+    }
+    return (3 - k) * S - 1;                          // p[-1,3-k]
+}
 
 __device__ __forceinline__ int i4_pred(const uint8_t *T /* tile at block (0,0) i.e. &tile[(by+1)*S + bx+1] */,
                                        int S, int mode, int x, int y, bool avT, bool avL, bool avTR)
@@ -375,39 +287,37 @@ __device__ __forceinline__ int i4_pred(const uint8_t *T /* tile at block (0,0) i
         else v = (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
         break;
     default: {
-        // modes 4..8 read a mix of left / top / corner samples: build S[13]
-        int Sx[13];
-        Sx[4] = PTL;
-#pragma unroll
-        for (int k = 0; k < 8; k++) Sx[5 + k] = PT(k);
-#pragma unroll
-        for (int k = 0; k < 4; k++) Sx[3 - k] = PL(k);
+        // modes 4..8 read a mix of left / top / corner samples; the virtual
+        // array Sx[k]: Sx[4] = p[-1,-1], Sx[5+k] = p[k,-1], Sx[3-k] = p[-1,k]
+        // (resolved to one LDS offset per access -- no private array)
+#define SX(k) ((int)T[sx_off((k), S, avTR)])
         if (mode == 4) {
             const int d = x - y;
-            v = (Sx[3 + d] + 2 * Sx[4 + d] + Sx[5 + d] + 2) >> 2;
+            v = (SX(3 + d) + 2 * SX(4 + d) + SX(5 + d) + 2) >> 2;
         } else if (mode == 5) {
             const int z = 2 * x - y, i = x - (y >> 1);
-            if (z >= 0 && !(z & 1)) v = (Sx[4 + i] + Sx[5 + i] + 1) >> 1;
-            else if (z > 0) v = (Sx[3 + i] + 2 * Sx[4 + i] + Sx[5 + i] + 2) >> 2;
-            else if (z == -1) v = (Sx[3] + 2 * Sx[4] + Sx[5] + 2) >> 2;
-            else v = (Sx[4 - y] + 2 * Sx[5 - y] + Sx[6 - y] + 2) >> 2;
+            if (z >= 0 && !(z & 1)) v = (SX(4 + i) + SX(5 + i) + 1) >> 1;
+            else if (z > 0) v = (SX(3 + i) + 2 * SX(4 + i) + SX(5 + i) + 2) >> 2;
+            else if (z == -1) v = (SX(3) + 2 * SX(4) + SX(5) + 2) >> 2;
+            else v = (SX(4 - y) + 2 * SX(5 - y) + SX(6 - y) + 2) >> 2;
         } else if (mode == 6) {
             const int z = 2 * y - x, i = y - (x >> 1);
-            if (z >= 0 && !(z & 1)) v = (Sx[4 - i] + Sx[3 - i] + 1) >> 1;
-            else if (z > 0) v = (Sx[5 - i] + 2 * Sx[4 - i] + Sx[3 - i] + 2) >> 2;
-            else if (z == -1) v = (Sx[3] + 2 * Sx[4] + Sx[5] + 2) >> 2;
-            else v = (Sx[4 + x] + 2 * Sx[3 + x] + Sx[2 + x] + 2) >> 2;
+            if (z >= 0 && !(z & 1)) v = (SX(4 - i) + SX(3 - i) + 1) >> 1;
+            else if (z > 0) v = (SX(5 - i) + 2 * SX(4 - i) + SX(3 - i) + 2) >> 2;
+            else if (z == -1) v = (SX(3) + 2 * SX(4) + SX(5) + 2) >> 2;
+            else v = (SX(4 + x) + 2 * SX(3 + x) + SX(2 + x) + 2) >> 2;
         } else if (mode == 7) {
             const int i = x + (y >> 1);
-            if (!(y & 1)) v = (Sx[5 + i] + Sx[6 + i] + 1) >> 1;
-            else v = (Sx[5 + i] + 2 * Sx[6 + i] + Sx[7 + i] + 2) >> 2;
+            if (!(y & 1)) v = (SX(5 + i) + SX(6 + i) + 1) >> 1;
+            else v = (SX(5 + i) + 2 * SX(6 + i) + SX(7 + i) + 2) >> 2;
         } else {
             const int z = x + 2 * y, i = y + (x >> 1);
-            if (z > 5) v = Sx[0];
-            else if (z == 5) v = (Sx[1] + 3 * Sx[0] + 2) >> 2;
-            else if (!(z & 1)) v = (Sx[3 - i] + Sx[2 - i] + 1) >> 1;
-            else v = (Sx[3 - i] + 2 * Sx[2 - i] + Sx[1 - i] + 2) >> 2;
+            if (z > 5) v = SX(0);
+            else if (z == 5) v = (SX(1) + 3 * SX(0) + 2) >> 2;
+            else if (!(z & 1)) v = (SX(3 - i) + SX(2 - i) + 1) >> 1;
+            else v = (SX(3 - i) + 2 * SX(2 - i) + SX(1 - i) + 2) >> 2;
         }
+#undef SX
         break;
     }
     }
@@ -416,146 +326,6 @@ __device__ __forceinline__ int i4_pred(const uint8_t *T /* tile at block (0,0) i
 #undef PTL
     return v;
 }
-
-// 10-step schedule of the 16 4x4 blocks (x + 2y = step), two blocks max
-__constant__ int8_t cI4Sched[10][2] = {{0, -1}, {1, -1}, {4, 2}, {5, 3}, {6, 8},
-                                       {7, 9}, {12, 10}, {13, 11}, {14, -1}, {15, -1}};
-
-__device__ void intra_mb(const MbRec &r, const uint8_t *__restrict__ edges, int mb_global, int mbx, int w,
-                         const int16_t *res, uint8_t *ty, uint8_t *tu, uint8_t *tv, int lane)
-{
-    const bool aA = r.avail & AV_A, aB = r.avail & AV_B, aC = r.avail & AV_C, aD = r.avail & AV_D;
-    // --- gather neighbours from the edge buffers (unfiltered samples)
-    const uint8_t *eA = edges + (size_t)(mb_global - 1) * 64;
-    const uint8_t *eB = edges + (size_t)(mb_global - w) * 64;
-    const uint8_t *eC = edges + (size_t)(mb_global - w + 1) * 64;
-    const uint8_t *eD = edges + (size_t)(mb_global - w - 1) * 64;
-    (void)mbx;
-    if (lane < 16) {
-        if (aB) ty[1 + lane] = eB[lane];                        // top row
-        if (aA) ty[(lane + 1) * TY_STRIDE] = eA[32 + lane];     // left column
-    } else if (lane < 20) {
-        if (aC) ty[1 + lane] = eC[lane - 16];                   // top-right
-    } else if (lane < 28) {
-        const int i = lane - 20;
-        if (aB) { tu[1 + i] = eB[16 + i]; tv[1 + i] = eB[24 + i]; }
-        if (aA) { tu[(i + 1) * TC_STRIDE] = eA[48 + i]; tv[(i + 1) * TC_STRIDE] = eA[56 + i]; }
-    } else if (lane == 28) {
-        if (aD) { ty[0] = eD[15]; tu[0] = eD[23]; tv[0] = eD[31]; }
-    }
-    __syncthreads();
-
-    if (r.type == MBT_I16) {
-        const int mode = r.pred & 3;
-        const int y = lane >> 2, x0 = (lane & 3) * 4;
-        int dcv = 128, a = 0, b = 0, c = 0;
-        if (mode == 2) {
-            int st = 0, sl = 0;
-            for (int i = 0; i < 16; i++) { st += ty[1 + i]; sl += ty[(i + 1) * TY_STRIDE]; }
-            if (aA && aB) dcv = (st + sl + 16) >> 5;
-            else if (aA) dcv = (sl + 8) >> 4;
-            else if (aB) dcv = (st + 8) >> 4;
-        } else if (mode == 3) {
-            int H = 0, V = 0;
-            for (int i = 0; i < 8; i++) {
-                H += (i + 1) * ((int)ty[1 + 8 + i] - (int)ty[1 + 6 - i]);
-                V += (i + 1) * ((int)ty[(1 + 8 + i) * TY_STRIDE] - (int)ty[(1 + 6 - i) * TY_STRIDE]);
-            }
-            a = 16 * ((int)ty[16 * TY_STRIDE] + (int)ty[16]);
-            b = (5 * H + 32) >> 6;
-            c = (5 * V + 32) >> 6;
-        }
-        int pv[4];
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int x = x0 + i;
-            int p;
-            if (mode == 0) p = ty[1 + x];
-            else if (mode == 1) p = ty[(y + 1) * TY_STRIDE];
-            else if (mode == 2) p = dcv;
-            else p = clip255((a + b * (x - 7) + c * (y - 7) + 16) >> 5);
-            pv[i] = clip255(p + res[y * 16 + x]);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 4; i++) ty[(y + 1) * TY_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
-    } else {
-        // Intra 4x4: 10 dependency steps, up to two blocks per step
-        for (int step = 0; step < 10; step++) {
-            const int slot = lane >> 4;
-            int v = 0;
-            int b = -1;
-            if (slot < 2) b = cI4Sched[step][slot];
-            const int px = lane & 3, py = (lane >> 2) & 3;
-            if (b >= 0) {
-                const int bx = blk_x(b), by = blk_y(b);
-                const bool avL = bx > 0 || aA;
-                const bool avT = by > 0 || aB;
-                bool avTR;
-                if (b == 3 || b == 7 || b == 11 || b == 13 || b == 15) avTR = false;
-                else if (by == 0) avTR = bx == 3 ? aC : aB;
-                else avTR = true;
-                const int mode = (r.i4[b >> 1] >> ((b & 1) * 4)) & 15;
-                const uint8_t *T = ty + (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;
-                const int p = i4_pred(T, TY_STRIDE, mode, px, py, avT, avL, avTR);
-                v = clip255(p + res[(by * 4 + py) * 16 + bx * 4 + px]);
-            }
-            __syncthreads();
-            if (b >= 0) ty[(blk_y(b) * 4 + py + 1) * TY_STRIDE + blk_x(b) * 4 + px + 1] = (uint8_t)v;
-            __syncthreads();
-        }
-    }
-    // chroma: lane -> row (0..7) x comp, 4 samples each
-    {
-        const int comp = lane >> 5, y = (lane >> 2) & 7, x0 = (lane & 3) * 2;
-        uint8_t *T = comp ? tv : tu;
-        const int cmode = (r.pred >> 4) & 3;
-        int pv[2];
-        int a = 0, b = 0, c = 0;
-        if (cmode == 3) {
-            int H = 0, V = 0;
-            for (int i = 0; i < 4; i++) {
-                H += (i + 1) * ((int)T[1 + 4 + i] - (int)T[1 + 2 - i]);
-                V += (i + 1) * ((int)T[(1 + 4 + i) * TC_STRIDE] - (int)T[(1 + 2 - i) * TC_STRIDE]);
-            }
-            a = 16 * ((int)T[8 * TC_STRIDE] + (int)T[8]);
-            b = (34 * H + 32) >> 6;
-            c = (34 * V + 32) >> 6;
-        }
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int x = x0 + i;
-            int p;
-            if (cmode == 0) {
-                const int xo = x & 4, yo = y & 4;
-                int st = 0, sl = 0;
-                for (int k = 0; k < 4; k++) { st += T[1 + xo + k]; sl += T[(1 + yo + k) * TC_STRIDE]; }
-                if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) {
-                    p = (aA && aB) ? (st + sl + 4) >> 3 : aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
-                } else if (xo > 0) {
-                    p = aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
-                } else {
-                    p = aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
-                }
-            } else if (cmode == 1) p = T[(y + 1) * TC_STRIDE];
-            else if (cmode == 2) p = T[1 + x];
-            else p = clip255((a + b * (x - 3) + c * (y - 3) + 16) >> 5);
-            pv[i] = clip255(p + res[256 + comp * 64 + y * 8 + x]);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 2; i++) T[(y + 1) * TC_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
-    }
-    __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// deblocking of one MB (deblocking.c:574-1736)
-// LDS region: luma rows -4..15, cols -4..15 (20x20); chroma rows -2..7,
-// cols -4..7 (10x12) per component.
-// ---------------------------------------------------------------------------
-#define DY_S 20
-#define DC_S 12
 
 __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int bq, bool mb_edge)
 {
@@ -613,168 +383,693 @@ __device__ __forceinline__ void filt_chroma(uint8_t *s, int step, int bS, int al
     }
 }
 
-__global__ __launch_bounds__(64) void k_wave(ReconArgs a)
+// ---------------------------------------------------------------------------
+// deblocking record (precomputed by k_mb, consumed by k_rows): 64 B per MB
+//   [0..15]  bS nibbles, index (dir*16 + seg*4 + edge): dir 0 = vertical edges;
+//            the four edges crossed by one line are one 16-bit word
+//   [16..63] 8 bytes per (plane*3 + class), plane 0 luma / 1 chroma, class
+//            0 internal / 1 left MB edge / 2 top MB edge:
+//            {alpha, beta, tc0(bS=1), tc0(bS=2), tc0(bS=3), indexA, 0, 0}
+// Reference: GetBoundaryStrengths deblocking.c:1134-1370,
+// GetLumaEdgeThresholds :1381-1449, GetChromaEdgeThresholds :1460-1532.
+// ---------------------------------------------------------------------------
+__device__ void mb_dbrec(const ReconArgs &a, int gmb, int mb, const MbRec &q, int lane, uint8_t *out)
 {
-    const int p = blockIdx.x / a.diag_len;
-    const int k = blockIdx.x - p * a.diag_len;
-    if (p >= a.npics) return;
-    const int t = a.diag;
-    const int r_lo = max(0, (t - (a.w - 1) + 1) >> 1);
-    const int mby = r_lo + k;
-    const int mbx = t - 2 * mby;
-    if (mby >= a.h || mbx < 0 || mbx >= a.w) return;
-    const PicDesc pd = a.pics[p];
-    const int mb = mby * a.w + mbx;
-    const int gmb = pd.rec_base + mb;
-    const MbRec &q = a.rec[gmb];
-    const bool intra = q.type >= MBT_I4x4;
-    const bool dbf = q.avail & DB_INNER;
-    if (!intra && !dbf) return;
-    const int lane = threadIdx.x;
-    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
-    uint8_t *cur = a.frames + (unsigned long long)(pd.frame_base + pd.cur_slot) * a.frame_bytes;
-    uint8_t *curU = cur + (size_t)W16 * H16;
-    uint8_t *curV = curU + (size_t)CW * CH;
-
-    __shared__ int16_t s_res[384];
-    __shared__ int32_t s_dc[24];
-    __shared__ uint8_t s_ty[17 * TY_STRIDE];
-    __shared__ uint8_t s_tu[9 * TC_STRIDE];
-    __shared__ uint8_t s_tv[9 * TC_STRIDE];
-    __shared__ uint8_t s_dy[20 * DY_S];
-    __shared__ uint8_t s_du[10 * DC_S];
-    __shared__ uint8_t s_dv[10 * DC_S];
-    __shared__ int8_t s_bs[2][4][4];
-    __shared__ int s_err;
-
-    // ---------------------------------------------------------- intra recon
-    if (intra) {
-        if (lane == 0) s_err = 0;
-        if (q.type == MBT_IPCM) {
-            const uint8_t *src = (const uint8_t *)(a.coef + ((size_t)pd.coef_base + q.coef) * 16);
-            for (int i = lane; i < 256; i += WAVE) s_ty[((i >> 4) + 1) * TY_STRIDE + (i & 15) + 1] = src[i];
-            for (int i = lane; i < 64; i += WAVE) {
-                s_tu[((i >> 3) + 1) * TC_STRIDE + (i & 7) + 1] = src[256 + i];
-                s_tv[((i >> 3) + 1) * TC_STRIDE + (i & 7) + 1] = src[320 + i];
-            }
-            __syncthreads();
-        } else {
-            int e = 0;
-            if (q.cbits) mb_residual(q, a.coef + (size_t)pd.coef_base * 16, s_res, s_dc, lane, &e);
-            else { for (int i = lane; i < 384; i += WAVE) s_res[i] = 0; __syncthreads(); }
-            if (e) s_err = 1;
-            intra_mb(q, a.edges, gmb, mbx, a.w, s_res, s_ty, s_tu, s_tv, lane);
-        }
-        // edge buffer of this MB (unfiltered), from the tile
-        write_edges(a.edges + (size_t)gmb * 64, s_ty + TY_STRIDE + 1, TY_STRIDE, s_tu + TC_STRIDE + 1,
-                    s_tv + TC_STRIDE + 1, TC_STRIDE, lane);
-        if (!dbf) {
-            // write the MB straight out
-            const int row = lane >> 2, qd = lane & 3;
-            for (int x = 0; x < 4; x++)
-                cur[(size_t)(mby * 16 + row) * W16 + mbx * 16 + qd * 4 + x] = s_ty[(row + 1) * TY_STRIDE + 1 + qd * 4 + x];
-            if (lane < 32) {
-                const int comp = lane >> 4, crow = (lane >> 1) & 7, cq = lane & 1;
-                uint8_t *cp = comp ? curV : curU;
-                const uint8_t *T = comp ? s_tv : s_tu;
-                for (int x = 0; x < 4; x++)
-                    cp[(size_t)(mby * 8 + crow) * CW + mbx * 8 + cq * 4 + x] = T[(crow + 1) * TC_STRIDE + 1 + cq * 4 + x];
-            }
-            if (lane == 0 && s_err) atomicOr(a.err + p, 1u);
-            return;
-        }
-    }
-
-    // -------------------------------------------------------------- deblock
+    __shared__ uint8_t s_db[64];
     const bool fl = q.avail & DB_LEFT, ft = q.avail & DB_TOP;
-    // load region into LDS
-    for (int i = lane; i < 20 * 20; i += WAVE) {
-        const int ry = i / 20 - 4, rx = i % 20 - 4;
-        uint8_t v = 0;
-        if (ry >= 0 && rx >= 0) {
-            v = intra ? s_ty[(ry + 1) * TY_STRIDE + rx + 1] : cur[(size_t)(mby * 16 + ry) * W16 + mbx * 16 + rx];
-        } else if (ry < 0 && rx >= 0) {
-            if (ft) v = cur[(size_t)(mby * 16 + ry) * W16 + mbx * 16 + rx];
-        } else if (rx < 0 && ry >= 0) {
-            if (fl) v = cur[(size_t)(mby * 16 + ry) * W16 + mbx * 16 + rx];
-        }
-        s_dy[(ry + 4) * DY_S + rx + 4] = v;
-    }
-    for (int i = lane; i < 2 * 10 * 12; i += WAVE) {
-        const int comp = i / 120, j = i - comp * 120;
-        const int ry = j / 12 - 2, rx = j % 12 - 4;
-        uint8_t *cp = comp ? curV : curU;
-        const uint8_t *T = comp ? s_tv : s_tu;
-        uint8_t v = 0;
-        if (ry >= 0 && rx >= 0) v = intra ? T[(ry + 1) * TC_STRIDE + rx + 1] : cp[(size_t)(mby * 8 + ry) * CW + mbx * 8 + rx];
-        else if (ry < 0 && rx >= 0) { if (ft) v = cp[(size_t)(mby * 8 + ry) * CW + mbx * 8 + rx]; }
-        else if (rx < 0 && ry >= 0) { if (fl) v = cp[(size_t)(mby * 8 + ry) * CW + mbx * 8 + rx]; }
-        (comp ? s_dv : s_du)[(ry + 2) * DC_S + rx + 4] = v;
-    }
-    // boundary strengths: lane -> (dir, edge, segment)
     if (lane < 32) {
-        const int dir = lane >> 4, e = (lane >> 2) & 3, kk = lane & 3;
+        const int dir = lane >> 4, kk = (lane >> 2) & 3, e = lane & 3;
         int bS = 0;
-        const bool on = e > 0 || (dir == 0 ? fl : ft);
+        const bool on = (q.avail & DB_INNER) && (e > 0 || (dir == 0 ? fl : ft));
         if (on) {
             const MbRec &pm = e > 0 ? q : (dir == 0 ? a.rec[gmb - 1] : a.rec[gmb - a.w]);
             const int bq = dir == 0 ? blk_of(e, kk) : blk_of(kk, e);
-            const int bp = e == 0 ? (dir == 0 ? blk_of(3, kk) : blk_of(kk, 3)) : (dir == 0 ? blk_of(e - 1, kk) : blk_of(kk, e - 1));
+            const int bp = e == 0 ? (dir == 0 ? blk_of(3, kk) : blk_of(kk, 3))
+                                  : (dir == 0 ? blk_of(e - 1, kk) : blk_of(kk, e - 1));
             bS = bs_of(pm, bp, q, bq, e == 0);
         }
-        s_bs[dir][e][kk] = (int8_t)bS;
+        // pack two nibbles per byte: even lane owns the low nibble
+        const int hi = __shfl_down(bS, 1, 64);
+        if (!(lane & 1)) s_db[lane >> 1] = (uint8_t)(bS | (hi << 4));
+    } else if (lane < 38) {
+        const int k = lane - 32;               // 0..2 luma classes, 3..5 chroma
+        const bool chroma = k >= 3;
+        const int cls = chroma ? k - 3 : k;
+        int qpp;
+        if (cls == 0) qpp = chroma ? q.qpc : q.qp;
+        else {
+            const bool has = cls == 1 ? fl : ft;
+            const MbRec *pm = has ? &a.rec[cls == 1 ? gmb - 1 : gmb - a.w] : &q;
+            qpp = chroma ? pm->qpc : pm->qp;
+        }
+        const int qq = chroma ? q.qpc : q.qp;
+        const int qpav = (qpp + qq + 1) >> 1;
+        const int ia = clip3(0, 51, qpav + q.offA), ib = clip3(0, 51, qpav + q.offB);
+        uint8_t *o = s_db + 16 + k * 8;
+        o[0] = cAlpha[ia];
+        o[1] = cBeta[ib];
+        o[2] = cTc0[ia][0];
+        o[3] = cTc0[ia][1];
+        o[4] = cTc0[ia][2];
+        o[5] = (uint8_t)ia;
+        o[6] = o[7] = 0;
     }
-    __syncthreads();
+    wave_sync();
+    if (lane < 16) ((uint32_t *)out)[lane] = ((const uint32_t *)s_db)[lane];
+    (void)mb;
+}
 
-    const int qp_left = fl ? a.rec[gmb - 1].qp : 0, qpc_left = fl ? a.rec[gmb - 1].qpc : 0;
-    const int qp_top = ft ? a.rec[gmb - a.w].qp : 0, qpc_top = ft ? a.rec[gmb - a.w].qpc : 0;
-    for (int dir = 0; dir < 2; dir++) {
-        for (int e = 0; e < 4; e++) {
-            if (lane < 16) {
-                const int kk = lane >> 2;
-                const int bS = s_bs[dir][e][kk];
-                if (bS) {
-                    const int qpp = e > 0 ? q.qp : (dir == 0 ? qp_left : qp_top);
-                    const int qpav = (qpp + q.qp + 1) >> 1;
-                    const int ia = clip3(0, 51, qpav + q.offA), ib = clip3(0, 51, qpav + q.offB);
-                    const int tc0 = bS < 4 ? cTc0[ia][bS - 1] : 0;
-                    uint8_t *s = dir == 0 ? &s_dy[(lane + 4) * DY_S + e * 4 + 4] : &s_dy[(e * 4 + 4) * DY_S + lane + 4];
-                    filt_luma(s, dir == 0 ? 1 : DY_S, bS, cAlpha[ia], cBeta[ib], tc0);
-                }
-            } else if (lane < 32 && !(e & 1)) {
-                const int comp = (lane - 16) >> 3, i = (lane - 16) & 7;
-                const int bS = s_bs[dir][e][i >> 1];
-                if (bS) {
-                    const int qpp = e > 0 ? q.qpc : (dir == 0 ? qpc_left : qpc_top);
-                    const int qpav = (qpp + q.qpc + 1) >> 1;
-                    const int ia = clip3(0, 51, qpav + q.offA), ib = clip3(0, 51, qpav + q.offB);
-                    const int tc0 = bS < 4 ? cTc0[ia][bS - 1] : 0;
-                    uint8_t *D = comp ? s_dv : s_du;
-                    const int ce = e >> 1;
-                    uint8_t *s = dir == 0 ? &D[(i + 2) * DC_S + ce * 4 + 4] : &D[(ce * 4 + 2) * DC_S + i + 4];
-                    filt_chroma(s, dir == 0 ? 1 : DC_S, bS, cAlpha[ia], cBeta[ib], tc0);
-                }
-            }
-            __syncthreads();
+// ---------------------------------------------------------------------------
+// k_mb: every MB of the batch in parallel (one wave per MB)
+//   all MBs : deblocking record
+//   inter   : residual + 6-tap/bilinear MC + clip-add + write-out
+//   intra   : residual -> scratch (consumed by k_rows)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_mb(ReconArgs a)
+{
+    const int nmbs = a.w * a.h;
+    const int gidx = blockIdx.x;
+    const int p = gidx / nmbs;
+    const int mb = gidx - p * nmbs;
+    if (p >= a.npics) return;
+    const PicDesc pd = a.pics[p];
+    const int gmb = pd.rec_base + mb;
+    const MbRec &r = a.rec[gmb];
+    const int lane = threadIdx.x;
+
+    __shared__ int16_t s_res[384];
+    __shared__ int32_t s_dc[24];
+    __shared__ uint8_t s_win[16 * 81];
+    __shared__ uint8_t s_cwin[2][16][9];
+    __shared__ uint8_t s_out[384];
+
+    mb_dbrec(a, gmb, mb, r, lane, a.dbrec + (size_t)gmb * 64);
+
+    if (r.type >= MBT_I4x4) {
+        if (r.type != MBT_IPCM && r.cbits) {
+            int e = 0;
+            mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, s_dc, lane, &e);
+            uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
+            const uint32_t *src = (const uint32_t *)s_res;
+            for (int i = lane; i < 192; i += WAVE) dst[i] = src[i];
+            if (e && lane == 0) atomicOr(a.err + p, 1u);
+        }
+        return;
+    }
+
+    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
+    const int mbx = mb % a.w, mby = mb / a.w;
+    const uint8_t *frames = a.frames;
+    int e = 0;
+    if (r.cbits) {
+        mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, s_dc, lane, &e);
+    } else {
+        for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
+    }
+
+    // stage luma windows: 16 blocks x 9x9
+    for (int idx = lane; idx < 16 * 81; idx += WAVE) {
+        const int b = idx / 81, rem = idx - b * 81;
+        const int wy = rem / 9, wx = rem - wy * 9;
+        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes;
+        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
+        const int x = clip3(0, W16 - 1, mbx * 16 + blk_x(b) * 4 + (mvx >> 2) - 2 + wx);
+        const int y = clip3(0, H16 - 1, mby * 16 + blk_y(b) * 4 + (mvy >> 2) - 2 + wy);
+        s_win[idx] = ref[y * W16 + x];
+    }
+    // chroma windows: 16 blocks x 2 comps x 3x3
+    for (int idx = lane; idx < 16 * 2 * 9; idx += WAVE) {
+        const int b = idx / 18, rem = idx - b * 18;
+        const int comp = rem / 9, k = rem - comp * 9;
+        const int wy = k / 3, wx = k - wy * 3;
+        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes +
+                             (unsigned long long)W16 * H16 + (unsigned long long)comp * CW * CH;
+        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
+        const int x = clip3(0, CW - 1, mbx * 8 + blk_x(b) * 2 + (mvx >> 3) + wx);
+        const int y = clip3(0, CH - 1, mby * 8 + blk_y(b) * 2 + (mvy >> 3) + wy);
+        s_cwin[comp][b][k] = ref[y * CW + x];
+    }
+    wave_sync();
+
+    {   // luma: lane -> (block, row)
+        const int b = lane >> 2, yy = lane & 3;
+        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
+        int o[4];
+        luma_row4(s_win + b * 81, yy, mvx & 3, mvy & 3, o);
+        const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
+#pragma unroll
+        for (int x = 0; x < 4; x++) s_out[by * 16 + bx + x] = (uint8_t)clip255(o[x] + s_res[by * 16 + bx + x]);
+    }
+    {   // chroma: lane -> (block, comp, row), 2 samples
+        const int b = lane >> 2, comp = (lane >> 1) & 1, yy = lane & 1;
+        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
+        const int fx = mvx & 7, fy = mvy & 7;
+        const uint8_t *w = s_cwin[comp][b];
+        const int cx = blk_x(b) * 2, cy = blk_y(b) * 2 + yy;
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            const int A = w[yy * 3 + x], B = w[yy * 3 + x + 1], C = w[(yy + 1) * 3 + x], D = w[(yy + 1) * 3 + x + 1];
+            const int v = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
+            s_out[256 + comp * 64 + cy * 8 + cx + x] = (uint8_t)clip255(v + s_res[256 + comp * 64 + cy * 8 + cx + x]);
         }
     }
-    // write back: MB + modified halo (top 3 rows if ft, left 3 cols if fl)
-    for (int i = lane; i < 20 * 20; i += WAVE) {
-        const int ry = i / 20 - 4, rx = i % 20 - 4;
-        bool w = false;
-        if (ry >= 0 && rx >= 0) w = true;
-        else if (ry < 0 && rx >= 0) w = ft && ry >= -3;
-        else if (rx < 0 && ry >= 0) w = fl && rx >= -3;
-        if (w) cur[(size_t)(mby * 16 + ry) * W16 + mbx * 16 + rx] = s_dy[(ry + 4) * DY_S + rx + 4];
+    wave_sync();
+
+    uint8_t *cur = a.frames + (unsigned long long)(pd.frame_base + pd.cur_slot) * a.frame_bytes;
+    {
+        const int row = lane >> 2, q4 = lane & 3;
+        *(uint32_t *)(cur + (size_t)(mby * 16 + row) * W16 + mbx * 16 + q4 * 4) = *(const uint32_t *)(s_out + row * 16 + q4 * 4);
     }
-    for (int i = lane; i < 2 * 10 * 12; i += WAVE) {
-        const int comp = i / 120, j = i - comp * 120;
-        const int ry = j / 12 - 2, rx = j % 12 - 4;
-        bool w = false;
-        if (ry >= 0 && rx >= 0) w = true;
-        else if (ry < 0 && rx >= 0) w = ft && ry >= -1;
-        else if (rx < 0 && ry >= 0) w = fl && rx >= -1;
-        if (w) (comp ? curV : curU)[(size_t)(mby * 8 + ry) * CW + mbx * 8 + rx] = (comp ? s_dv : s_du)[(ry + 2) * DC_S + rx + 4];
+    if (lane < 32) {
+        const int comp = lane >> 4, row = (lane >> 1) & 7, q2 = lane & 1;
+        uint8_t *cp = cur + (size_t)W16 * H16 + (size_t)comp * CW * CH;
+        *(uint32_t *)(cp + (size_t)(mby * 8 + row) * CW + mbx * 8 + q2 * 4) =
+            *(const uint32_t *)(s_out + 256 + comp * 64 + row * 8 + q2 * 4);
     }
-    if (intra && lane == 0 && s_err) atomicOr(a.err + p, 1u);
+    if (lane == 0 && e) atomicOr(a.err + p, 1u);
+}
+
+// ---------------------------------------------------------------------------
+// intra reconstruction of one MB inside a wave-private tile whose 1-sample
+// halo (top row incl. top-left/top-right, left column) is already filled.
+// ---------------------------------------------------------------------------
+// I4x4 sub-wavefront: step -> (block of slot 0, block of slot 1), one nibble
+// per step; slot 1 uses 15 for "none" (block 15 is always slot 0)
+//   {0,-} {1,-} {4,2} {5,3} {6,8} {7,9} {12,10} {13,11} {14,-} {15,-}
+#define I4SCHED0 0xFEDC765410ull
+#define I4SCHED1 0xFFBA9832FFull
+
+__device__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
+                           uint8_t *ty, uint8_t *tu, uint8_t *tv, int lane)
+{
+    const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C;
+    if (mbtype == MBT_I16) {
+        const int mode = pred & 3;
+        const int y = lane >> 2, x0 = (lane & 3) * 4;
+        int dcv = 128, pa = 0, pb = 0, pc = 0;
+        if (mode == 2) {
+            int st = 0, sl = 0;
+            for (int i = 0; i < 16; i++) { st += ty[1 + i]; sl += ty[(i + 1) * TY_STRIDE]; }
+            if (aA && aB) dcv = (st + sl + 16) >> 5;
+            else if (aA) dcv = (sl + 8) >> 4;
+            else if (aB) dcv = (st + 8) >> 4;
+        } else if (mode == 3) {
+            int H = 0, V = 0;
+            for (int i = 0; i < 8; i++) {
+                H += (i + 1) * ((int)ty[1 + 8 + i] - (int)ty[1 + 6 - i]);
+                V += (i + 1) * ((int)ty[(1 + 8 + i) * TY_STRIDE] - (int)ty[(1 + 6 - i) * TY_STRIDE]);
+            }
+            pa = 16 * ((int)ty[16 * TY_STRIDE] + (int)ty[16]);
+            pb = (5 * H + 32) >> 6;
+            pc = (5 * V + 32) >> 6;
+        }
+        int pv[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int x = x0 + i;
+            int pr;
+            if (mode == 0) pr = ty[1 + x];
+            else if (mode == 1) pr = ty[(y + 1) * TY_STRIDE];
+            else if (mode == 2) pr = dcv;
+            else pr = clip255((pa + pb * (x - 7) + pc * (y - 7) + 16) >> 5);
+            pv[i] = clip255(pr + (has_res ? res[y * 16 + x] : 0));
+        }
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 4; i++) ty[(y + 1) * TY_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
+    } else {
+#pragma unroll 1
+        for (int step = 0; step < 10; step++) {
+            const int slot = lane >> 4;
+            int v = 0;
+            int b = -1;
+            if (slot == 0) b = (int)(I4SCHED0 >> (step * 4)) & 15;
+            else if (slot == 1) { b = (int)(I4SCHED1 >> (step * 4)) & 15; if (b == 15) b = -1; }
+            const int px = lane & 3, py = (lane >> 2) & 3;
+            if (b >= 0) {
+                const int bx = blk_x(b), by = blk_y(b);
+                const bool avL = bx > 0 || aA;
+                const bool avT = by > 0 || aB;
+                bool avTR;
+                if (b == 3 || b == 7 || b == 11 || b == 13 || b == 15) avTR = false;
+                else if (by == 0) avTR = bx == 3 ? aC : aB;
+                else avTR = true;
+                const int mode = (int)(i4 >> (b * 4)) & 15;
+                const uint8_t *T = ty + (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;
+                const int pr = i4_pred(T, TY_STRIDE, mode, px, py, avT, avL, avTR);
+                v = clip255(pr + (has_res ? res[(by * 4 + py) * 16 + bx * 4 + px] : 0));
+            }
+            wave_sync();
+            if (b >= 0) ty[(blk_y(b) * 4 + py + 1) * TY_STRIDE + blk_x(b) * 4 + px + 1] = (uint8_t)v;
+            wave_sync();
+        }
+    }
+    {   // chroma: lane -> (comp, row, pair)
+        const int comp = lane >> 5, y = (lane >> 2) & 7, x0 = (lane & 3) * 2;
+        uint8_t *T = comp ? tv : tu;
+        const int cmode = (pred >> 4) & 3;
+        int pv[2];
+        int pa = 0, pb = 0, pc = 0;
+        if (cmode == 3) {
+            int H = 0, V = 0;
+            for (int i = 0; i < 4; i++) {
+                H += (i + 1) * ((int)T[1 + 4 + i] - (int)T[1 + 2 - i]);
+                V += (i + 1) * ((int)T[(1 + 4 + i) * TC_STRIDE] - (int)T[(1 + 2 - i) * TC_STRIDE]);
+            }
+            pa = 16 * ((int)T[8 * TC_STRIDE] + (int)T[8]);
+            pb = (34 * H + 32) >> 6;
+            pc = (34 * V + 32) >> 6;
+        }
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+            const int x = x0 + i;
+            int pr;
+            if (cmode == 0) {
+                const int xo = x & 4, yo = y & 4;
+                int st = 0, sl = 0;
+                for (int k = 0; k < 4; k++) { st += T[1 + xo + k]; sl += T[(1 + yo + k) * TC_STRIDE]; }
+                if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) {
+                    pr = (aA && aB) ? (st + sl + 4) >> 3 : aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
+                } else if (xo > 0) {
+                    pr = aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
+                } else {
+                    pr = aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
+                }
+            } else if (cmode == 1) pr = T[(y + 1) * TC_STRIDE];
+            else if (cmode == 2) pr = T[1 + x];
+            else pr = clip255((pa + pb * (x - 3) + pc * (y - 3) + 16) >> 5);
+            pv[i] = clip255(pr + (has_res ? res[256 + comp * 64 + y * 8 + x] : 0));
+        }
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 2; i++) T[(y + 1) * TC_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
+    }
+    wave_sync();
+}
+
+// ---------------------------------------------------------------------------
+// k_rows: intra reconstruction + in-loop deblocking.  One single-wave
+// workgroup per MB row (grid = rows x pictures, blockIdx = row * npics + pic
+// so a picture's rows share one XCD under round-robin placement -- speed
+// only).  The wave walks its row left to right; MB (r,c) needs the row above
+// finished through (r-1,c+1) -- the raster-order dependencies of intra
+// prediction and h264bsdFilterPicture (deblocking.c:603-637).
+//
+// Row hand-off (row r -> row r+1) goes through a per-row mailbox in HBM,
+// 32 granules per MB column, each granule = {dword of data, launch epoch}
+// written by ONE 8-byte sc1 store (MI355X_MICROARCH.md, R2 granules: no
+// fence, no drain, no flag); the consumer re-reads with 8-byte sc1 loads
+// until every tag carries this launch's epoch.  Entry layout (dwords):
+//   [0..15]  luma rows 12..15 (final once the next MB's vertical edges ran)
+//   [16..23] Cb/Cr rows 6..7 (dword = comp*4 + row*2 + half)
+//   [24..31] unfiltered bottom row Y16 U8 V8 (intra neighbours of row r+1)
+// Every output sample is written exactly once, by the MB that finalises it,
+// so no other ordering of frame stores is needed.
+// ---------------------------------------------------------------------------
+#define RY_S 20       // region luma stride (cols -4..15)
+#define RC_S 12       // region chroma stride (cols -4..7)
+
+struct __attribute__((aligned(16))) RowLds {
+    int16_t res[384];
+    uint8_t db[64];
+    uint8_t ry[20 * RY_S];      // rows -4..15
+    uint8_t ru[10 * RC_S];      // rows -2..7
+    uint8_t rv[10 * RC_S];
+    uint8_t ty[17 * TY_STRIDE];
+    uint8_t tu[9 * TC_STRIDE];
+    uint8_t tv[9 * TC_STRIDE];
+    uint8_t left_unf[32];       // unfiltered right column of the previous MB: Y16 U8 V8
+};
+
+
+__device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn_sad_u8((unsigned)a, (unsigned)b, 0u); }
+
+// one sample line across edge k (p3..q3 = v[4k..4k+7]); chroma lines only
+// use p1..q1.  filterSamples / bS<4 / bS==4 of deblocking.c:1543-1736.  The
+// bS==4 arithmetic runs only when some lane of the wave has bS==4 on this
+// edge (wave-uniform branch); everything else is select-based.
+__device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int alpha, int beta, int tc0s,
+                                          bool chroma)
+{
+    const int o = 4 * k;
+    const int p2 = v[o + 1], p1 = v[o + 2], p0 = v[o + 3];
+    const int q0 = v[o + 4], q1 = v[o + 5], q2 = v[o + 6];
+    const int d0 = absd(p0, q0);
+    const bool f = bS != 0 && d0 < alpha && absd(p1, p0) < beta && absd(q1, q0) < beta;
+    const bool ap = !chroma && absd(p2, p0) < beta, aq = !chroma && absd(q2, q0) < beta;
+    // bS < 4
+    const int tc0 = (tc0s >> (((bS - 1) & 3) * 8)) & 255;
+    const int tc = tc0 + (chroma ? 1 : (int)ap + (int)aq);
+    const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+    const int avg = (p0 + q0 + 1) >> 1;
+    int r_p2 = p2, r_q2 = q2;
+    int r_p1 = f && ap ? p1 + clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1) : p1;
+    int r_q1 = f && aq ? q1 + clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1) : q1;
+    int r_p0 = f ? clip255(p0 + d) : p0;
+    int r_q0 = f ? clip255(q0 - d) : q0;
+    const bool b4 = f && bS >= 4;
+    if (__builtin_amdgcn_ballot_w64(b4) != 0) {
+        const int p3 = v[o], q3 = v[o + 7];
+        const bool strong = d0 < ((alpha >> 2) + 2);
+        const bool sp = ap && strong, sq = aq && strong;
+        const int s_p0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
+        const int s_q0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
+        r_p0 = b4 ? s_p0 : r_p0;
+        r_q0 = b4 ? s_q0 : r_q0;
+        r_p1 = b4 ? (sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1) : r_p1;
+        r_q1 = b4 ? (sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1) : r_q1;
+        r_p2 = b4 && sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : r_p2;
+        r_q2 = b4 && sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : r_q2;
+    }
+    v[o + 1] = r_p2; v[o + 2] = r_p1; v[o + 3] = r_p0;
+    v[o + 4] = r_q0; v[o + 5] = r_q1; v[o + 6] = r_q2;
+}
+
+// all edges of one direction: lanes 0..15 = luma lines, 16..31 = chroma
+// lines (comp = bit 3, index = bits 0..2).  dir 0: lines are rows, edges are
+// the 4 (chroma 2) vertical edges, left to right; dir 1: columns / horizontal
+// edges, top to bottom.  Each lane owns its line for all edges of the
+// direction, so no cross-lane ordering is needed inside a direction.  Lanes
+// 32..63 mirror lanes 0..31 (same addresses, same values) so that every
+// access is unconditional.
+__device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, uint8_t *ry, uint8_t *ru, uint8_t *rv,
+                                            int lane, bool mb_edge_on)
+{
+    const int li = lane & 31;
+    const bool chroma = li >= 16;
+    const int idx = chroma ? (li & 7) : (li & 15);
+    const int seg = chroma ? idx >> 1 : idx >> 2;
+    uint8_t *D = chroma ? ((li & 8) ? rv : ru) : ry;
+    const int S = chroma ? RC_S : RY_S;
+    // this line's four bS nibbles and the two threshold sets
+    const uint32_t bsw = *(const uint16_t *)(db + dir * 8 + seg * 2);
+    const uint8_t *pe = db + 16 + ((chroma ? 3 : 0) + 1 + dir) * 8;    // MB edge class
+    const uint8_t *pi = db + 16 + (chroma ? 3 : 0) * 8;                  // internal class
+    const uint2 te = *(const uint2 *)pe, ti = *(const uint2 *)pi;
+    int v[20];
+    if (dir == 0) {
+        const uint8_t *row = D + (idx + (chroma ? 2 : 4)) * S;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint32_t w = *(const uint32_t *)(row + (chroma ? min(j, 2) : j) * 4);
+            v[4 * j] = w & 255; v[4 * j + 1] = (w >> 8) & 255; v[4 * j + 2] = (w >> 16) & 255; v[4 * j + 3] = w >> 24;
+        }
+    } else {
+        // luma: region rows 0..19 = sample rows -4..15; chroma: region rows 0..9
+        // = sample rows -2..7, read into v[2..11]
+        const uint8_t *col = D + idx + 4;
+#pragma unroll
+        for (int j = 0; j < 20; j++) {
+            const int rr = chroma ? min(max(j - 2, 0), 9) : j;
+            v[j] = col[rr * S];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        // chroma edge k sits on luma edge 2k; chroma has no edges 2, 3
+        int b = (int)(bsw >> ((chroma ? 2 * k : k) * 4)) & 15;
+        if (chroma && k >= 2) b = 0;
+        if (k == 0 && !mb_edge_on) b = 0;
+        if (__builtin_amdgcn_ballot_w64(b != 0) == 0) continue;    // wave-uniform skip
+        const uint2 t = k == 0 ? te : ti;
+        filt_line(v, k, b, (int)(t.x & 255), (int)((t.x >> 8) & 255), (int)((t.x >> 16) | (t.y << 16)), chroma);
+    }
+    if (lane >= 32) return;
+    if (dir == 0) {
+        uint8_t *row = D + (idx + (chroma ? 2 : 4)) * S;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint32_t w = (uint32_t)v[4 * j] | ((uint32_t)v[4 * j + 1] << 8) | ((uint32_t)v[4 * j + 2] << 16) | ((uint32_t)v[4 * j + 3] << 24);
+            if (!chroma || j < 3) *(uint32_t *)(row + j * 4) = w;
+        }
+    } else {
+        uint8_t *col = D + idx + 4;
+#pragma unroll
+        for (int j = 1; j < 19; j++) {
+            if (!chroma) col[j * S] = (uint8_t)v[j];
+            else if (j == 3 || j == 4 || j == 7 || j == 8) col[(j - 2) * S] = (uint8_t)v[j];
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_gran(unsigned long long *p, uint32_t v, uint32_t tag)
+{
+    __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(64) void k_rows(ReconArgs a)
+{
+    __shared__ RowLds L;
+    const int p = blockIdx.x % a.npics, r = blockIdx.x / a.npics;
+    const int W = a.w, H = a.h;
+    if (r >= H) return;
+    const int lane = threadIdx.x;
+    const PicDesc *pdp = a.pics + p;
+    const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
+    const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
+    const int coef_base = __builtin_amdgcn_readfirstlane(pdp->coef_base);
+    const int W16 = W * 16, H16 = H * 16, CW = W16 / 2, CH = H16 / 2;
+    uint8_t *cur = a.frames + (unsigned long long)fslot * a.frame_bytes;
+    uint8_t *curU = cur + (size_t)W16 * H16;
+    uint8_t *curV = curU + (size_t)CW * CH;
+    unsigned *perr = a.err + p;
+    const uint32_t tag = a.epoch;
+    const bool has_up = r > 0, has_down = r + 1 < H;
+    const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
+    unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
+    const bool last_row = r == H - 1;
+    const uint32_t *recw = (const uint32_t *)(a.rec + rec_base + r * W);   // 24 dwords per record
+
+    // lane roles for dword transfers
+    const int orow = lane >> 2, oq = lane & 3;                                   // luma 16x16
+    const int li = lane & 31;
+    const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;          // chroma (lanes 32..63 mirror)
+    const size_t yoff = (size_t)(r * 16 + orow) * W16 + oq * 4;
+    const size_t coff = (size_t)(r * 8 + crow) * CW + cq * 4;
+    uint8_t *cplane = ccomp ? curV : curU;
+    // top-entry fetch lane map: lanes 0..31 entry c dword lane; 32: entry c+1
+    // dword 24; 33..35: entry c-1 dwords 27/29/31; others: dummy (entry c dword 0)
+    const int tsel = lane < 32 ? 0 : lane == 32 ? 1 : lane < 36 ? 2 : 0;
+    const int tdw = lane < 32 ? lane : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 0;
+
+    // prefetch registers for MB (r, 0)
+    uint32_t n_db, n_y, n_c, n_r0, n_r1, n_r2;
+    uint32_t n_h0, n_h1, n_h2, n_h3, n_h4, n_h5;   // record dwords 0..5 (uniform)
+    {
+        const int g0 = rec_base + r * W;
+        n_db = ((const uint32_t *)(a.dbrec + (size_t)g0 * 64))[lane & 15];
+        n_y = *(const uint32_t *)(cur + yoff);
+        n_c = *(const uint32_t *)(cplane + coff);
+        const uint32_t *rs = (const uint32_t *)(a.res + (size_t)g0 * 384);
+        n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+        n_h0 = recw[0]; n_h1 = recw[1]; n_h2 = recw[2]; n_h3 = recw[3]; n_h4 = recw[4]; n_h5 = recw[5];
+    }
+    unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    const bool prof = a.prof != nullptr;
+    const unsigned long long tstart = prof ? wall_clock64() : 0;
+    uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
+
+    for (int c = 0; c < W; c++) {
+        const uint32_t db_w = n_db, own_y = n_y, own_c = n_c, res0 = n_r0, res1 = n_r1, res2 = n_r2;
+        const uint32_t h0 = __builtin_amdgcn_readfirstlane(n_h0), h1 = __builtin_amdgcn_readfirstlane(n_h1);
+        const uint32_t cbits = __builtin_amdgcn_readfirstlane(n_h2), qcoef = __builtin_amdgcn_readfirstlane(n_h3);
+        const uint64_t i4 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(n_h5) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(n_h4);
+        const int qtype = h0 & 255, avail = (h0 >> 24) & 255, pred = h1 & 255;
+        const bool intra = qtype >= MBT_I4x4;
+        const bool dbf = avail & DB_INNER;
+        unsigned long long tc0 = prof ? clock64() : 0, tc1;
+        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 8 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
+        if (prof && lane == 0) pmb[0] = wall_clock64();
+        // ---- prefetch MB (r, c+1) (clamped: the last iteration re-reads MB W-1)
+        {
+            const int cn = min(c + 1, W - 1);
+            const int gn = rec_base + r * W + cn;
+            n_db = ((const uint32_t *)(a.dbrec + (size_t)gn * 64))[lane & 15];
+            n_y = *(const uint32_t *)(cur + yoff + cn * 16);
+            n_c = *(const uint32_t *)(cplane + coff + cn * 8);
+            const uint32_t *rs = (const uint32_t *)(a.res + (size_t)gn * 384);
+            n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+            const uint32_t *rw = recw + cn * 24;
+            n_h0 = rw[0]; n_h1 = rw[1]; n_h2 = rw[2]; n_h3 = rw[3]; n_h4 = rw[4]; n_h5 = rw[5];
+        }
+        // ---- own samples / residual / deblocking record into LDS
+        if (lane < 16) ((uint32_t *)L.db)[lane] = db_w;
+        if (qtype == MBT_IPCM) {
+            const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)coef_base + qcoef) * 16);
+            const uint32_t py = src[lane], pc = src[64 + li];
+            *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = py;
+            if (lane < 32) *(uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4] = pc;
+        } else if (!intra) {
+            *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = own_y;
+            if (lane < 32) *(uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4] = own_c;
+        } else if (cbits) {
+            ((uint32_t *)L.res)[lane] = res0;
+            ((uint32_t *)L.res)[64 + lane] = res1;
+            ((uint32_t *)L.res)[128 + lane] = res2;
+        }
+
+        // ---- row above: wait until entry c is final, then fetch it (+ the
+        //      neighbours' unfiltered samples for intra).  Intra MBs need it
+        //      before prediction; all others only before the horizontal edges.
+        // speculative read of the granules; re-read until all carry this epoch
+        const unsigned long long *tga = mbx_up + (size_t)(tsel == 0 ? c : tsel == 1 ? min(c + 1, W - 1) : max(c - 1, 0)) * 32 + tdw;
+        unsigned long long gr = 0;
+        if (has_up) gr = ld_gran(tga);
+        uint32_t top = 0;
+        auto fetch_top = [&]() {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_ballot_w64((uint32_t)(gr >> 32) != tag) != 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 18)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
+                gr = ld_gran(tga);
+            }
+            top = (uint32_t)gr;
+            if (prof && lane == 0) pmb[1] = wall_clock64();
+        };
+        const bool early = has_up && intra && qtype != MBT_IPCM;
+        if (early) fetch_top();
+        if (prof) { tc1 = clock64(); pt[0] += tc1 - tc0; tc0 = tc1; }
+
+        if (intra && qtype != MBT_IPCM) {
+            const bool aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
+            const uint32_t b0 = top & 255, b1 = (top >> 8) & 255, b2 = (top >> 16) & 255, b3 = top >> 24;
+            if (lane >= 24 && lane < 32) {
+                if (aB) {
+                    const int k = lane - 24;
+                    uint8_t *dst = k < 4 ? &L.ty[1 + k * 4] : (k < 6 ? &L.tu[1 + (k - 4) * 4] : &L.tv[1 + (k - 6) * 4]);
+                    dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
+                }
+            } else if (lane == 32) {
+                if (aC) { L.ty[17] = b0; L.ty[18] = b1; L.ty[19] = b2; L.ty[20] = b3; }
+            } else if (lane < 36) {
+                if (aD) (lane == 33 ? L.ty[0] : lane == 34 ? L.tu[0] : L.tv[0]) = b3;
+            } else if (lane >= 40 && lane < 56) L.ty[(lane - 39) * TY_STRIDE] = L.left_unf[lane - 40];
+            else if (lane >= 56) {
+                const int k = lane - 56;
+                L.tu[(k + 1) * TC_STRIDE] = L.left_unf[16 + k];
+                L.tv[(k + 1) * TC_STRIDE] = L.left_unf[24 + k];
+            }
+            wave_sync();
+            intra_tile(qtype, avail, pred, i4, L.res, cbits != 0, L.ty, L.tu, L.tv, lane);
+            {   // tile samples start at column 1: byte reads (LDS dword reads must be aligned)
+                const uint8_t *sy = &L.ty[(orow + 1) * TY_STRIDE + 1 + oq * 4];
+                *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = sy[0] | (sy[1] << 8) | (sy[2] << 16) | ((uint32_t)sy[3] << 24);
+            }
+            if (lane < 32) {
+                const uint8_t *T = ccomp ? L.tv : L.tu;
+                uint8_t *D = ccomp ? L.rv : L.ru;
+                const uint8_t *sp = &T[(crow + 1) * TC_STRIDE + 1 + cq * 4];
+                *(uint32_t *)&D[(crow + 2) * RC_S + 4 + cq * 4] = sp[0] | (sp[1] << 8) | (sp[2] << 16) | ((uint32_t)sp[3] << 24);
+            }
+        }
+        wave_sync();
+
+        // ---- unfiltered edges: bottom row (mailbox dwords 24..31), right column
+        uint32_t unf;
+        {
+            const int k = li & 7;     // lanes 24..31 (mirrored for the rest)
+            const uint8_t *ub = k < 4 ? &L.ry[19 * RY_S + 4 + k * 4] : k < 6 ? &L.ru[9 * RC_S + 4 + (k - 4) * 4] : &L.rv[9 * RC_S + 4 + (k - 6) * 4];
+            unf = *(const uint32_t *)ub;
+            const uint8_t *rcp = li < 16 ? &L.ry[(li + 4) * RY_S + 19] : li < 24 ? &L.ru[(li - 16 + 2) * RC_S + 11] : &L.rv[(li - 24 + 2) * RC_S + 11];
+            const uint8_t rc = *rcp;
+            wave_sync();
+            if (lane < 32) L.left_unf[lane] = rc;
+        }
+
+        // ---- vertical edges (need only this row's samples)
+        if (dbf) {
+            deblock_dir(0, L.db, L.ry, L.ru, L.rv, lane, avail & DB_LEFT);
+            wave_sync();
+        }
+        if (prof) { tc1 = clock64(); pt[1] += tc1 - tc0; tc0 = tc1; }
+
+        // ---- hand-off: entry c-1 is final now (only this MB's vertical edges
+        //      touch its columns 13..15): publish it, and the unfiltered row
+        //      of this MB's first four luma samples (the next row's top-right)
+        if (has_down) {
+            const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
+            const uint32_t patch = li < 16 ? *(const uint32_t *)&L.ry[(16 + (li >> 2)) * RY_S]
+                                           : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
+            const bool is_patch = li < 16 ? (li & 3) == 3 : (li < 24 && qq);
+            const uint32_t ent = is_patch ? patch : prov;
+            if (c > 0 && lane < 32) st_gran(mbx_me + (size_t)(c - 1) * 32 + lane, ent, tag);
+            if (lane == 24) st_gran(mbx_me + (size_t)c * 32 + 24, unf, tag);
+            if (prof && lane == 0) pmb[2] = wall_clock64();
+        }
+        if (prof) { tc1 = clock64(); pt[3] += tc1 - tc0; tc0 = tc1; }
+
+        // ---- top halo, horizontal edges
+        if (has_up) {
+            if (!early) fetch_top();
+            if (lane < 16) *(uint32_t *)&L.ry[orow * RY_S + 4 + oq * 4] = top;              // rows -4..-1
+            else if (lane < 24) {
+                const int k = lane - 16, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
+                *(uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4] = top;          // rows -2..-1
+            }
+            wave_sync();
+        }
+        if (prof) { tc1 = clock64(); pt[5] += tc1 - tc0; tc0 = tc1; }
+        if (dbf) {
+            deblock_dir(1, L.db, L.ry, L.ru, L.rv, lane, avail & DB_TOP);
+            wave_sync();
+        }
+        // provisional entry c (rows 12..15 final except columns 13..15)
+        if (has_down) {
+            const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
+            const uint32_t pl = *(const uint32_t *)&L.ry[(16 + ((li >> 2) & 3)) * RY_S + 4 + (li & 3) * 4];
+            const uint32_t pc = *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S + 4 + qq * 4];
+            prov = li < 16 ? pl : li < 24 ? pc : unf;
+        }
+        if (prof) { tc1 = clock64(); pt[2] += tc1 - tc0; tc0 = tc1; }
+
+        // ---- frame stores, once per sample
+        {
+            const int yrows = last_row ? 16 : 12;
+            const int crows = last_row ? 8 : 6;
+            const bool last_col = c == W - 1;
+            if (orow < yrows && (oq < 3 || last_col))
+                *(uint32_t *)(cur + yoff + c * 16) = *(const uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4];
+            if (lane < 32 && crow < crows && (cq == 0 || last_col))
+                *(uint32_t *)(cplane + coff + c * 8) = *(const uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4];
+            if (c > 0) {    // left halo: MB (r,c-1) luma cols 12..15 / chroma cols 4..7
+                if (lane < 16) {
+                    if (lane < yrows)
+                        *(uint32_t *)(cur + (size_t)(r * 16 + lane) * W16 + c * 16 - 4) = *(const uint32_t *)&L.ry[(lane + 4) * RY_S];
+                } else if (lane < 32) {
+                    const int k = lane - 16, comp = k >> 3, row = k & 7;
+                    if (row < crows)
+                        *(uint32_t *)((comp ? curV : curU) + (size_t)(r * 8 + row) * CW + c * 8 - 4) = *(const uint32_t *)&(comp ? L.rv : L.ru)[(row + 2) * RC_S];
+                }
+            }
+            if (has_up) {   // top halo: MB (r-1,c) luma rows 12..15, chroma rows 6..7 (now final)
+                if (lane >= 32 && lane < 48) {
+                    const int k = lane - 32;
+                    *(uint32_t *)(cur + (size_t)(r * 16 - 4 + (k >> 2)) * W16 + c * 16 + (k & 3) * 4) = *(const uint32_t *)&L.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4];
+                } else if (lane >= 48 && lane < 56) {
+                    const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
+                    *(uint32_t *)((comp ? curV : curU) + (size_t)(r * 8 - 2 + row) * CW + c * 8 + qq * 4) = *(const uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4];
+                }
+            }
+        }
+        wave_sync();
+        // ---- shift: this MB's cols 12..15 / 4..7 become the next MB's left halo
+        if (lane < 16) *(uint32_t *)&L.ry[(lane + 4) * RY_S] = *(const uint32_t *)&L.ry[(lane + 4) * RY_S + 16];
+        else if (lane < 32) {
+            const int k = lane - 16, comp = k >> 3, row = k & 7;
+            uint8_t *D = comp ? L.rv : L.ru;
+            *(uint32_t *)&D[(row + 2) * RC_S] = *(const uint32_t *)&D[(row + 2) * RC_S + 8];
+        }
+        wave_sync();
+        if (prof) { tc1 = clock64(); pt[4] += tc1 - tc0; }
+    }
+    // last entry of the row is final as it stands
+    if (has_down) {
+        if (lane < 32) st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, prov, tag);
+    }
+    if (prof && lane == 0) {
+        unsigned long long *o = a.prof + (size_t)blockIdx.x * 8;
+        o[0] = tstart; o[1] = wall_clock64();
+        for (int i = 0; i < 6; i++) o[2 + i] = pt[i];
+    }
 }

@@ -117,6 +117,16 @@ class Engine:
             return None
         return float(v[0]), float(v[1])
 
+    def set_timing(self, max_batches: int) -> None:
+        if self._L.h264mi_engine_set_timing(self._h, int(max_batches)) != 0:
+            raise RuntimeError("h264mi_engine_set_timing failed")
+
+    def timing_report(self):
+        a, b, n = C.c_double(), C.c_double(), C.c_int()
+        if self._L.h264mi_engine_timing_report(self._h, C.byref(a), C.byref(b), C.byref(n)) != 0:
+            return None
+        return a.value, b.value, n.value
+
     def close(self):
         if self._h:
             self._L.h264mi_engine_destroy(self._h)

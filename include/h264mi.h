@@ -141,8 +141,17 @@ int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);  
 int  h264mi_engine_sync(h264mi_engine *e);
 /* residual range errors seen since the last call (reference transform.c:181) */
 uint32_t h264mi_engine_errors(h264mi_engine *e);
-/* average duration (us) of the last batch's kernels: [0] k_inter, [1] k_wave sum */
+/* average duration (us) of the last batch's kernels: [0] k_mb, [1] k_rows */
 int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
+/* per-batch kernel timing with HIP events on the engine's stream:
+ * record up to max_batches batches (0 disables); the report syncs and returns
+ * the summed durations of k_mb and of k_rows, in microseconds */
+int  h264mi_engine_set_timing(h264mi_engine *e, int max_batches);
+int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches);
+/* diagnostics: per k_rows workgroup (row r of batch picture p at index
+ * r * npics + p) 8 u64: wall-clock start/end (100 MHz) and shader-clock sums
+ * of its phases; enable != 0 allocates, out != NULL copies the last launch */
+int  h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long long *out, size_t n);
 void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);          /* device pointer */
 size_t h264mi_engine_frame_bytes(h264mi_engine *e);
 

@@ -1,0 +1,49 @@
+"""Diagnostics: k_rows per-row phase clocks on the bench workload (not a test)."""
+import sys, os, ctypes as C, numpy as np
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench
+from broadway_amd import _lib
+from broadway_amd.engine import Engine
+L = _lib.mi()
+S = 8
+streams, caps = bench.prepare(3, [100 + i for i in range(S)], 6)
+w, h = caps[0].w_mbs, caps[0].h_mbs
+d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6)
+eng = Engine(w, h, S, nslots)
+L.h264mi_engine_profile(eng._h, 1, None, 0)
+for k in range(6):
+    eng.decode_device(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32)
+    eng.sync()
+    buf = (C.c_uint64 * (S * h * 8))()
+    L.h264mi_engine_profile(eng._h, 1, buf, S * h * 8)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(h, S, 8).astype(np.float64)
+    t0 = a[:, :, 0].min()
+    st = (a[:, :, 0] - t0) / 100.0   # us
+    en = (a[:, :, 1] - t0) / 100.0
+    ph = a[:, :, 2:8] / w            # cycles per MB
+    print(f"pic {k}: span {en.max():.1f} us; row start  r0 {st[0].mean():.1f} r1 {st[1].mean():.1f} r10 {st[10].mean():.1f} r67 {st[-1].mean():.1f}; "
+          f"row dur r0 {(en[0]-st[0]).mean():.1f} r34 {(en[34]-st[34]).mean():.1f} r67 {(en[-1]-st[-1]).mean():.1f}")
+    print("   cycles/MB  pre(+intra wait) %.0f  intra+V %.0f  H %.0f  publish %.0f  stores %.0f  top-wait %.0f" % tuple(ph.mean(axis=(0, 1))))
+    print("   row0 cycles/MB", " ".join("%.0f" % x for x in ph[0].mean(axis=0)), " row40", " ".join("%.0f" % x for x in ph[40].mean(axis=0)))
+
+# per-MB hand-off timing of the last picture batch (100 MHz clock -> us)
+buf = (C.c_uint64 * (S * h * 8 + S * w * h * 4))()
+L.h264mi_engine_profile(eng._h, 1, buf, len(buf))
+m = np.frombuffer(buf, dtype=np.uint64)[S * h * 8:].reshape(S, h, w, 4).astype(np.float64) / 100.0
+p0 = m[0]
+for r in (1, 2, 20, 40):
+    for c in (10, 60):
+        start, valid, pub = p0[r, c, 0], p0[r, c, 1], p0[r - 1, c + 1, 2]
+        print(f"row {r} col {c}: consumer start {start - p0[r-1, c, 0]:.2f}us after producer's start of same col; "
+              f"producer published entry {c} at +{pub - p0[r-1, c+1, 0]:.2f}us into its iter {c+1}; "
+              f"consumer saw it {valid - pub:.2f}us after publish; iter len {p0[r, c+1, 0] - p0[r, c, 0]:.2f}us")
+
+# per-row: duration, summed top-wait, own work (cycles/MB) for picture 0 of the last batch
+a = np.frombuffer(buf, dtype=np.uint64)[:S * h * 8].reshape(h, S, 8).astype(np.float64)
+t0 = a[:, :, 0].min()
+for r in range(h):
+    st = (a[r, 0, 0] - t0) / 100; en = (a[r, 0, 1] - t0) / 100
+    ph = a[r, 0, 2:8] / w
+    own = ph.sum() - ph[5]
+    xcc = ""
+    print(f"r{r:02d} start {st:7.1f} end {en:7.1f} dur {en-st:7.1f}  own {own:6.0f} cyc/MB  wait {ph[5]:6.0f}  [pre {ph[0]:.0f} V {ph[1]:.0f} H {ph[2]:.0f} pub {ph[3]:.0f} st {ph[4]:.0f}]")
