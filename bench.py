@@ -10,10 +10,15 @@ libh264mi.so) and the batches are uploaded to HBM before timing, so the timed
 region is the reconstruction hot path only (kernel-only fps).
 
 A *step* = one picture of each of the rank's 8 streams reconstructed on the
-GPU: k_inter (residual + motion compensation for all inter MBs of the 8
-pictures) followed by the k_wave anti-diagonal sweep (intra + deblocking).
-Steps follow decoding order, so the W warmup steps decode the first W
-pictures and the K timed steps the next K.
+GPU: k_mb (every MB in parallel: residual, 6-tap/bilinear motion compensation
+of inter MBs, deblocking records) followed by k_rows (one wave per MB row:
+intra prediction and in-loop deblocking, rows pipelined through HBM
+mailboxes).  Steps follow decoding order, so the W warmup steps decode the
+first W pictures and the K timed steps the next K.
+
+Bit-exactness: rank 0 checks the frames still resident in stream 0's slots
+against the reference decoder's per-frame MD5s (tests/golden/golden.json,
+made by running the reference C on the same generated streams).
 
 Multi-GPU: one process per GPU (torch.distributed.run), streams partitioned
 across ranks with no data-path collective (SURVEY.md §8e) -> "scaling": "weak";
@@ -54,6 +59,19 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     return ap.parse_args()
+
+
+def shard_seeds(rank: int, streams_per_gpu: int):
+    """Stream seeds of one rank: streams partition across ranks, no overlap."""
+    return [100 + rank * streams_per_gpu + i for i in range(streams_per_gpu)]
+
+
+def max_over_ranks(dist, torch, value: float) -> float:
+    if dist is None:
+        return value
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def dist_setup(gpus):
@@ -117,7 +135,7 @@ def upload(L, caps, nsteps):
 
 
 def inter_alg_bytes(caps, lo, hi):
-    """Algorithmic bytes of k_inter for pictures [lo, hi) of every stream:
+    """Algorithmic bytes of k_mb for pictures [lo, hi) of every stream:
     MC reference footprint (SURVEY §8d R_alg luma+chroma term), the
     coefficient blocks and records of inter MBs, and the 384-B write of every
     inter MB."""
@@ -141,10 +159,12 @@ def inter_alg_bytes(caps, lo, hi):
     return total, n_inter
 
 
-def cpu_baseline(streams, nframes):
+def cpu_baseline(streams, nframes, reps=10):
     """Reference C decoder (oracle/_ref/refdec, built from /root/reference
-    sources) when present, else the CPU oracle restatement; one decoder
-    process per stream, all streams in parallel."""
+    sources by oracle/Makefile.ref) when present, else the CPU oracle
+    restatement.  One decoder process per stream, all streams in parallel
+    (one host core each), each stream decoded `reps` times back to back:
+    a bounded sample of about 10 s of CPU work."""
     refdec = os.path.join(ROOT, "oracle", "_ref", "refdec")
     ncores = min(len(streams), os.cpu_count() or 1, 16)
     td = tempfile.mkdtemp(prefix="h264bench")
@@ -162,45 +182,61 @@ def cpu_baseline(streams, nframes):
             kind = "port"
             exe = os.path.join(ROOT, "oracle", "_build", "oracle_dec")
             cmd = lambda p: [exe, "-Onone", p]  # noqa: E731
-        t0 = time.perf_counter()
-        t_single = None
-        for batch_start in range(0, len(paths), ncores):
-            procs = [subprocess.Popen(cmd(p), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-                     for p in paths[batch_start:batch_start + ncores]]
-            for pr in procs:
-                pr.wait()
-        t1 = time.perf_counter()
-        # single-core rate on one stream
+
+        def run(pth):
+            for _ in range(reps):
+                subprocess.run(cmd(pth), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
+
         ts = time.perf_counter()
-        subprocess.run(cmd(paths[0]), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        subprocess.run(cmd(paths[0]), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, check=True)
         t_single = time.perf_counter() - ts
-        frames = nframes * len(paths)
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(max_workers=ncores) as ex:
+            list(ex.map(run, paths[:ncores]))
+        t1 = time.perf_counter()
+        frames = nframes * ncores * reps
+        try:
+            cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+        except (OSError, StopIteration):
+            cpu_model = "unknown"
         return {"value": round(frames / (t1 - t0), 2), "unit": "frames/s", "cores": ncores, "kind": kind,
-                "sample": f"{len(paths)} x {nframes}-frame 1080p streams, one decoder process per stream "
-                          f"on {ncores} host cores ({frames} frames, {t1 - t0:.1f}s); single core "
-                          f"{nframes / t_single:.1f} fps"}
+                "sample": f"{ncores} x {nframes}-frame 1080p streams x {reps} passes, one decoder process per "
+                          f"stream on {ncores} host cores ({frames} frames, {t1 - t0:.1f} s, {cpu_model}); "
+                          f"single core {nframes / t_single:.1f} fps"}
     finally:
         shutil.rmtree(td, ignore_errors=True)
 
 
-def verify(eng, caps, streams, n_decoded):
-    """Bit-exactness spot check: every slot still holding one of the last
-    decoded pictures of stream 0 vs the CPU oracle's frame of that picture."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+def verify(eng, caps, seeds, n_decoded):
+    """Bit-exactness: every slot of stream 0 still holding one of the decoded
+    pictures vs the reference decoder's MD5 of that picture (POC type 2:
+    output order == decode order)."""
+    gold = os.path.join(ROOT, "tests", "golden", "golden.json")
+    cases = json.load(open(gold))["cases"] if os.path.exists(gold) else {}
+    ref = cases.get(f"bench_1080p_s{seeds[0]}")
+    if ref is None:
+        return None, 0
     c = caps[0]
-    rep = O.Replay(c.w_mbs, c.h_mbs, c.nslots)
-    for k in range(n_decoded):
-        p = c.pictures[k]
-        rep.picture(p.rec, p.coef, p.cur_slot)
     last = {}
-    for k in range(n_decoded):
+    for k in range(min(n_decoded, len(ref["frames"]))):
         last[c.pictures[k].cur_slot] = k
     ok = True
     for slot, k in last.items():
-        if eng.read(0, slot).tobytes() != rep.frame(slot):
+        if hashlib.md5(eng.read(0, slot).tobytes()).hexdigest() != ref["frames"][k]:
             ok = False
     return ok, len(last)
+
+
+def load_traffic():
+    """HBM bytes per step from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.py -> profiles/traffic.json), or None."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p))
+    except ValueError:
+        return None
 
 
 def main():
@@ -211,7 +247,7 @@ def main():
     L = _lib.mi()
 
     S = a.streams
-    seeds = [100 + rank * S + i for i in range(S)]
+    seeds = shard_seeds(rank, S)
     nframes = a.warmup + a.steps
     t_prep = time.perf_counter()
     streams, caps = prepare(a.config, seeds, nframes)
@@ -242,32 +278,33 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
-    dt = t1 - t0
-    if dist:
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
-    inter_us, wave_us, nb = eng.timing_report()
+    dt = max_over_ranks(dist, torch, t1 - t0)
+    mb_us, rows_us, nb = eng.timing_report()
     errors = eng.errors()
 
     frames_total = S * a.steps * world
     fps = frames_total / dt
-    alg, n_inter = inter_alg_bytes(caps, a.warmup, a.warmup + a.steps)
-    per_launch_bytes = alg / a.steps
-    per_launch_us = inter_us / max(nb, 1)
-    achieved = per_launch_bytes / (per_launch_us * 1e-6) / 1e9 if per_launch_us > 0 else 0.0
-    # whole-frame read roofline of SURVEY §8d: R_alg = MC footprint + coefficients + records
+    # roofline: R_alg per frame = MC reference footprint + coded
+    # 4x4 blocks x 32 B + 96-B MB records; one step = one frame of each of
+    # the S streams; the reconstruction of a step is the k_mb + k_rows pair
     r_alg = 0
     for c in caps:
         for k in range(a.warmup, a.warmup + a.steps):
             p = c.pictures[k]
             r_alg += p.alg_ref_bytes + 32 * p.n_coded + MBREC * c.w_mbs * c.h_mbs
+    per_step_bytes = r_alg / a.steps
+    mb_us_avg, rows_us_avg = mb_us / max(nb, 1), rows_us / max(nb, 1)
+    step_us = mb_us_avg + rows_us_avg
+    achieved = per_step_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
+    kmb_alg, n_inter = inter_alg_bytes(caps, a.warmup, a.warmup + a.steps)
+    kmb_achieved = (kmb_alg / a.steps) / (mb_us_avg * 1e-6) / 1e9 if mb_us_avg > 0 else 0.0
+    traffic = load_traffic()
     frame_read_gbs = r_alg * world / dt / 1e9
 
     ok = None
     n_checked = 0
     if not a.no_verify and rank == 0:
-        ok, n_checked = verify(eng, caps, streams, nframes)
+        ok, n_checked = verify(eng, caps, seeds, nframes)
 
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
@@ -292,15 +329,20 @@ def main():
                        "streams_per_gpu": S, "total_streams": S * world,
                        "frames_per_stream_timed": a.steps, "seeds": f"100..{100 + S * world - 1}",
                        "parallelism": f"streams sharded {S}/GPU, no collective"},
-            "roofline": {"kernel": "k_inter", "bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None,
-                         "alg_bytes_per_launch": int(per_launch_bytes),
-                         "avg_launch_us": round(per_launch_us, 2)},
-            "kernel_time_us_per_step": {"k_inter": round(inter_us / max(nb, 1), 2),
-                                        "k_wave_sweep": round(wave_us / max(nb, 1), 2)},
-            "frame_read_roofline": {"R_alg_GBs": round(frame_read_gbs, 2),
-                                    "frac": round(frame_read_gbs / HBM_PEAK_GBS, 5)},
+            "roofline": {"kernel": "k_mb+k_rows (one reconstruction step)", "bound": "hbm",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
+                         "alg_bytes_per_step": int(per_step_bytes),
+                         "avg_step_kernel_us": round(step_us, 2),
+                         "traffic_source": traffic.get("source") if traffic else None},
+            "kernels": {"k_mb": {"avg_launch_us": round(mb_us_avg, 2),
+                                 "alg_bytes_per_launch": int(kmb_alg / a.steps),
+                                 "achieved_GBs": round(kmb_achieved, 1),
+                                 "frac": round(kmb_achieved / HBM_PEAK_GBS, 5)},
+                        "k_rows": {"avg_launch_us": round(rows_us_avg, 2),
+                                   "bound": "latency (MB-row dependency chain)"}},
+            "wall_read_GBs": round(frame_read_gbs, 2),
             "cpu_baseline": cpu,
             "bitexact_check": {"ok": ok, "frames_checked": n_checked, "residual_range_errors": errors},
             "prep_seconds": round(t_prep, 1),

@@ -42,6 +42,7 @@ void h264gen_default_params(GenParams *p, int w_mbs, int h_mbs)
     p->coef_pct = 50; p->level_tail_pct = 5;
     p->mv_jitter = 24; p->offpic_pct = 5;
     p->log2_max_frame_num = 8;
+    p->poc_swap = 0;
     p->seed = 1;
 }
 
@@ -672,6 +673,15 @@ static void gen_picture(Gen *g, int idx)
         g->nref = 0;
         g->poc_lsb = 0;
     }
+    {   /* display order: 2 * index in GOP, optionally swapped in pairs */
+        int k = idx % p->gop, d = k;
+        int last = p->gop - 1;
+        if (p->poc_swap && k >= 1) {
+            if ((k & 1) && k + 1 <= last) d = k + 1;
+            else if (!(k & 1)) d = k - 1;
+        }
+        g->poc_lsb = (2 * d) & 255;
+    }
     for (int i = 0; i < nmb; i++) g->pc.mb[i].slice = SLICE_NONE;
     g->gmx += rnd_range(&g->rng, -6, 6);
     g->gmy += rnd_range(&g->rng, -4, 4);
@@ -700,7 +710,6 @@ static void gen_picture(Gen *g, int idx)
     }
     if (idr) g->idr_id = (g->idr_id + 1) & 0xFFFF;
     g->frame_num = (g->frame_num + 1) & ((1 << p->log2_max_frame_num) - 1);
-    g->poc_lsb = (g->poc_lsb + 2) & 255;
     if (g->nref < p->num_ref_frames) g->nref++;
 }
 

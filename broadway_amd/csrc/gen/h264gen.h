@@ -38,6 +38,7 @@ typedef struct GenParams {
     int mv_jitter;                 /* per-MB motion spread, quarter-pel */
     int offpic_pct;                /* partitions forced to reference off-picture */
     int log2_max_frame_num;        /* 4..16 */
+    int poc_swap;                  /* POC type 0: swap display order of picture pairs (1,2),(3,4).. of a GOP */
     uint64_t seed;
 } GenParams;
 

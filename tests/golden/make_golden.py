@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/golden.json: per-frame MD5s of the REFERENCE decoder.
+
+Runs only in the build container, where oracle/_ref/refdec is built from the
+reference C sources (oracle/Makefile.ref; SURVEY.md §8c: the reference ships
+no test vectors, so parity is pinned by running it on identical input here).
+Every stream comes from the in-tree seeded generator; the fixture records the
+generator parameters, the stream's SHA-256 (so generator drift is detected)
+and the MD5 of every output frame (full MB-aligned I420 buffer, the
+DecTestBench -O output).  Nothing from the reference itself is stored.
+
+    python tests/golden/make_golden.py          # rewrites golden.json
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+# name -> (config, seed, overrides, no_reorder)
+CASES = {
+    # GPU parity cases (tests/test_gpu_parity.py SMALL)
+    "small_i_6x5": (1, 1, dict(nframes=3, w_mbs=6, h_mbs=5), False),
+    "small_ip_8x6_2sl": (2, 11, dict(nframes=8, w_mbs=8, h_mbs=6, crop_bottom=0, slices=2, gop=6), False),
+    "small_ip_11x9_cip": (2, 21, dict(nframes=8, w_mbs=11, h_mbs=9, crop_bottom=0, slices=3, cip=1, gop=4), False),
+    "small_ip_13x7_qpoff": (2, 33, dict(nframes=10, w_mbs=13, h_mbs=7, crop_bottom=0, slices=4, gop=5,
+                                        chroma_qp_offset=-7, num_ref_frames=3, dbf_idc1_pct=10,
+                                        dbf_idc2_pct=30, level_tail_pct=20), False),
+    "small_plumb_9x5": (0, 3, dict(nframes=6, w_mbs=9, h_mbs=5, crop_bottom=0), False),
+    # POC type 0 (output reordering through the DPB), with and without reordering
+    "poc0_reorder": (2, 41, dict(nframes=12, w_mbs=10, h_mbs=6, crop_bottom=0, poc_type=0, gop=6,
+                                 num_ref_frames=2, poc_swap=1), False),
+    "poc0_noreorder": (2, 41, dict(nframes=12, w_mbs=10, h_mbs=6, crop_bottom=0, poc_type=0, gop=6,
+                                   num_ref_frames=2, poc_swap=1), True),
+    "poc0_inorder": (2, 42, dict(nframes=9, w_mbs=7, h_mbs=5, crop_bottom=0, poc_type=0, gop=4), False),
+    # SURVEY §8d configs
+    "cfg1_plumbing_640x368": (0, 1, dict(nframes=30), False),
+    "cfg2_720p_ionly_s1": (1, 1, dict(nframes=4), False),
+    "cfg2_720p_ionly_idc1_s2": (1, 2, dict(nframes=3, dbf_idc1_pct=100), False),
+    "cfg5_2160p_s200": (4, 200, dict(nframes=4), False),
+}
+# bench.py streams: config 3, seeds 100..107, 60 frames (4 warmup + 56 timed)
+for s in range(100, 108):
+    CASES[f"bench_1080p_s{s}"] = (3, s, dict(nframes=60), False)
+
+
+def main():
+    from broadway_amd import gen
+    import oracle as O
+
+    out = {"generator": "broadway_amd.gen (libh264gen.so)",
+           "decoder": "reference C (Decoder/src, make.py file list + DecTestBench.c), gcc -O2",
+           "frame_md5": "MD5 of each output frame: full MB-aligned I420 (w*h*3/2 bytes), output order",
+           "cases": {}}
+    for name, (cfg, seed, ov, nr) in CASES.items():
+        stream = gen.generate(cfg, seed, **ov)
+        frames = O.refdec_frames(stream, no_reorder=nr)
+        p = gen.params(cfg, seed, **ov)
+        w, h = p.w_mbs * 16, p.h_mbs * 16
+        assert frames and all(len(f) == w * h * 3 // 2 for f in frames), name
+        out["cases"][name] = {
+            "config": cfg, "seed": seed, "overrides": ov, "no_reorder": nr,
+            "stream_bytes": len(stream), "stream_sha256": hashlib.sha256(stream).hexdigest(),
+            "width": w, "height": h,
+            "frames": [hashlib.md5(f).hexdigest() for f in frames],
+        }
+        print(f"{name}: {len(frames)} frames {w}x{h}", flush=True)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json"), "w") as f:
+        json.dump(out, f, indent=1)
+        f.write("\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,56 @@
+"""Multi-GPU path on CPU: world_size-2 gloo ranks run bench.py's sharding and
+timing reduction.  Streams partition across ranks with no data-path
+collective; the only exchange is the max over ranks of the
+timed region."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+    import bench
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    seeds = bench.shard_seeds(rank, 8)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, seeds)
+    t = bench.max_over_ranks(dist, torch, 1.0 + rank)
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, gathered, t))
+
+
+@pytest.mark.timeout(120)
+def test_two_rank_sharding_and_max():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, gathered, t in res:
+        assert t == 2.0                              # max over ranks
+        flat = [s for g in gathered for s in g]
+        assert len(flat) == len(set(flat)) == 16     # disjoint stream sets
+        assert sorted(flat) == list(range(100, 116))  # config 4: seeds 100.. 8 per GPU

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Summarise a gpu_round.sh session into profiles/:
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of the bench command
+  profiles/<tag>_pmc.json           FETCH_SIZE / WRITE_SIZE per launch (separate passes)
+  profiles/traffic.json             HBM bytes per reconstruction step (k_mb + k_rows),
+                                    read by bench.py for roofline.traffic
+
+Units and corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE / WRITE_SIZE are
+KiB; on gfx950 FETCH_SIZE counts 64 B per 128-B request, so it is doubled.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+    return {k: (sum(v) / len(v), len(v)) for k, v in d.items()}
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    fetch = per_launch(os.path.join(src, "pmc_fetch", "bench_counter_collection.csv"), "FETCH_SIZE")
+    write = per_launch(os.path.join(src, "pmc_write", "bench_counter_collection.csv"), "WRITE_SIZE")
+    kernels = {}
+    step = 0.0
+    for k in ("k_mb", "k_rows"):
+        f_kib, n = fetch[k]
+        w_kib, _ = write[k]
+        hbm = (2 * f_kib + w_kib) * 1024
+        kernels[k] = {"launches": n, "FETCH_SIZE_KiB": round(f_kib, 1), "WRITE_SIZE_KiB": round(w_kib, 1),
+                      "read_bytes_corrected": int(2 * f_kib * 1024), "write_bytes": int(w_kib * 1024),
+                      "hbm_bytes": int(hbm)}
+        step += hbm
+    out = {"tag": tag, "kernels": kernels,
+           "note": "FETCH_SIZE doubled per the gfx950 correction (calibrated for 16-B/lane streaming reads)"}
+    json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+    json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
+               "hbm_bytes_per_step": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    if os.path.exists(os.path.join(src, "bench.json")):
+        shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
