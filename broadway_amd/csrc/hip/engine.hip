@@ -369,6 +369,11 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
 {
     H264Backend be;
     memset(&be, 0, sizeof(be));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+        fprintf(stderr, "h264mi: no HIP device %d: the reconstruction path needs an MI355X\n", device);
+        return be;                                  /* ctx == NULL: H264SwDecInit fails */
+    }
     HipBackendCtx *c = (HipBackendCtx *)calloc(1, sizeof(HipBackendCtx));
     c->device = device;
     be.ctx = c;
