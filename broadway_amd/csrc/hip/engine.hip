@@ -144,7 +144,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     hipLaunchKernelGGL(k_mb, dim3(npics * e->nmbs), dim3(64), 0, e->st, a);
     HIPCHECK(hipGetLastError());
     if (rec) (void)hipEventRecord(t1, e->st);
-    hipLaunchKernelGGL(k_rows, dim3(npics * e->h), dim3(64), 0, e->st, a);
+    hipLaunchKernelGGL(k_rows, dim3(npics * ((e->h + ROWS_PER_WG - 1) / ROWS_PER_WG)), dim3(ROWS_PER_WG * 64), 0, e->st, a);
     HIPCHECK(hipGetLastError());
     if (rec) (void)hipEventRecord(t2, e->st);
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
@@ -274,7 +274,7 @@ extern "C" int h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long
                            hipMemcpyDeviceToHost));
     }
     if (enable && !e->d_prof) {
-        e->prof_cap = (size_t)e->nstreams * e->h * 8 + (size_t)e->nstreams * e->nmbs * 4;
+        e->prof_cap = (size_t)e->nstreams * e->h * 16 + (size_t)e->nstreams * e->nmbs * 4;
         HIPCHECK(hipMalloc(&e->d_prof, sizeof(unsigned long long) * e->prof_cap));
         HIPCHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * e->prof_cap));
     } else if (!enable && e->d_prof) {

@@ -39,7 +39,7 @@ struct ReconArgs {
     unsigned int *err;        // per picture: bit0 residual range error, bit1 wait timeout
     unsigned long long *mbx;  // row mailboxes: 32 tagged granules per MB of the batch (k_rows)
     unsigned int epoch;       // launch counter != 0: granule tag (no reset between launches)
-    unsigned long long *prof; // optional k_rows phase clocks: 8 per (row, picture) workgroup
+    unsigned long long *prof; // optional k_rows phase clocks: 16 per (row, picture) workgroup
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -65,11 +65,14 @@ __constant__ uint8_t cTc0[52][3] = {
 
 // ordering of LDS traffic between the lanes of one wave (waves of k_rows
 // work independently; k_mb workgroups are a single wave)
+// A wave's LDS instructions execute in issue order, so lanes of one wave see
+// each other's LDS writes once the compiler keeps program order: a compiler
+// barrier is enough (no s_waitcnt, which would also drain in-flight global
+// prefetches because vmcnt retires in order).
 __device__ __forceinline__ void wave_sync()
 {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
 }
 
 __device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
@@ -686,8 +689,15 @@ __device__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const i
 // Every output sample is written exactly once, by the MB that finalises it,
 // so no other ordering of frame stores is needed.
 // ---------------------------------------------------------------------------
+// MB rows (waves) per k_rows workgroup.  Rows inside a workgroup hand off
+// through an LDS ring, rows at band edges through HBM granules.  Measured at
+// 1080p x 8 streams (r01): 1 row 950 us, 2 rows 969, 4 rows 977, 8 rows 1025
+// per k_rows launch -- the row lag is set by the MB dependency chain, not by
+// the hand-off latency, and more waves per SIMD slow every row.
+#define ROWS_PER_WG 1
+#define RING_K 16     // LDS ring slots (MB columns) per in-workgroup row hand-off
 #define RY_S 20       // region luma stride (cols -4..15)
-#define RC_S 12       // region chroma stride (cols -4..7)
+#define RC_S 20       // region chroma stride (cols -4..7, padded to the luma stride)
 
 struct __attribute__((aligned(16))) RowLds {
     int16_t res[384];
@@ -760,29 +770,28 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
     const int idx = chroma ? (li & 7) : (li & 15);
     const int seg = chroma ? idx >> 1 : idx >> 2;
     uint8_t *D = chroma ? ((li & 8) ? rv : ru) : ry;
-    const int S = chroma ? RC_S : RY_S;
     // this line's four bS nibbles and the two threshold sets
     const uint32_t bsw = *(const uint16_t *)(db + dir * 8 + seg * 2);
     const uint8_t *pe = db + 16 + ((chroma ? 3 : 0) + 1 + dir) * 8;    // MB edge class
     const uint8_t *pi = db + 16 + (chroma ? 3 : 0) * 8;                  // internal class
     const uint2 te = *(const uint2 *)pe, ti = *(const uint2 *)pi;
+    // one stride for both planes (RC_S == RY_S): every access below is
+    // base + immediate.  Chroma lines read past their 12/10 samples into
+    // neighbouring LDS (values unused) and write back only what they own.
+    static_assert(RC_S == RY_S, "deblock_dir assumes one region stride");
     int v[20];
     if (dir == 0) {
-        const uint8_t *row = D + (idx + (chroma ? 2 : 4)) * S;
+        const uint32_t *row = (const uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
 #pragma unroll
         for (int j = 0; j < 5; j++) {
-            const uint32_t w = *(const uint32_t *)(row + (chroma ? min(j, 2) : j) * 4);
+            const uint32_t w = row[j];
             v[4 * j] = w & 255; v[4 * j + 1] = (w >> 8) & 255; v[4 * j + 2] = (w >> 16) & 255; v[4 * j + 3] = w >> 24;
         }
     } else {
-        // luma: region rows 0..19 = sample rows -4..15; chroma: region rows 0..9
-        // = sample rows -2..7, read into v[2..11]
-        const uint8_t *col = D + idx + 4;
+        // v[j] = sample row j-4 of this column (chroma region row 0 = sample row -2)
+        const uint8_t *col = D + idx + 4 - (chroma ? 2 * RY_S : 0);
 #pragma unroll
-        for (int j = 0; j < 20; j++) {
-            const int rr = chroma ? min(max(j - 2, 0), 9) : j;
-            v[j] = col[rr * S];
-        }
+        for (int j = 0; j < 20; j++) v[j] = col[j * RY_S];
     }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -796,18 +805,17 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
     }
     if (lane >= 32) return;
     if (dir == 0) {
-        uint8_t *row = D + (idx + (chroma ? 2 : 4)) * S;
+        uint32_t *row = (uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
 #pragma unroll
         for (int j = 0; j < 5; j++) {
             const uint32_t w = (uint32_t)v[4 * j] | ((uint32_t)v[4 * j + 1] << 8) | ((uint32_t)v[4 * j + 2] << 16) | ((uint32_t)v[4 * j + 3] << 24);
-            if (!chroma || j < 3) *(uint32_t *)(row + j * 4) = w;
+            if (!chroma || j < 3) row[j] = w;
         }
     } else {
-        uint8_t *col = D + idx + 4;
+        uint8_t *col = D + idx + 4 - (chroma ? 2 * RY_S : 0);
 #pragma unroll
         for (int j = 1; j < 19; j++) {
-            if (!chroma) col[j * S] = (uint8_t)v[j];
-            else if (j == 3 || j == 4 || j == 7 || j == 8) col[(j - 2) * S] = (uint8_t)v[j];
+            if (!chroma || j == 3 || j == 4 || j == 7 || j == 8) col[j * RY_S] = (uint8_t)v[j];
         }
     }
 }
@@ -818,13 +826,30 @@ __device__ __forceinline__ void st_gran(unsigned long long *p, uint32_t v, uint3
     __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(64) void k_rows(ReconArgs a)
+__device__ __forceinline__ unsigned long long lds_gran_ld(const unsigned long long *p)
 {
-    __shared__ RowLds L;
-    const int p = blockIdx.x % a.npics, r = blockIdx.x / a.npics;
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_gran_st(unsigned long long *p, uint32_t v, uint32_t tag)
+{
+    __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
+{
+    __shared__ RowLds s_rows[ROWS_PER_WG];
+    __shared__ unsigned long long s_ring[ROWS_PER_WG > 1 ? ROWS_PER_WG - 1 : 1][RING_K * 32];
+    __shared__ int s_done[ROWS_PER_WG];
     const int W = a.w, H = a.h;
+    const int p = blockIdx.x % a.npics, band = blockIdx.x / a.npics;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (ROWS_PER_WG > 1)
+        for (int i = threadIdx.x; i < (ROWS_PER_WG - 1) * RING_K * 32; i += blockDim.x) (&s_ring[0][0])[i] = 0;
+    if (threadIdx.x < ROWS_PER_WG) s_done[threadIdx.x] = 0;
+    __syncthreads();                              // the only workgroup barrier
+    const int r = band * ROWS_PER_WG + wid;
     if (r >= H) return;
-    const int lane = threadIdx.x;
+    RowLds &L = s_rows[wid];
     const PicDesc *pdp = a.pics + p;
     const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
     const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
@@ -836,10 +861,19 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
     unsigned *perr = a.err + p;
     const uint32_t tag = a.epoch;
     const bool has_up = r > 0, has_down = r + 1 < H;
+    // hand-off inside the workgroup (LDS ring) or across bands (HBM granules)
+    const bool up_lds = has_up && wid > 0, down_lds = has_down && wid < ROWS_PER_WG - 1;
+    const unsigned long long *ring_up = up_lds ? s_ring[wid - 1] : nullptr;
+    unsigned long long *ring_me = down_lds ? s_ring[wid] : nullptr;
+    int *done_me = &s_done[wid];
+    const int *done_down = &s_done[down_lds ? wid + 1 : wid];
     const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
     unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
     const bool last_row = r == H - 1;
-    const uint32_t *recw = (const uint32_t *)(a.rec + rec_base + r * W);   // 24 dwords per record
+    // record words through the constant address space: uniform scalar
+    // (SMEM) loads, counted by lgkmcnt instead of the in-order vmcnt
+    typedef const __attribute__((address_space(4))) uint32_t *cu32p;
+    const cu32p recw = (cu32p)(const void *)(a.rec + rec_base + r * W);   // 24 dwords per record
 
     // lane roles for dword transfers
     const int orow = lane >> 2, oq = lane & 3;                                   // luma 16x16
@@ -864,8 +898,12 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
         const uint32_t *rs = (const uint32_t *)(a.res + (size_t)g0 * 384);
         n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
         n_h0 = recw[0]; n_h1 = recw[1]; n_h2 = recw[2]; n_h3 = recw[3]; n_h4 = recw[4]; n_h5 = recw[5];
+        // retire these before the loop: otherwise the waitcnt pass merges their
+        // pending state into the loop header and, inside the loop, waits for
+        // each iteration's newest loads before reusing these registers
+        __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
     }
-    unsigned long long pt[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool prof = a.prof != nullptr;
     const unsigned long long tstart = prof ? wall_clock64() : 0;
     uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
@@ -879,8 +917,20 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
         const bool intra = qtype >= MBT_I4x4;
         const bool dbf = avail & DB_INNER;
         unsigned long long tc0 = prof ? clock64() : 0, tc1;
-        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 8 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
+        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
         if (prof && lane == 0) pmb[0] = wall_clock64();
+        // speculative read of the row above's granules (issued before the
+        // prefetch: vmcnt retires in order, so waiting for it must not wait
+        // for the prefetch); re-read until the needed ones
+        // carry this epoch.  Lanes 24..35 (unfiltered samples: intra
+        // neighbours) are published right after the row above reconstructs
+        // an MB; lanes 0..23 (final rows) after its next MB's vertical edges.
+        const int ce = tsel == 0 ? c : tsel == 1 ? min(c + 1, W - 1) : max(c - 1, 0);
+        const unsigned long long *tga = mbx_up + (size_t)ce * 32 + tdw;
+        const unsigned long long *tgl = up_lds ? ring_up + (ce % RING_K) * 32 + tdw : nullptr;
+        const uint32_t want = up_lds ? (uint32_t)ce + 1 : tag;     // ring tags: column + 1
+        unsigned long long gr = 0;
+        if (has_up) gr = up_lds ? lds_gran_ld(tgl) : ld_gran(tga);
         // ---- prefetch MB (r, c+1) (clamped: the last iteration re-reads MB W-1)
         {
             const int cn = min(c + 1, W - 1);
@@ -890,7 +940,7 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
             n_c = *(const uint32_t *)(cplane + coff + cn * 8);
             const uint32_t *rs = (const uint32_t *)(a.res + (size_t)gn * 384);
             n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
-            const uint32_t *rw = recw + cn * 24;
+            const cu32p rw = recw + cn * 24;
             n_h0 = rw[0]; n_h1 = rw[1]; n_h2 = rw[2]; n_h3 = rw[3]; n_h4 = rw[4]; n_h5 = rw[5];
         }
         // ---- own samples / residual / deblocking record into LDS
@@ -912,23 +962,20 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
         // ---- row above: wait until entry c is final, then fetch it (+ the
         //      neighbours' unfiltered samples for intra).  Intra MBs need it
         //      before prediction; all others only before the horizontal edges.
-        // speculative read of the granules; re-read until all carry this epoch
-        const unsigned long long *tga = mbx_up + (size_t)(tsel == 0 ? c : tsel == 1 ? min(c + 1, W - 1) : max(c - 1, 0)) * 32 + tdw;
-        unsigned long long gr = 0;
-        if (has_up) gr = ld_gran(tga);
         uint32_t top = 0;
-        auto fetch_top = [&]() {
+        auto fetch_top = [&](bool unfiltered) {
+            const bool mine = unfiltered ? (lane >= 24 && lane < 36) : lane < 24;
             unsigned spins = 0;
-            while (__builtin_amdgcn_ballot_w64((uint32_t)(gr >> 32) != tag) != 0) {
+            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != want) != 0) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 18)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-                gr = ld_gran(tga);
+                if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
+                gr = up_lds ? lds_gran_ld(tgl) : ld_gran(tga);
             }
             top = (uint32_t)gr;
             if (prof && lane == 0) pmb[1] = wall_clock64();
         };
         const bool early = has_up && intra && qtype != MBT_IPCM;
-        if (early) fetch_top();
+        if (early) fetch_top(true);
         if (prof) { tc1 = clock64(); pt[0] += tc1 - tc0; tc0 = tc1; }
 
         if (intra && qtype != MBT_IPCM) {
@@ -976,7 +1023,21 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
             wave_sync();
             if (lane < 32) L.left_unf[lane] = rc;
         }
+        // publish this MB's unfiltered bottom row (the row below's intra neighbours)
+        if (down_lds) {
+            // ring slot c % K last held column c-K, read by the row below up to
+            // its iteration c-K+1: wait until that iteration is done
+            if (c - RING_K + 2 > 0) {
+                unsigned spins = 0;
+                while (__hip_atomic_load(done_down, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < c - RING_K + 2) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }
+                }
+            }
+            if (lane >= 24 && lane < 32) lds_gran_st(ring_me + (c % RING_K) * 32 + lane, unf, (uint32_t)c + 1);
+        } else if (has_down && lane >= 24 && lane < 32) st_gran(mbx_me + (size_t)c * 32 + lane, unf, tag);
 
+        if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
         // ---- vertical edges (need only this row's samples)
         if (dbf) {
             deblock_dir(0, L.db, L.ry, L.ru, L.rv, lane, avail & DB_LEFT);
@@ -984,24 +1045,25 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
         }
         if (prof) { tc1 = clock64(); pt[1] += tc1 - tc0; tc0 = tc1; }
 
-        // ---- hand-off: entry c-1 is final now (only this MB's vertical edges
-        //      touch its columns 13..15): publish it, and the unfiltered row
-        //      of this MB's first four luma samples (the next row's top-right)
+        // ---- hand-off: the final rows of MB c-1 (entry dwords 0..23) are
+        //      final now -- only this MB's vertical edges touch its columns 13..15
         if (has_down) {
             const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
             const uint32_t patch = li < 16 ? *(const uint32_t *)&L.ry[(16 + (li >> 2)) * RY_S]
                                            : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
             const bool is_patch = li < 16 ? (li & 3) == 3 : (li < 24 && qq);
             const uint32_t ent = is_patch ? patch : prov;
-            if (c > 0 && lane < 32) st_gran(mbx_me + (size_t)(c - 1) * 32 + lane, ent, tag);
-            if (lane == 24) st_gran(mbx_me + (size_t)c * 32 + 24, unf, tag);
+            if (c > 0 && lane < 24) {
+                if (down_lds) lds_gran_st(ring_me + ((c - 1) % RING_K) * 32 + lane, ent, (uint32_t)c);
+                else st_gran(mbx_me + (size_t)(c - 1) * 32 + lane, ent, tag);
+            }
             if (prof && lane == 0) pmb[2] = wall_clock64();
         }
         if (prof) { tc1 = clock64(); pt[3] += tc1 - tc0; tc0 = tc1; }
 
         // ---- top halo, horizontal edges
         if (has_up) {
-            if (!early) fetch_top();
+            fetch_top(false);
             if (lane < 16) *(uint32_t *)&L.ry[orow * RY_S + 4 + oq * 4] = top;              // rows -4..-1
             else if (lane < 24) {
                 const int k = lane - 16, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
@@ -1019,7 +1081,7 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
             const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
             const uint32_t pl = *(const uint32_t *)&L.ry[(16 + ((li >> 2) & 3)) * RY_S + 4 + (li & 3) * 4];
             const uint32_t pc = *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S + 4 + qq * 4];
-            prov = li < 16 ? pl : li < 24 ? pc : unf;
+            prov = li < 16 ? pl : pc;
         }
         if (prof) { tc1 = clock64(); pt[2] += tc1 - tc0; tc0 = tc1; }
 
@@ -1061,15 +1123,20 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
             *(uint32_t *)&D[(row + 2) * RC_S] = *(const uint32_t *)&D[(row + 2) * RC_S + 8];
         }
         wave_sync();
+        // this row no longer needs the row above's entries <= c
+        if (lane == 0) __hip_atomic_store(done_me, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (prof) { tc1 = clock64(); pt[4] += tc1 - tc0; }
     }
     // last entry of the row is final as it stands
     if (has_down) {
-        if (lane < 32) st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, prov, tag);
+        if (lane < 24) {
+            if (down_lds) lds_gran_st(ring_me + ((W - 1) % RING_K) * 32 + lane, prov, (uint32_t)W);
+            else st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, prov, tag);
+        }
     }
     if (prof && lane == 0) {
-        unsigned long long *o = a.prof + (size_t)blockIdx.x * 8;
+        unsigned long long *o = a.prof + ((size_t)r * a.npics + p) * 16;
         o[0] = tstart; o[1] = wall_clock64();
-        for (int i = 0; i < 6; i++) o[2 + i] = pt[i];
+        for (int i = 0; i < 8; i++) o[2 + i] = pt[i];
     }
 }

@@ -149,8 +149,8 @@ int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
 int  h264mi_engine_set_timing(h264mi_engine *e, int max_batches);
 int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches);
 /* diagnostics: per k_rows workgroup (row r of batch picture p at index
- * r * npics + p) 8 u64: wall-clock start/end (100 MHz) and shader-clock sums
- * of its phases; enable != 0 allocates, out != NULL copies the last launch */
+ * r * npics + p) 16 u64: wall-clock start/end (100 MHz) and shader-clock sums
+ * of its phases, then 4 u64 per MB (hand-off timestamps); enable != 0 allocates, out != NULL copies the last launch */
 int  h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long long *out, size_t n);
 void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);          /* device pointer */
 size_t h264mi_engine_frame_bytes(h264mi_engine *e);

@@ -14,22 +14,22 @@ L.h264mi_engine_profile(eng._h, 1, None, 0)
 for k in range(6):
     eng.decode_device(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32)
     eng.sync()
-    buf = (C.c_uint64 * (S * h * 8))()
-    L.h264mi_engine_profile(eng._h, 1, buf, S * h * 8)
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(h, S, 8).astype(np.float64)
+    buf = (C.c_uint64 * (S * h * 16))()
+    L.h264mi_engine_profile(eng._h, 1, buf, S * h * 16)
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(h, S, 16).astype(np.float64)
     t0 = a[:, :, 0].min()
     st = (a[:, :, 0] - t0) / 100.0   # us
     en = (a[:, :, 1] - t0) / 100.0
-    ph = a[:, :, 2:8] / w            # cycles per MB
+    ph = a[:, :, 2:10] / w           # cycles per MB
     print(f"pic {k}: span {en.max():.1f} us; row start  r0 {st[0].mean():.1f} r1 {st[1].mean():.1f} r10 {st[10].mean():.1f} r67 {st[-1].mean():.1f}; "
           f"row dur r0 {(en[0]-st[0]).mean():.1f} r34 {(en[34]-st[34]).mean():.1f} r67 {(en[-1]-st[-1]).mean():.1f}")
-    print("   cycles/MB  pre(+intra wait) %.0f  intra+V %.0f  H %.0f  publish %.0f  stores %.0f  top-wait %.0f" % tuple(ph.mean(axis=(0, 1))))
+    print("   cycles/MB  pre(+intra wait) %.0f  V %.0f  H %.0f  publish %.0f  stores %.0f  top-wait %.0f  intra+unf %.0f" % tuple(ph.mean(axis=(0, 1)))[:7])
     print("   row0 cycles/MB", " ".join("%.0f" % x for x in ph[0].mean(axis=0)), " row40", " ".join("%.0f" % x for x in ph[40].mean(axis=0)))
 
 # per-MB hand-off timing of the last picture batch (100 MHz clock -> us)
-buf = (C.c_uint64 * (S * h * 8 + S * w * h * 4))()
+buf = (C.c_uint64 * (S * h * 16 + S * w * h * 4))()
 L.h264mi_engine_profile(eng._h, 1, buf, len(buf))
-m = np.frombuffer(buf, dtype=np.uint64)[S * h * 8:].reshape(S, h, w, 4).astype(np.float64) / 100.0
+m = np.frombuffer(buf, dtype=np.uint64)[S * h * 16:].reshape(S, h, w, 4).astype(np.float64) / 100.0
 p0 = m[0]
 for r in (1, 2, 20, 40):
     for c in (10, 60):
@@ -39,11 +39,21 @@ for r in (1, 2, 20, 40):
               f"consumer saw it {valid - pub:.2f}us after publish; iter len {p0[r, c+1, 0] - p0[r, c, 0]:.2f}us")
 
 # per-row: duration, summed top-wait, own work (cycles/MB) for picture 0 of the last batch
-a = np.frombuffer(buf, dtype=np.uint64)[:S * h * 8].reshape(h, S, 8).astype(np.float64)
+a = np.frombuffer(buf, dtype=np.uint64)[:S * h * 16].reshape(h, S, 16).astype(np.float64)
 t0 = a[:, :, 0].min()
 for r in range(h):
     st = (a[r, 0, 0] - t0) / 100; en = (a[r, 0, 1] - t0) / 100
-    ph = a[r, 0, 2:8] / w
+    ph = a[r, 0, 2:10] / w
     own = ph.sum() - ph[5]
     xcc = ""
-    print(f"r{r:02d} start {st:7.1f} end {en:7.1f} dur {en-st:7.1f}  own {own:6.0f} cyc/MB  wait {ph[5]:6.0f}  [pre {ph[0]:.0f} V {ph[1]:.0f} H {ph[2]:.0f} pub {ph[3]:.0f} st {ph[4]:.0f}]")
+    print(f"r{r:02d} start {st:7.1f} end {en:7.1f} dur {en-st:7.1f}  own {own:6.0f} cyc/MB  wait {ph[5]:6.0f}  [pre {ph[0]:.0f} intra+unf {ph[6]:.0f} V {ph[1]:.0f} H {ph[2]:.0f} pub {ph[3]:.0f} st {ph[4]:.0f}]")
+
+# row progress timeline of picture 0 of the last batch (us since the first row started)
+t0m = m[0, :, 0, 0].min()
+print("row: t(c=0) t(c=30) t(c=60) t(c=90) t(c=119) | per-row delta at c=60")
+prev = None
+for r in range(0, h, 4):
+    ts = [m[0, r, c, 0] - t0m for c in (0, 30, 60, 90, w - 1)]
+    d = "" if prev is None else f"{(ts[2] - prev) / 4:.2f}/row"
+    print(f"r{r:02d} " + " ".join(f"{x:7.1f}" for x in ts) + "  " + d)
+    prev = ts[2]
