@@ -141,7 +141,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     const bool rec = e->timing || e->tev;
     if (rec) (void)hipEventRecord(t0, e->st);
-    hipLaunchKernelGGL(k_mb, dim3(npics * e->nmbs), dim3(64), 0, e->st, a);
+    hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
     HIPCHECK(hipGetLastError());
     if (rec) (void)hipEventRecord(t1, e->st);
     hipLaunchKernelGGL(k_rows, dim3(npics * ((e->h + ROWS_PER_WG - 1) / ROWS_PER_WG)), dim3(ROWS_PER_WG * 64), 0, e->st, a);

@@ -207,9 +207,10 @@ __device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f)
 
 // win: 9x9 window whose (2,2) element is the integer sample G of output x=0.
 // Computes 4 outputs (x = 0..3) of window row offset `yy` (0..3).
+// win: 9 rows x 9 samples of the block's reference window (row stride 12)
 __device__ __forceinline__ void luma_row4(const uint8_t *win, int yy, int fx, int fy, int out[4])
 {
-#define W(x, y) ((int)win[((y) + 2 + yy) * 9 + (x) + 2])
+#define W(x, y) ((int)win[((y) + 2 + yy) * 12 + (x) + 2])
 #define B1(x, y) tap6(W((x)-2, y), W((x)-1, y), W(x, y), W((x)+1, y), W((x)+2, y), W((x)+3, y))
 #define H1(x, y) tap6(W(x, (y)-2), W(x, (y)-1), W(x, y), W(x, (y)+1), W(x, (y)+2), W(x, (y)+3))
     const int pos = fy * 4 + fx;
@@ -450,11 +451,17 @@ __device__ void mb_dbrec(const ReconArgs &a, int gmb, int mb, const MbRec &q, in
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
 {
+    // XCD-aware MB order: workgroups are dealt round-robin over the 8 XCDs
+    // (speed only, not correctness), so XCD x = blockIdx % 8 gets the x-th
+    // contiguous eighth of the batch -- neighbouring MBs share its L2 when
+    // their reference windows overlap.
     const int nmbs = a.w * a.h;
-    const int gidx = blockIdx.x;
+    const int total = a.npics * nmbs;
+    const int chunk = (total + 7) >> 3;
+    const int gidx = (blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
+    if (gidx >= total) return;
     const int p = gidx / nmbs;
     const int mb = gidx - p * nmbs;
-    if (p >= a.npics) return;
     const PicDesc pd = a.pics[p];
     const int gmb = pd.rec_base + mb;
     const MbRec &r = a.rec[gmb];
@@ -462,8 +469,9 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
 
     __shared__ int16_t s_res[384];
     __shared__ int32_t s_dc[24];
-    __shared__ uint8_t s_win[16 * 81];
-    __shared__ uint8_t s_cwin[2][16][9];
+    __shared__ uint32_t s_wraw[16][9][3];   // luma windows: 12 bytes per row from an aligned column
+    __shared__ uint32_t s_craw[2][16][3][2]; // chroma windows: 8 bytes per row
+    __shared__ uint8_t s_wxo[16], s_cxo[2][16];
     __shared__ uint8_t s_out[384];
 
     mb_dbrec(a, gmb, mb, r, lane, a.dbrec + (size_t)gmb * 64);
@@ -490,27 +498,65 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
     }
 
-    // stage luma windows: 16 blocks x 9x9
-    for (int idx = lane; idx < 16 * 81; idx += WAVE) {
-        const int b = idx / 81, rem = idx - b * 81;
-        const int wy = rem / 9, wx = rem - wy * 9;
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes;
+    // Reference windows with aligned dword loads (h264bsdPredictSamples
+    // reads, reconstruct.c:1819-1941; out-of-picture samples clamp like
+    // h264bsdFillBlock, :2222-2314).  Luma: block b = lane>>2 owns window rows
+    // (lane&3)+4k, 3 dwords each from the aligned column ax; chroma: lanes
+    // 0..31 = (block, plane), 3 rows x 2 dwords.  A window crossing the
+    // picture's left/right edge is rebuilt per sample (offset 0).
+    {
+        const int b = lane >> 2, sub = lane & 3;
         const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int x = clip3(0, W16 - 1, mbx * 16 + blk_x(b) * 4 + (mvx >> 2) - 2 + wx);
-        const int y = clip3(0, H16 - 1, mby * 16 + blk_y(b) * 4 + (mvy >> 2) - 2 + wy);
-        s_win[idx] = ref[y * W16 + x];
+        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes;
+        const int x0 = mbx * 16 + blk_x(b) * 4 + (mvx >> 2) - 2;
+        const int y0 = mby * 16 + blk_y(b) * 4 + (mvy >> 2) - 2;
+        const int ax = clip3(0, W16 - 12, x0 & ~3);
+        const bool inside = x0 >= 0 && x0 + 8 <= W16 - 1;
+        for (int wy = sub; wy < 9; wy += 4) {
+            const int y = clip3(0, H16 - 1, y0 + wy);
+            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + ax);
+            uint32_t d0 = src[0], d1 = src[1], d2 = src[2];
+            if (!inside) {
+                uint32_t o[3] = {0, 0, 0};
+#pragma unroll
+                for (int i = 0; i < 9; i++) {
+                    const int k = clip3(0, W16 - 1, x0 + i) - ax;
+                    const uint32_t w = k < 4 ? d0 : (k < 8 ? d1 : d2);
+                    o[i >> 2] |= ((w >> ((k & 3) * 8)) & 255u) << ((i & 3) * 8);
+                }
+                d0 = o[0]; d1 = o[1]; d2 = o[2];
+            }
+            s_wraw[b][wy][0] = d0; s_wraw[b][wy][1] = d1; s_wraw[b][wy][2] = d2;
+        }
+        if (sub == 0) s_wxo[b] = (uint8_t)(inside ? x0 - ax : 0);
     }
-    // chroma windows: 16 blocks x 2 comps x 3x3
-    for (int idx = lane; idx < 16 * 2 * 9; idx += WAVE) {
-        const int b = idx / 18, rem = idx - b * 18;
-        const int comp = rem / 9, k = rem - comp * 9;
-        const int wy = k / 3, wx = k - wy * 3;
+    if (lane < 32) {
+        const int b = lane >> 1, comp = lane & 1;
+        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
         const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes +
                              (unsigned long long)W16 * H16 + (unsigned long long)comp * CW * CH;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int x = clip3(0, CW - 1, mbx * 8 + blk_x(b) * 2 + (mvx >> 3) + wx);
-        const int y = clip3(0, CH - 1, mby * 8 + blk_y(b) * 2 + (mvy >> 3) + wy);
-        s_cwin[comp][b][k] = ref[y * CW + x];
+        const int x0 = mbx * 8 + blk_x(b) * 2 + (mvx >> 3);
+        const int y0 = mby * 8 + blk_y(b) * 2 + (mvy >> 3);
+        const int ax = clip3(0, CW - 8, x0 & ~3);
+        const bool inside = x0 >= 0 && x0 + 2 <= CW - 1;
+#pragma unroll
+        for (int wy = 0; wy < 3; wy++) {
+            const int y = clip3(0, CH - 1, y0 + wy);
+            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + ax);
+            uint32_t d0 = src[0], d1 = src[1];
+            if (!inside) {
+                uint32_t o = 0;
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    const int k = clip3(0, CW - 1, x0 + i) - ax;
+                    const uint32_t w = k < 4 ? d0 : d1;
+                    o |= ((w >> ((k & 3) * 8)) & 255u) << (i * 8);
+                }
+                d0 = o;
+            }
+            s_craw[comp][b][wy][0] = d0; s_craw[comp][b][wy][1] = d1;
+        }
+        s_cxo[comp][b] = (uint8_t)(inside ? x0 - ax : 0);
     }
     wave_sync();
 
@@ -518,7 +564,7 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         const int b = lane >> 2, yy = lane & 3;
         const int mvx = r.mv[b][0], mvy = r.mv[b][1];
         int o[4];
-        luma_row4(s_win + b * 81, yy, mvx & 3, mvy & 3, o);
+        luma_row4((const uint8_t *)&s_wraw[b][0][0] + s_wxo[b], yy, mvx & 3, mvy & 3, o);
         const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
 #pragma unroll
         for (int x = 0; x < 4; x++) s_out[by * 16 + bx + x] = (uint8_t)clip255(o[x] + s_res[by * 16 + bx + x]);
@@ -527,11 +573,11 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         const int b = lane >> 2, comp = (lane >> 1) & 1, yy = lane & 1;
         const int mvx = r.mv[b][0], mvy = r.mv[b][1];
         const int fx = mvx & 7, fy = mvy & 7;
-        const uint8_t *w = s_cwin[comp][b];
+        const uint8_t *w = (const uint8_t *)&s_craw[comp][b][0][0] + s_cxo[comp][b];
         const int cx = blk_x(b) * 2, cy = blk_y(b) * 2 + yy;
 #pragma unroll
         for (int x = 0; x < 2; x++) {
-            const int A = w[yy * 3 + x], B = w[yy * 3 + x + 1], C = w[(yy + 1) * 3 + x], D = w[(yy + 1) * 3 + x + 1];
+            const int A = w[yy * 8 + x], B = w[yy * 8 + x + 1], C = w[(yy + 1) * 8 + x], D = w[(yy + 1) * 8 + x + 1];
             const int v = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
             s_out[256 + comp * 64 + cy * 8 + cx + x] = (uint8_t)clip255(v + s_res[256 + comp * 64 + cy * 8 + cx + x]);
         }
