@@ -54,8 +54,12 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=56)
     ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="pictures per stream per launch (>1: frame-pipelined k_wg; 1: k_mb + k_rows)")
     ap.add_argument("--streams", type=int, default=8, help="streams per GPU (configs[3]: 8)")
     ap.add_argument("--config", type=int, default=3, help="generator preset (3 = 1080p I+P)")
+    ap.add_argument("--pipe-kernel", action="store_true", help="use the pipelined k_wg launch even for --pipeline 1")
+    ap.add_argument("--gen", default="", help="generator overrides k=v,... (experiments; default: preset)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     return ap.parse_args()
@@ -86,13 +90,13 @@ def dist_setup(gpus):
     return torch, (dist if world > 1 else None), rank, local, world
 
 
-def prepare(config, seeds, nframes):
+def prepare(config, seeds, nframes, overrides=None):
     """generate + host-parse every stream (threads: ctypes releases the GIL)"""
     from broadway_amd import gen
     from broadway_amd.engine import Capture
 
     def one(seed):
-        s = gen.generate(config, seed, nframes=nframes)
+        s = gen.generate(config, seed, nframes=nframes, **(overrides or {}))
         return s, Capture(s)
 
     with cf.ThreadPoolExecutor(max_workers=min(len(seeds), 8)) as ex:
@@ -100,26 +104,44 @@ def prepare(config, seeds, nframes):
     return [r[0] for r in res], [r[1] for r in res]
 
 
-def upload(L, caps, nsteps):
+def upload(L, caps, npics, depth, ring):
     """Lay out all record batches / coefficients / picture descriptors in HBM.
-    Step k's batch = picture k of every stream, records contiguous."""
+    Launch k covers pictures [k*depth, (k+1)*depth) of every stream, records
+    picture-major (picture t of the launch, stream s at (t*S + s)), so a
+    launch's records are contiguous; PicDesc.rec_base is relative to them.
+    ring > 0 (pipelined launches): picture j writes frame slot j % ring and
+    the records' reference slots are rewritten from DPB slots to ring slots."""
     S = len(caps)
     w, h = caps[0].w_mbs, caps[0].h_mbs
     nmbs = w * h
-    nslots = max(c.nslots for c in caps)
+    nslots = ring if ring else max(c.nslots for c in caps)
     rec_bytes = nmbs * MBREC
-    recs = bytearray(nsteps * S * rec_bytes)
+    recs = bytearray(npics * S * rec_bytes)
     coef_parts = []
-    pics = np.zeros((nsteps * S, 8), dtype=np.uint32)
+    pics = np.zeros((npics * S, 8), dtype=np.uint32)
     cbase = 0
-    for k in range(nsteps):
+    dpb_pic = [dict() for _ in caps]        # DPB slot -> picture index now in it
+    for j in range(npics):
         for s, c in enumerate(caps):
-            p = c.pictures[k]
-            off = (k * S + s) * rec_bytes
+            p = c.pictures[j]
+            off = (j * S + s) * rec_bytes
             recs[off:off + rec_bytes] = C.string_at(p.rec, rec_bytes)
+            slot = p.cur_slot
+            if ring:
+                r = np.frombuffer(recs, dtype=REC_DT, count=nmbs, offset=off)
+                inter = r["type"] <= 1
+                if inter.any():
+                    lut = np.zeros(64, dtype=np.uint8)
+                    for d, pj in dpb_pic[s].items():
+                        lut[d] = pj % ring
+                    refs = r["ref"].copy()
+                    refs[inter] = lut[refs[inter]]
+                    r["ref"][:] = refs
+                dpb_pic[s][p.cur_slot] = j
+                slot = j % ring
             if p.ncoef:
                 coef_parts.append(C.string_at(p.coef, p.ncoef * 32))
-            pics[k * S + s] = (s * nmbs, s * nslots, p.cur_slot, 0, cbase, 0, 0, 0)
+            pics[j * S + s] = (((j % depth) * S + s) * nmbs, s * nslots, slot, 0, cbase, 0, 0, 0)
             cbase += p.ncoef
     coefs = b"".join(coef_parts) + b"\0" * 64
     d_recs = L.h264mi_device_alloc(len(recs))
@@ -134,14 +156,37 @@ def upload(L, caps, nsteps):
     return d_recs, d_coef, d_pics, rec_bytes * S, nslots, len(recs) + len(coefs)
 
 
+REC_DT = np.dtype([("type", "u1"), ("qp", "u1"), ("qpc", "u1"), ("avail", "u1"), ("pred", "u1"),
+                   ("dbf", "u1"), ("offA", "i1"), ("offB", "i1"), ("cbits", "<u4"), ("coef", "<u4"),
+                   ("i4", "u1", 8), ("ref", "u1", 4), ("mv", "<i2", 32), ("slice", "<u2"), ("rsv", "<u2")])
+
+
+def row_reach(caps, lo, hi):
+    """How many MB rows beyond its own an inter MB of pictures [lo, hi) reads
+    from a reference (6-tap footprint included, clamped to the picture)."""
+    dy = 0
+    for c in caps:
+        nmbs, H16 = c.w_mbs * c.h_mbs, c.h_mbs * 16
+        rows = np.repeat(np.arange(c.h_mbs), c.w_mbs)
+        for j in range(lo, hi):
+            r = np.frombuffer(C.string_at(c.pictures[j].rec, nmbs * MBREC), dtype=REC_DT)
+            inter = r["type"] <= 1
+            if not inter.any():
+                continue
+            mvy = r["mv"][inter].reshape(-1, 16, 2)[:, :, 1].astype(np.int64) >> 2
+            y0 = (rows[inter] * 16)[:, None] + mvy
+            lo_r = np.clip(y0 - 2, 0, H16 - 1) // 16
+            hi_r = np.clip(y0 + 15 + 3, 0, H16 - 1) // 16
+            dy = max(dy, int((rows[inter][:, None] - lo_r).max()), int((hi_r - rows[inter][:, None]).max()))
+    return dy
+
+
 def inter_alg_bytes(caps, lo, hi):
     """Algorithmic bytes of k_mb for pictures [lo, hi) of every stream:
     MC reference footprint (SURVEY §8d R_alg luma+chroma term), the
     coefficient blocks and records of inter MBs, and the 384-B write of every
     inter MB."""
-    dt = np.dtype([("type", "u1"), ("qp", "u1"), ("qpc", "u1"), ("avail", "u1"), ("pred", "u1"),
-                   ("dbf", "u1"), ("offA", "i1"), ("offB", "i1"), ("cbits", "<u4"), ("coef", "<u4"),
-                   ("i4", "u1", 8), ("ref", "u1", 4), ("mv", "<i2", 32), ("slice", "<u2"), ("rsv", "<u2")])
+    dt = REC_DT
     assert dt.itemsize == MBREC
     total = 0
     n_inter = 0
@@ -207,7 +252,7 @@ def cpu_baseline(streams, nframes, reps=10):
         shutil.rmtree(td, ignore_errors=True)
 
 
-def verify(eng, caps, seeds, n_decoded):
+def verify(eng, caps, seeds, n_decoded, ring=0):
     """Bit-exactness: every slot of stream 0 still holding one of the decoded
     pictures vs the reference decoder's MD5 of that picture (POC type 2:
     output order == decode order)."""
@@ -218,13 +263,17 @@ def verify(eng, caps, seeds, n_decoded):
         return None, 0
     c = caps[0]
     last = {}
-    for k in range(min(n_decoded, len(ref["frames"]))):
-        last[c.pictures[k].cur_slot] = k
+    for k in range(n_decoded):
+        last[k % ring if ring else c.pictures[k].cur_slot] = k    # the picture each slot holds now
     ok = True
+    n = 0
     for slot, k in last.items():
+        if k >= len(ref["frames"]):
+            continue                              # beyond the fixture
+        n += 1
         if hashlib.md5(eng.read(0, slot).tobytes()).hexdigest() != ref["frames"][k]:
             ok = False
-    return ok, len(last)
+    return ok, n
 
 
 def load_traffic():
@@ -247,20 +296,30 @@ def main():
     L = _lib.mi()
 
     S = a.streams
+    P = max(1, a.pipeline)
     seeds = shard_seeds(rank, S)
-    nframes = a.warmup + a.steps
+    nframes = (a.warmup + a.steps) * P
     t_prep = time.perf_counter()
-    streams, caps = prepare(a.config, seeds, nframes)
+    overrides = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.gen.split(",") if kv)
+    streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= nframes for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    d_recs, d_coef, d_pics, step_rec_bytes, nslots, resident = upload(L, caps, nframes)
+    use_pipe = P > 1 or a.pipe_kernel
+    ring = P + 17 if use_pipe else 0        # frame-slot ring: launch + any short-term reference span
+    d_recs, d_coef, d_pics, pic_rec_bytes, nslots, resident = upload(L, caps, nframes, P, ring)
+    lags = [row_reach(caps, k * P, (k + 1) * P) + 2 for k in range(a.warmup + a.steps)] if use_pipe else []
     t_prep = time.perf_counter() - t_prep
 
     eng = Engine(w, h, S, nslots, device=local)
+    eng.set_pipeline(P)
     torch.cuda.set_device(local)
 
     def step(k):
-        eng.decode_device(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32)
+        if not use_pipe:
+            eng.decode_device(S, d_recs + k * pic_rec_bytes, d_coef, d_pics + k * S * 32)
+        else:
+            eng.decode_pipelined(S, P, d_recs + k * P * pic_rec_bytes, d_coef, d_pics + k * P * S * 32, k * P,
+                                 lags[k])
 
     for k in range(a.warmup):
         step(k)
@@ -282,21 +341,21 @@ def main():
     mb_us, rows_us, nb = eng.timing_report()
     errors = eng.errors()
 
-    frames_total = S * a.steps * world
+    frames_total = S * a.steps * P * world
     fps = frames_total / dt
     # roofline: R_alg per frame = MC reference footprint + coded
-    # 4x4 blocks x 32 B + 96-B MB records; one step = one frame of each of
-    # the S streams; the reconstruction of a step is the k_mb + k_rows pair
+    # 4x4 blocks x 32 B + 96-B MB records; one step = P frames of each of the
+    # S streams, reconstructed by one k_wg launch (P > 1) or k_mb + k_rows
     r_alg = 0
     for c in caps:
-        for k in range(a.warmup, a.warmup + a.steps):
+        for k in range(a.warmup * P, (a.warmup + a.steps) * P):
             p = c.pictures[k]
             r_alg += p.alg_ref_bytes + 32 * p.n_coded + MBREC * c.w_mbs * c.h_mbs
     per_step_bytes = r_alg / a.steps
     mb_us_avg, rows_us_avg = mb_us / max(nb, 1), rows_us / max(nb, 1)
     step_us = mb_us_avg + rows_us_avg
     achieved = per_step_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
-    kmb_alg, n_inter = inter_alg_bytes(caps, a.warmup, a.warmup + a.steps)
+    kmb_alg, n_inter = inter_alg_bytes(caps, a.warmup * P, (a.warmup + a.steps) * P)
     kmb_achieved = (kmb_alg / a.steps) / (mb_us_avg * 1e-6) / 1e9 if mb_us_avg > 0 else 0.0
     traffic = load_traffic()
     frame_read_gbs = r_alg * world / dt / 1e9
@@ -304,7 +363,7 @@ def main():
     ok = None
     n_checked = 0
     if not a.no_verify and rank == 0:
-        ok, n_checked = verify(eng, caps, seeds, nframes)
+        ok, n_checked = verify(eng, caps, seeds, nframes, ring)
 
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
@@ -327,21 +386,28 @@ def main():
             "config": {"workload": "configs[3]: 1080p (1920x1088, crop 1080) Baseline I+P, 1 I per 60, "
                                    "4 slices/picture, deblock idc 0/2",
                        "streams_per_gpu": S, "total_streams": S * world,
-                       "frames_per_stream_timed": a.steps, "seeds": f"100..{100 + S * world - 1}",
-                       "parallelism": f"streams sharded {S}/GPU, no collective"},
-            "roofline": {"kernel": "k_mb+k_rows (one reconstruction step)", "bound": "hbm",
+                       "frames_per_stream_timed": a.steps * P, "pictures_per_stream_per_step": P,
+                       "seeds": f"100..{100 + S * world - 1}",
+                       "parallelism": f"streams sharded {S}/GPU, no collective; "
+                                      f"{P} consecutive pictures per stream overlapped per launch"},
+            "roofline": {"kernel": ("k_wg (one launch = one step)" if use_pipe
+                                    else "k_mb+k_rows (one reconstruction step)"), "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
                          "alg_bytes_per_step": int(per_step_bytes),
                          "avg_step_kernel_us": round(step_us, 2),
                          "traffic_source": traffic.get("source") if traffic else None},
-            "kernels": {"k_mb": {"avg_launch_us": round(mb_us_avg, 2),
-                                 "alg_bytes_per_launch": int(kmb_alg / a.steps),
-                                 "achieved_GBs": round(kmb_achieved, 1),
-                                 "frac": round(kmb_achieved / HBM_PEAK_GBS, 5)},
-                        "k_rows": {"avg_launch_us": round(rows_us_avg, 2),
-                                   "bound": "latency (MB-row dependency chain)"}},
+            "kernels": ({"k_wg": {"avg_launch_us": round(rows_us_avg, 2),
+                                    "pictures_per_launch": S * P, "frame_slot_ring": ring,
+                                    "row_lag_max": max(lags) if lags else None}}
+                        if use_pipe else
+                        {"k_mb": {"avg_launch_us": round(mb_us_avg, 2),
+                                  "alg_bytes_per_launch": int(kmb_alg / a.steps),
+                                  "achieved_GBs": round(kmb_achieved, 1),
+                                  "frac": round(kmb_achieved / HBM_PEAK_GBS, 5)},
+                         "k_rows": {"avg_launch_us": round(rows_us_avg, 2),
+                                    "bound": "latency (MB-row dependency chain)"}}),
             "wall_read_GBs": round(frame_read_gbs, 2),
             "cpu_baseline": cpu,
             "bitexact_check": {"ok": ok, "frames_checked": n_checked, "residual_range_errors": errors},

@@ -28,6 +28,11 @@ struct h264mi_engine {
     unsigned epoch;
     unsigned long long *d_prof;   // optional k_rows phase clocks
     size_t prof_cap;
+    int pipe_cap;                 // pictures per launch the per-picture buffers hold
+    uint32_t *d_progress;         // k_wg<PIPE>: per picture row drained-store progress
+    uint32_t *d_order, *h_order;  // k_wg: (picture, row) dispatch order
+    int classic;                  // single-picture launches: k_mb + k_rows (default) or k_wg (H264MI_KERNEL=wg)
+    int order_depth, order_lag;
     uint8_t *d_dbrec;         // 64 B per batch MB
     int16_t *d_res;           // 384 x int16 per batch MB (intra residual)
     MbRec *d_rec;
@@ -49,6 +54,40 @@ struct h264mi_engine {
     int tev_cap, tev_n;
 };
 
+// per-picture buffers of one launch (deblocking records, intra residuals,
+// row mailboxes, error flags, pipeline progress/counters), for `cap` pictures
+static void free_pic_buffers(h264mi_engine *e)
+{
+    (void)hipFree(e->d_mbx); (void)hipFree(e->d_dbrec); (void)hipFree(e->d_res); (void)hipFree(e->d_err);
+    (void)hipFree(e->d_progress);
+    (void)hipHostFree(e->h_err);
+    (void)hipFree(e->d_order); (void)hipHostFree(e->h_order);
+    e->d_order = NULL; e->h_order = NULL; e->order_depth = e->order_lag = 0;
+    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL;
+    e->d_progress = NULL; e->h_err = NULL;
+    e->pipe_cap = 0;
+}
+
+static int alloc_pic_buffers(h264mi_engine *e, int cap)
+{
+    const size_t np = (size_t)cap, mbs = np * e->nmbs, rows = np * e->h;
+    bool ok = hipMalloc(&e->d_mbx, mbs * 256) == hipSuccess &&
+              hipMalloc(&e->d_dbrec, mbs * 64) == hipSuccess &&
+              hipMalloc(&e->d_res, mbs * 768) == hipSuccess &&
+              hipMalloc(&e->d_err, sizeof(unsigned) * np) == hipSuccess &&
+              hipMalloc(&e->d_progress, rows * 4) == hipSuccess &&
+              hipHostMalloc(&e->h_err, sizeof(unsigned) * np, hipHostMallocDefault) == hipSuccess &&
+              hipMalloc(&e->d_order, sizeof(uint32_t) * rows) == hipSuccess &&
+              hipHostMalloc(&e->h_order, sizeof(uint32_t) * rows, hipHostMallocDefault) == hipSuccess;
+    if (!ok) { free_pic_buffers(e); return -1; }
+    // cleared granules / progress carry epoch 0, which no launch uses
+    (void)hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st);
+    (void)hipMemsetAsync(e->d_progress, 0, rows * 4, e->st);
+    memset(e->h_err, 0, sizeof(unsigned) * np);
+    e->pipe_cap = cap;
+    return 0;
+}
+
 extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
 {
     if (w_mbs < 1 || h_mbs < 1 || h_mbs > 1024 || nstreams < 1 || nslots < 1) return NULL;
@@ -67,29 +106,31 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
     e->h_coef_cap = e->coef_cap;
     e->timing = getenv("H264MI_TIMING") != NULL;
+    {
+        const char *km = getenv("H264MI_KERNEL");
+        e->classic = !(km && !strcmp(km, "wg"));
+    }
     bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
-              hipMalloc(&e->d_mbx, (size_t)nstreams * e->nmbs * 256) == hipSuccess &&
-              hipMalloc(&e->d_dbrec, (size_t)nstreams * e->nmbs * 64) == hipSuccess &&
-              hipMalloc(&e->d_res, (size_t)nstreams * e->nmbs * 768) == hipSuccess &&
+
               hipMalloc(&e->d_rec, sizeof(MbRec) * nstreams * e->nmbs) == hipSuccess &&
               hipMalloc(&e->d_coef, e->coef_cap * 32) == hipSuccess &&
               hipMalloc(&e->d_pics, sizeof(PicDesc) * nstreams) == hipSuccess &&
-              hipMalloc(&e->d_err, sizeof(unsigned) * nstreams) == hipSuccess &&
+
               hipHostMalloc(&e->h_rec, sizeof(MbRec) * nstreams * e->nmbs, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&e->h_coef, e->h_coef_cap * 32, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&e->h_pics, sizeof(PicDesc) * nstreams, hipHostMallocDefault) == hipSuccess &&
-              hipHostMalloc(&e->h_err, sizeof(unsigned) * nstreams, hipHostMallocDefault) == hipSuccess &&
+
               hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess &&
               hipEventCreate(&e->ev2) == hipSuccess;
+    ok = ok && alloc_pic_buffers(e, nstreams) == 0;
     if (!ok) {
         fprintf(stderr, "h264mi: engine allocation failed\n");
         h264mi_engine_destroy(e);
         return NULL;
     }
     (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * nslots * nstreams, e->st);
-    (void)hipMemsetAsync(e->d_mbx, 0, (size_t)nstreams * e->nmbs * 256, e->st);
     e->epoch = 0;
     (void)hipEventRecord(e->ev_staged, e->st);
     (void)hipStreamSynchronize(e->st);
@@ -100,9 +141,10 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
 {
     if (!e) return;
     if (e->st) (void)hipStreamSynchronize(e->st);
-    (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_mbx); (void)hipFree(e->d_dbrec); (void)hipFree(e->d_res); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
-    (void)hipFree(e->d_pics); (void)hipFree(e->d_err);
-    (void)hipHostFree(e->h_rec); (void)hipHostFree(e->h_coef); (void)hipHostFree(e->h_pics); (void)hipHostFree(e->h_err);
+    free_pic_buffers(e);
+    (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
+    (void)hipFree(e->d_pics);
+    (void)hipHostFree(e->h_rec); (void)hipHostFree(e->h_coef); (void)hipHostFree(e->h_pics);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -112,17 +154,36 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     free(e);
 }
 
+// (picture k, row r) pairs by r + lag*k, then k: with lag > every reference
+// reach in rows + 1, each unit's dependencies come earlier in the order
+static int pipe_order(h264mi_engine *e, int depth, int lag)
+{
+    if (e->order_depth == depth && e->order_lag == lag) return 0;
+    int n = 0;
+    for (int key = 0; key <= e->h - 1 + lag * (depth - 1); key++)
+        for (int k = 0; k < depth; k++) {
+            const int r = key - lag * k;
+            if (r >= 0 && r < e->h) e->h_order[n++] = ((uint32_t)k << 16) | (uint32_t)r;
+        }
+    HIPCHECK(hipMemcpyAsync(e->d_order, e->h_order, sizeof(uint32_t) * n, hipMemcpyHostToDevice, e->st));
+    e->order_depth = depth;
+    e->order_lag = lag;
+    return 0;
+}
+
 static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
-                        const PicDesc *d_pics)
+                        const PicDesc *d_pics, bool pipe = false, int depth = 1, int base_pic = 0, int lag = 0)
 {
     ReconArgs a;
+    memset(&a, 0, sizeof(a));
     a.frames = e->d_frames;
     a.frame_bytes = e->frame_bytes;
     a.rec = d_rec;
     a.coef = d_coef;
     a.mbx = e->d_mbx;
-    if (++e->epoch == 0) {                    // granule tags: never 0 (the cleared state)
-        HIPCHECK(hipMemsetAsync(e->d_mbx, 0, (size_t)e->nstreams * e->nmbs * 256, e->st));
+    if (++e->epoch >= (1u << 20)) {           // tags: granules epoch, progress (epoch << 12) | count
+        HIPCHECK(hipMemsetAsync(e->d_mbx, 0, (size_t)e->pipe_cap * e->nmbs * 256, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_progress, 0, (size_t)e->pipe_cap * e->h * 4, e->st));
         e->epoch = 1;
     }
     a.epoch = e->epoch;
@@ -133,7 +194,17 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.dbrec = e->d_dbrec;
     a.res = e->d_res;
     a.err = e->d_err;
+    a.progress = e->d_progress;
+    a.S = npics / depth;
+    a.ring = e->nslots;
+    a.base_pic = base_pic % e->nslots;
     HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * npics, e->st));
+    const bool wg = pipe || !e->classic;
+    if (wg) {
+        if (pipe) a.prof = NULL;
+        if (pipe_order(e, depth, lag < 1 ? e->h : lag)) return -1;
+        a.order = e->d_order;
+    }
     hipEvent_t t0 = e->ev0, t1 = e->ev1, t2 = e->ev2;
     if (e->tev && e->tev_n < e->tev_cap) {
         t0 = e->tev[3 * e->tev_n]; t1 = e->tev[3 * e->tev_n + 1]; t2 = e->tev[3 * e->tev_n + 2];
@@ -141,11 +212,21 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     const bool rec = e->timing || e->tev;
     if (rec) (void)hipEventRecord(t0, e->st);
-    hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
-    HIPCHECK(hipGetLastError());
-    if (rec) (void)hipEventRecord(t1, e->st);
-    hipLaunchKernelGGL(k_rows, dim3(npics * ((e->h + ROWS_PER_WG - 1) / ROWS_PER_WG)), dim3(ROWS_PER_WG * 64), 0, e->st, a);
-    HIPCHECK(hipGetLastError());
+    if (!wg) {
+        hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
+        HIPCHECK(hipGetLastError());
+        if (rec) (void)hipEventRecord(t1, e->st);
+        hipLaunchKernelGGL(k_rows, dim3(npics * e->h), dim3(64), 0, e->st, a);
+        HIPCHECK(hipGetLastError());
+    } else {
+        // one launch: row workgroups with in-workgroup MC (k_wg); the k_mb
+        // slot of the timing is empty
+        if (rec) (void)hipEventRecord(t1, e->st);
+        const dim3 grid(a.S * e->h * depth), blk(64 * (1 + WG_NMC));
+        if (pipe) hipLaunchKernelGGL((k_wg<true, WG_NMC>), grid, blk, 0, e->st, a);
+        else hipLaunchKernelGGL((k_wg<false, WG_NMC>), grid, blk, 0, e->st, a);
+        HIPCHECK(hipGetLastError());
+    }
     if (rec) (void)hipEventRecord(t2, e->st);
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
     return 0;
@@ -198,13 +279,36 @@ extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const vo
     return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics);
 }
 
+extern "C" int h264mi_engine_set_pipeline(h264mi_engine *e, int depth)
+{
+    if (!e || depth < 1) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    HIPCHECK(hipStreamSynchronize(e->st));
+    const int cap = e->nstreams * depth;
+    if (cap == e->pipe_cap) return 0;
+    free_pic_buffers(e);
+    if (alloc_pic_buffers(e, cap)) return -1;
+    HIPCHECK(hipStreamSynchronize(e->st));
+    return 0;
+}
+
+extern "C" int h264mi_engine_decode_pipelined(h264mi_engine *e, int nstreams, int depth, const void *d_recs,
+                                              const int16_t *d_coef, const void *d_pics, int base_pic, int lag_rows)
+{
+    if (!e || nstreams < 1 || nstreams > e->nstreams || depth < 1 || nstreams * depth > e->pipe_cap) return -1;
+    if (base_pic < 0 || depth > e->nslots) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    return launch_batch(e, nstreams * depth, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, true, depth,
+                        base_pic, lag_rows);
+}
+
 extern "C" int h264mi_engine_sync(h264mi_engine *e)
 {
     if (!e) return -1;
     HIPCHECK(hipSetDevice(e->dev));
     HIPCHECK(hipStreamSynchronize(e->st));
-    for (int i = 0; i < e->nstreams; i++) e->err_accum += e->h_err[i] ? 1 : 0;
-    memset(e->h_err, 0, sizeof(unsigned) * e->nstreams);
+    for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
+    memset(e->h_err, 0, sizeof(unsigned) * e->pipe_cap);
     return 0;
 }
 

@@ -40,6 +40,14 @@ struct ReconArgs {
     unsigned long long *mbx;  // row mailboxes: 32 tagged granules per MB of the batch (k_rows)
     unsigned int epoch;       // launch counter != 0: granule tag (no reset between launches)
     unsigned long long *prof; // optional k_rows phase clocks: 16 per (row, picture) workgroup
+    // frame-pipelined launches (k_wg): pictures p = k*S + s, k = 0..P-1.
+    // Frame slots follow a ring: the launch's picture k of a stream writes
+    // slot (base_pic + k) mod ring, so a reference slot x was written in this
+    // launch by picture (x - base_pic) mod ring if that is < k.
+    uint32_t *progress;       // per picture row: (epoch << 12) | iterations whose frame stores drained
+    int S;                    // streams per pipeline stage
+    int ring, base_pic;
+    const uint32_t *order;    // k_wg: dispatch order of the P*H (picture, row) pairs, (k << 16) | r
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -74,6 +82,22 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
 }
+
+// write-through (sc1) stores and L1-bypassing loads for data another CU
+// consumes within the same launch (MI355X_MICROARCH.md, inter-workgroup
+// visibility, table row 1)
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_sc1_u32(uint32_t *p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <bool SC1> __device__ __forceinline__ uint32_t ld32(const void *p)
+{
+    return SC1 ? ld_sc1_u32((const uint32_t *)p) : *(const uint32_t *)p;
+}
+template <bool SC1> __device__ __forceinline__ void st32(void *p, uint32_t v)
+{
+    if (SC1) st_sc1_u32((uint32_t *)p, v);
+    else *(uint32_t *)p = v;
+}
+__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
 __device__ __forceinline__ int clip3(int lo, int hi, int v) { return min(max(v, lo), hi); }
@@ -340,53 +364,6 @@ __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int
     return 0;
 }
 
-__device__ __forceinline__ void filt_luma(uint8_t *s, int step, int bS, int alpha, int beta, int tc0)
-{
-    const int p0 = s[-step], p1 = s[-2 * step], p2 = s[-3 * step], p3 = s[-4 * step];
-    const int q0 = s[0], q1 = s[step], q2 = s[2 * step], q3 = s[3 * step];
-    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-    const int ap = abs(p2 - p0), aq = abs(q2 - q0);
-    if (bS < 4) {
-        const int tc = tc0 + (ap < beta) + (aq < beta);
-        const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-        s[-step] = (uint8_t)clip255(p0 + d);
-        s[0] = (uint8_t)clip255(q0 - d);
-        if (ap < beta) s[-2 * step] = (uint8_t)(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-        if (aq < beta) s[step] = (uint8_t)(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
-    } else {
-        const bool strong = abs(p0 - q0) < ((alpha >> 2) + 2);
-        if (ap < beta && strong) {
-            s[-step] = (uint8_t)((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-            s[-2 * step] = (uint8_t)((p2 + p1 + p0 + q0 + 2) >> 2);
-            s[-3 * step] = (uint8_t)((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
-        } else {
-            s[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-        }
-        if (aq < beta && strong) {
-            s[0] = (uint8_t)((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-            s[step] = (uint8_t)((p0 + q0 + q1 + q2 + 2) >> 2);
-            s[2 * step] = (uint8_t)((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
-        } else {
-            s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
-        }
-    }
-}
-
-__device__ __forceinline__ void filt_chroma(uint8_t *s, int step, int bS, int alpha, int beta, int tc0)
-{
-    const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
-    if (!(abs(p0 - q0) < alpha && abs(p1 - p0) < beta && abs(q1 - q0) < beta)) return;
-    if (bS < 4) {
-        const int tc = tc0 + 1;
-        const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-        s[-step] = (uint8_t)clip255(p0 + d);
-        s[0] = (uint8_t)clip255(q0 - d);
-    } else {
-        s[-step] = (uint8_t)((2 * p1 + p0 + q1 + 2) >> 2);
-        s[0] = (uint8_t)((2 * q1 + q0 + p1 + 2) >> 2);
-    }
-}
-
 // ---------------------------------------------------------------------------
 // deblocking record (precomputed by k_mb, consumed by k_rows): 64 B per MB
 //   [0..15]  bS nibbles, index (dir*16 + seg*4 + edge): dir 0 = vertical edges;
@@ -397,9 +374,9 @@ __device__ __forceinline__ void filt_chroma(uint8_t *s, int step, int bS, int al
 // Reference: GetBoundaryStrengths deblocking.c:1134-1370,
 // GetLumaEdgeThresholds :1381-1449, GetChromaEdgeThresholds :1460-1532.
 // ---------------------------------------------------------------------------
-__device__ void mb_dbrec(const ReconArgs &a, int gmb, int mb, const MbRec &q, int lane, uint8_t *out)
+// computes the record into s_db (LDS, 64 B)
+__device__ void mb_dbrec(const ReconArgs &a, int gmb, const MbRec &q, int lane, uint8_t *s_db)
 {
-    __shared__ uint8_t s_db[64];
     const bool fl = q.avail & DB_LEFT, ft = q.avail & DB_TOP;
     if (lane < 32) {
         const int dir = lane >> 4, kk = (lane >> 2) & 3, e = lane & 3;
@@ -439,8 +416,6 @@ __device__ void mb_dbrec(const ReconArgs &a, int gmb, int mb, const MbRec &q, in
         o[6] = o[7] = 0;
     }
     wave_sync();
-    if (lane < 16) ((uint32_t *)out)[lane] = ((const uint32_t *)s_db)[lane];
-    (void)mb;
 }
 
 // ---------------------------------------------------------------------------
@@ -449,51 +424,84 @@ __device__ void mb_dbrec(const ReconArgs &a, int gmb, int mb, const MbRec &q, in
 //   inter   : residual + 6-tap/bilinear MC + clip-add + write-out
 //   intra   : residual -> scratch (consumed by k_rows)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_mb(ReconArgs a)
+// per-wave LDS scratch of the MB reconstruction (reference windows)
+struct McScratch {
+    int32_t dc[24];
+    uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
+    uint32_t craw[2][16][3][2];  // chroma windows: 8 bytes per row
+    uint8_t wxo[16], cxo[2][16];
+};
+
+// MB `mb` of picture p (one wave): deblocking record -> db[64]; residual ->
+// res[384] (intra MBs with coded blocks; inter MBs use it as scratch); inter
+// MBs: 6-tap / bilinear MC + residual, clipped, -> px[384] (luma 16x16, Cb
+// 8x8, Cr 8x8).  All outputs in LDS.  PIPE: reference samples written by a
+// picture of this launch are waited for (per-row progress) and read sc1.
+template <bool PIPE>
+__device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M, uint8_t *px, int16_t *res,
+                       uint8_t *db)
 {
-    // XCD-aware MB order: workgroups are dealt round-robin over the 8 XCDs
-    // (speed only, not correctness), so XCD x = blockIdx % 8 gets the x-th
-    // contiguous eighth of the batch -- neighbouring MBs share its L2 when
-    // their reference windows overlap.
-    const int nmbs = a.w * a.h;
-    const int total = a.npics * nmbs;
-    const int chunk = (total + 7) >> 3;
-    const int gidx = (blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
-    if (gidx >= total) return;
-    const int p = gidx / nmbs;
-    const int mb = gidx - p * nmbs;
     const PicDesc pd = a.pics[p];
     const int gmb = pd.rec_base + mb;
     const MbRec &r = a.rec[gmb];
-    const int lane = threadIdx.x;
+    int16_t *s_res = res;
+    uint8_t *s_out = px;
 
-    __shared__ int16_t s_res[384];
-    __shared__ int32_t s_dc[24];
-    __shared__ uint32_t s_wraw[16][9][3];   // luma windows: 12 bytes per row from an aligned column
-    __shared__ uint32_t s_craw[2][16][3][2]; // chroma windows: 8 bytes per row
-    __shared__ uint8_t s_wxo[16], s_cxo[2][16];
-    __shared__ uint8_t s_out[384];
-
-    mb_dbrec(a, gmb, mb, r, lane, a.dbrec + (size_t)gmb * 64);
+    const int mbx = mb % a.w, mby = mb / a.w;
+    mb_dbrec(a, gmb, r, lane, db);
 
     if (r.type >= MBT_I4x4) {
         if (r.type != MBT_IPCM && r.cbits) {
             int e = 0;
-            mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, s_dc, lane, &e);
-            uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
-            const uint32_t *src = (const uint32_t *)s_res;
-            for (int i = lane; i < 192; i += WAVE) dst[i] = src[i];
+            mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
             if (e && lane == 0) atomicOr(a.err + p, 1u);
         }
-        return;
+        return r.type;
     }
 
     const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
-    const int mbx = mb % a.w, mby = mb / a.w;
+    if (PIPE) {
+        // wait for exactly the reference samples this MB reads that a picture
+        // of this launch writes: per 8x8 partition q (one reference slot), the
+        // clamped 6-tap footprint of its four 4x4 blocks; a sample of row R,
+        // column C is final once that row's progress passed C+1 and the row
+        // below's passed C (progress >= C+2 over rows R..R+1)
+        const int kcur = p / a.S, s = p - kcur * a.S;
+        const int b = lane >> 2;
+        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
+        const int bx0 = mbx * 16 + blk_x(b) * 4 + (mvx >> 2), by0 = mby * 16 + blk_y(b) * 4 + (mvy >> 2);
+        int xlo = clip3(0, W16 - 1, bx0 - 2), xhi = clip3(0, W16 - 1, bx0 + 6);
+        int ylo = clip3(0, H16 - 1, by0 - 2), yhi = clip3(0, H16 - 1, by0 + 6);
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {          // reduce over the partition's 16 lanes
+            xlo = min(xlo, __shfl_xor(xlo, m, 64)); xhi = max(xhi, __shfl_xor(xhi, m, 64));
+            ylo = min(ylo, __shfl_xor(ylo, m, 64)); yhi = max(yhi, __shfl_xor(yhi, m, 64));
+        }
+        for (int q = 0; q < 4; q++) {
+            const int x = r.ref[q];
+            const int t = ((x - a.base_pic) % a.ring + a.ring) % a.ring;
+            if (t >= kcur) continue;                 // written before this launch
+            const int pp = t * a.S + s;
+            const int rlo = __builtin_amdgcn_readlane(ylo, 16 * q) >> 4;
+            const int rhi = min(a.h - 1, (__builtin_amdgcn_readlane(yhi, 16 * q) >> 4) + 1);
+            const uint32_t need = (a.epoch << 12) + (uint32_t)min(a.w, (__builtin_amdgcn_readlane(xhi, 16 * q) >> 4) + 2);
+            for (int base = rlo; base <= rhi; base += WAVE) {
+                const int R = base + lane;
+                unsigned spins = 0;
+                for (;;) {
+                    const uint32_t v = R <= rhi ? ld_sc1_u32(a.progress + (size_t)pp * a.h + R) : 0xFFFFFFFFu;
+                    if (__builtin_amdgcn_ballot_w64(v < need) == 0) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > (1u << 20)) { if (lane == 0) atomicOr(a.err + p, 4u); break; }   // bounded wait
+                }
+            }
+        }
+    }
+
     const uint8_t *frames = a.frames;
     int e = 0;
     if (r.cbits) {
-        mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, s_dc, lane, &e);
+        mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
     } else {
         for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
     }
@@ -515,7 +523,7 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         for (int wy = sub; wy < 9; wy += 4) {
             const int y = clip3(0, H16 - 1, y0 + wy);
             const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + ax);
-            uint32_t d0 = src[0], d1 = src[1], d2 = src[2];
+            uint32_t d0 = ld32<PIPE>(src), d1 = ld32<PIPE>(src + 1), d2 = ld32<PIPE>(src + 2);
             if (!inside) {
                 uint32_t o[3] = {0, 0, 0};
 #pragma unroll
@@ -526,9 +534,9 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
                 }
                 d0 = o[0]; d1 = o[1]; d2 = o[2];
             }
-            s_wraw[b][wy][0] = d0; s_wraw[b][wy][1] = d1; s_wraw[b][wy][2] = d2;
+            M.wraw[b][wy][0] = d0; M.wraw[b][wy][1] = d1; M.wraw[b][wy][2] = d2;
         }
-        if (sub == 0) s_wxo[b] = (uint8_t)(inside ? x0 - ax : 0);
+        if (sub == 0) M.wxo[b] = (uint8_t)(inside ? x0 - ax : 0);
     }
     if (lane < 32) {
         const int b = lane >> 1, comp = lane & 1;
@@ -543,7 +551,7 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         for (int wy = 0; wy < 3; wy++) {
             const int y = clip3(0, CH - 1, y0 + wy);
             const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + ax);
-            uint32_t d0 = src[0], d1 = src[1];
+            uint32_t d0 = ld32<PIPE>(src), d1 = ld32<PIPE>(src + 1);
             if (!inside) {
                 uint32_t o = 0;
 #pragma unroll
@@ -554,9 +562,9 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
                 }
                 d0 = o;
             }
-            s_craw[comp][b][wy][0] = d0; s_craw[comp][b][wy][1] = d1;
+            M.craw[comp][b][wy][0] = d0; M.craw[comp][b][wy][1] = d1;
         }
-        s_cxo[comp][b] = (uint8_t)(inside ? x0 - ax : 0);
+        M.cxo[comp][b] = (uint8_t)(inside ? x0 - ax : 0);
     }
     wave_sync();
 
@@ -564,7 +572,7 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         const int b = lane >> 2, yy = lane & 3;
         const int mvx = r.mv[b][0], mvy = r.mv[b][1];
         int o[4];
-        luma_row4((const uint8_t *)&s_wraw[b][0][0] + s_wxo[b], yy, mvx & 3, mvy & 3, o);
+        luma_row4((const uint8_t *)&M.wraw[b][0][0] + M.wxo[b], yy, mvx & 3, mvy & 3, o);
         const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
 #pragma unroll
         for (int x = 0; x < 4; x++) s_out[by * 16 + bx + x] = (uint8_t)clip255(o[x] + s_res[by * 16 + bx + x]);
@@ -573,7 +581,7 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         const int b = lane >> 2, comp = (lane >> 1) & 1, yy = lane & 1;
         const int mvx = r.mv[b][0], mvy = r.mv[b][1];
         const int fx = mvx & 7, fy = mvy & 7;
-        const uint8_t *w = (const uint8_t *)&s_craw[comp][b][0][0] + s_cxo[comp][b];
+        const uint8_t *w = (const uint8_t *)&M.craw[comp][b][0][0] + M.cxo[comp][b];
         const int cx = blk_x(b) * 2, cy = blk_y(b) * 2 + yy;
 #pragma unroll
         for (int x = 0; x < 2; x++) {
@@ -584,18 +592,50 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
     }
     wave_sync();
 
+    if (lane == 0 && e) atomicOr(a.err + p, 1u);
+    return r.type;
+}
+
+// k_mb: every MB of the batch in parallel, one wave per MB.  XCD-aware MB
+// order: workgroups are dealt round-robin over the 8 XCDs (speed only, not
+// correctness), so XCD x = blockIdx % 8 gets the x-th contiguous eighth of the
+// batch -- neighbouring MBs share its L2 when their reference windows overlap.
+// Outputs to HBM for k_rows: deblocking record, intra residual, inter samples.
+__global__ __launch_bounds__(64) void k_mb(ReconArgs a)
+{
+    __shared__ McScratch M;
+    __shared__ uint8_t s_px[384];
+    __shared__ int16_t s_res[384];
+    __shared__ uint8_t s_db[64];
+    const int nmbs = a.w * a.h;
+    const int total = a.npics * nmbs;
+    const int chunk = (total + 7) >> 3;
+    const int gidx = (blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
+    if (gidx >= total) return;
+    const int p = gidx / nmbs, mb = gidx - p * nmbs, lane = threadIdx.x;
+    const PicDesc &pd = a.pics[p];
+    const int gmb = pd.rec_base + mb;
+    const int type = mc_core<false>(a, p, mb, lane, M, s_px, s_res, s_db);
+    if (lane < 16) ((uint32_t *)(a.dbrec + (size_t)gmb * 64))[lane] = ((const uint32_t *)s_db)[lane];
+    if (type >= MBT_I4x4) {
+        if (type != MBT_IPCM && a.rec[gmb].cbits) {
+            uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
+            for (int i = lane; i < 192; i += WAVE) dst[i] = ((const uint32_t *)s_res)[i];
+        }
+        return;
+    }
+    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
+    const int mbx = mb % a.w, mby = mb / a.w;
     uint8_t *cur = a.frames + (unsigned long long)(pd.frame_base + pd.cur_slot) * a.frame_bytes;
     {
         const int row = lane >> 2, q4 = lane & 3;
-        *(uint32_t *)(cur + (size_t)(mby * 16 + row) * W16 + mbx * 16 + q4 * 4) = *(const uint32_t *)(s_out + row * 16 + q4 * 4);
+        *(uint32_t *)(cur + (size_t)(mby * 16 + row) * W16 + mbx * 16 + q4 * 4) = *(const uint32_t *)(s_px + row * 16 + q4 * 4);
     }
     if (lane < 32) {
         const int comp = lane >> 4, row = (lane >> 1) & 7, q2 = lane & 1;
         uint8_t *cp = cur + (size_t)W16 * H16 + (size_t)comp * CW * CH;
-        *(uint32_t *)(cp + (size_t)(mby * 8 + row) * CW + mbx * 8 + q2 * 4) =
-            *(const uint32_t *)(s_out + 256 + comp * 64 + row * 8 + q2 * 4);
+        *(uint32_t *)(cp + (size_t)(mby * 8 + row) * CW + mbx * 8 + q2 * 4) = *(const uint32_t *)(s_px + 256 + comp * 64 + row * 8 + q2 * 4);
     }
-    if (lane == 0 && e) atomicOr(a.err + p, 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -608,7 +648,7 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
 #define I4SCHED0 0xFEDC765410ull
 #define I4SCHED1 0xFFBA9832FFull
 
-__device__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
+__device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
                            uint8_t *ty, uint8_t *tu, uint8_t *tv, int lane)
 {
     const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C;
@@ -735,13 +775,10 @@ __device__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const i
 // Every output sample is written exactly once, by the MB that finalises it,
 // so no other ordering of frame stores is needed.
 // ---------------------------------------------------------------------------
-// MB rows (waves) per k_rows workgroup.  Rows inside a workgroup hand off
-// through an LDS ring, rows at band edges through HBM granules.  Measured at
-// 1080p x 8 streams (r01): 1 row 950 us, 2 rows 969, 4 rows 977, 8 rows 1025
-// per k_rows launch -- the row lag is set by the MB dependency chain, not by
-// the hand-off latency, and more waves per SIMD slow every row.
-#define ROWS_PER_WG 1
-#define RING_K 16     // LDS ring slots (MB columns) per in-workgroup row hand-off
+// One MB row per single-wave workgroup.  (Measured at 1080p x 8 streams:
+// bands of 2/4/8 rows per workgroup handing off through an LDS ring ran
+// 969/977/1025 us per launch vs 950 us -- the row lag is set by the MB
+// dependency chain, not by the hand-off latency.)
 #define RY_S 20       // region luma stride (cols -4..15)
 #define RC_S 20       // region chroma stride (cols -4..7, padded to the luma stride)
 
@@ -872,30 +909,35 @@ __device__ __forceinline__ void st_gran(unsigned long long *p, uint32_t v, uint3
     __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ unsigned long long lds_gran_ld(const unsigned long long *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_gran_st(unsigned long long *p, uint32_t v, uint32_t tag)
-{
-    __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
+// LDS hand-off ring between the MC waves of a row workgroup and its row
+// unit: slot c % RING_K holds MB c's MC samples, residual and deblocking
+// record; flag[slot] = c + 1 once filled, consumed = c + 1 once the row unit
+// no longer reads MB c's slot.  LDS instructions of one wave execute in
+// order, so a flag written after the data (compiler barrier between) is
+// seen after it by every other wave of the workgroup.
+#ifndef RING_K
+#define RING_K 8
+#endif
+struct __attribute__((aligned(16))) MbRing {
+    uint8_t px[RING_K][384];
+    int16_t res[RING_K][384];
+    uint8_t db[RING_K][64];
+    int flag[RING_K];
+    int consumed;
+};
 
-__global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
+__device__ __forceinline__ int lds_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// One MB row of picture p, left to right (one wave).  RING: MB c's MC
+// outputs come from the workgroup's MC waves through the LDS ring (k_wg);
+// otherwise from k_mb's HBM outputs (k_rows).  PIPE (RING only): frame
+// stores are sc1 and per-row progress is published for later pictures' MC.
+template <bool PIPE, bool RING>
+__device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, MbRing *R)
 {
-    __shared__ RowLds s_rows[ROWS_PER_WG];
-    __shared__ unsigned long long s_ring[ROWS_PER_WG > 1 ? ROWS_PER_WG - 1 : 1][RING_K * 32];
-    __shared__ int s_done[ROWS_PER_WG];
+    static_assert(RING || !PIPE, "pipelined row units take MC outputs from the LDS ring");
     const int W = a.w, H = a.h;
-    const int p = blockIdx.x % a.npics, band = blockIdx.x / a.npics;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (ROWS_PER_WG > 1)
-        for (int i = threadIdx.x; i < (ROWS_PER_WG - 1) * RING_K * 32; i += blockDim.x) (&s_ring[0][0])[i] = 0;
-    if (threadIdx.x < ROWS_PER_WG) s_done[threadIdx.x] = 0;
-    __syncthreads();                              // the only workgroup barrier
-    const int r = band * ROWS_PER_WG + wid;
-    if (r >= H) return;
-    RowLds &L = s_rows[wid];
     const PicDesc *pdp = a.pics + p;
     const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
     const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
@@ -907,12 +949,6 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
     unsigned *perr = a.err + p;
     const uint32_t tag = a.epoch;
     const bool has_up = r > 0, has_down = r + 1 < H;
-    // hand-off inside the workgroup (LDS ring) or across bands (HBM granules)
-    const bool up_lds = has_up && wid > 0, down_lds = has_down && wid < ROWS_PER_WG - 1;
-    const unsigned long long *ring_up = up_lds ? s_ring[wid - 1] : nullptr;
-    unsigned long long *ring_me = down_lds ? s_ring[wid] : nullptr;
-    int *done_me = &s_done[wid];
-    const int *done_down = &s_done[down_lds ? wid + 1 : wid];
     const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
     unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
     const bool last_row = r == H - 1;
@@ -933,16 +969,20 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
     const int tsel = lane < 32 ? 0 : lane == 32 ? 1 : lane < 36 ? 2 : 0;
     const int tdw = lane < 32 ? lane : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 0;
 
+    uint32_t *progress_me = PIPE ? a.progress + (size_t)p * H + r : nullptr;
+
     // prefetch registers for MB (r, 0)
-    uint32_t n_db, n_y, n_c, n_r0, n_r1, n_r2;
+    uint32_t n_db = 0, n_y = 0, n_c = 0, n_r0 = 0, n_r1 = 0, n_r2 = 0;
     uint32_t n_h0, n_h1, n_h2, n_h3, n_h4, n_h5;   // record dwords 0..5 (uniform)
     {
-        const int g0 = rec_base + r * W;
-        n_db = ((const uint32_t *)(a.dbrec + (size_t)g0 * 64))[lane & 15];
-        n_y = *(const uint32_t *)(cur + yoff);
-        n_c = *(const uint32_t *)(cplane + coff);
-        const uint32_t *rs = (const uint32_t *)(a.res + (size_t)g0 * 384);
-        n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+        if (!RING) {
+            const int g0 = rec_base + r * W;
+            n_db = ((const uint32_t *)(a.dbrec + (size_t)g0 * 64))[lane & 15];
+            n_y = *(const uint32_t *)(cur + yoff);
+            n_c = *(const uint32_t *)(cplane + coff);
+            const uint32_t *rs = (const uint32_t *)(a.res + (size_t)g0 * 384);
+            n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+        }
         n_h0 = recw[0]; n_h1 = recw[1]; n_h2 = recw[2]; n_h3 = recw[3]; n_h4 = recw[4]; n_h5 = recw[5];
         // retire these before the loop: otherwise the waitcnt pass merges their
         // pending state into the loop header and, inside the loop, waits for
@@ -955,7 +995,7 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
     uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
 
     for (int c = 0; c < W; c++) {
-        const uint32_t db_w = n_db, own_y = n_y, own_c = n_c, res0 = n_r0, res1 = n_r1, res2 = n_r2;
+        const uint32_t db_w = n_db, n_y0 = n_y, n_c0 = n_c, res0 = n_r0, res1 = n_r1, res2 = n_r2;
         const uint32_t h0 = __builtin_amdgcn_readfirstlane(n_h0), h1 = __builtin_amdgcn_readfirstlane(n_h1);
         const uint32_t cbits = __builtin_amdgcn_readfirstlane(n_h2), qcoef = __builtin_amdgcn_readfirstlane(n_h3);
         const uint64_t i4 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(n_h5) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(n_h4);
@@ -973,24 +1013,39 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
         // an MB; lanes 0..23 (final rows) after its next MB's vertical edges.
         const int ce = tsel == 0 ? c : tsel == 1 ? min(c + 1, W - 1) : max(c - 1, 0);
         const unsigned long long *tga = mbx_up + (size_t)ce * 32 + tdw;
-        const unsigned long long *tgl = up_lds ? ring_up + (ce % RING_K) * 32 + tdw : nullptr;
-        const uint32_t want = up_lds ? (uint32_t)ce + 1 : tag;     // ring tags: column + 1
         unsigned long long gr = 0;
-        if (has_up) gr = up_lds ? lds_gran_ld(tgl) : ld_gran(tga);
+        if (has_up) gr = ld_gran(tga);
         // ---- prefetch MB (r, c+1) (clamped: the last iteration re-reads MB W-1)
         {
             const int cn = min(c + 1, W - 1);
-            const int gn = rec_base + r * W + cn;
-            n_db = ((const uint32_t *)(a.dbrec + (size_t)gn * 64))[lane & 15];
-            n_y = *(const uint32_t *)(cur + yoff + cn * 16);
-            n_c = *(const uint32_t *)(cplane + coff + cn * 8);
-            const uint32_t *rs = (const uint32_t *)(a.res + (size_t)gn * 384);
-            n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+            if (!RING) {
+                const int gn = rec_base + r * W + cn;
+                n_db = ((const uint32_t *)(a.dbrec + (size_t)gn * 64))[lane & 15];
+                n_y = *(const uint32_t *)(cur + yoff + cn * 16);
+                n_c = *(const uint32_t *)(cplane + coff + cn * 8);
+                const uint32_t *rs = (const uint32_t *)(a.res + (size_t)gn * 384);
+                n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+            }
             const cu32p rw = recw + cn * 24;
             n_h0 = rw[0]; n_h1 = rw[1]; n_h2 = rw[2]; n_h3 = rw[3]; n_h4 = rw[4]; n_h5 = rw[5];
         }
+        // ---- RING: wait for the MC waves to fill MB c's slot
+        const int slot = c & (RING_K - 1);
+        uint32_t own_y = n_y0, own_c = n_c0;
+        if (RING) {
+            unsigned spins = 0;
+            const unsigned long long tw = prof ? clock64() : 0;
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
+            }
+            wave_sync();
+            if (prof) pt[7] += clock64() - tw;
+            own_y = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
+            own_c = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
+        }
         // ---- own samples / residual / deblocking record into LDS
-        if (lane < 16) ((uint32_t *)L.db)[lane] = db_w;
+        if (lane < 16) ((uint32_t *)L.db)[lane] = RING ? ((const uint32_t *)R->db[slot])[lane] : db_w;
         if (qtype == MBT_IPCM) {
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)coef_base + qcoef) * 16);
             const uint32_t py = src[lane], pc = src[64 + li];
@@ -999,7 +1054,7 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
         } else if (!intra) {
             *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = own_y;
             if (lane < 32) *(uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4] = own_c;
-        } else if (cbits) {
+        } else if (!RING && cbits) {
             ((uint32_t *)L.res)[lane] = res0;
             ((uint32_t *)L.res)[64 + lane] = res1;
             ((uint32_t *)L.res)[128 + lane] = res2;
@@ -1012,10 +1067,10 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
         auto fetch_top = [&](bool unfiltered) {
             const bool mine = unfiltered ? (lane >= 24 && lane < 36) : lane < 24;
             unsigned spins = 0;
-            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != want) != 0) {
+            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-                gr = up_lds ? lds_gran_ld(tgl) : ld_gran(tga);
+                gr = ld_gran(tga);
             }
             top = (uint32_t)gr;
             if (prof && lane == 0) pmb[1] = wall_clock64();
@@ -1044,7 +1099,7 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
                 L.tv[(k + 1) * TC_STRIDE] = L.left_unf[24 + k];
             }
             wave_sync();
-            intra_tile(qtype, avail, pred, i4, L.res, cbits != 0, L.ty, L.tu, L.tv, lane);
+            intra_tile(qtype, avail, pred, i4, RING ? R->res[slot] : L.res, cbits != 0, L.ty, L.tu, L.tv, lane);
             {   // tile samples start at column 1: byte reads (LDS dword reads must be aligned)
                 const uint8_t *sy = &L.ty[(orow + 1) * TY_STRIDE + 1 + oq * 4];
                 *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = sy[0] | (sy[1] << 8) | (sy[2] << 16) | ((uint32_t)sy[3] << 24);
@@ -1057,6 +1112,8 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
             }
         }
         wave_sync();
+        // MB c's ring slot is no longer read: hand it back to the MC waves
+        if (RING && lane == 0) lds_st(&R->consumed, c + 1);
 
         // ---- unfiltered edges: bottom row (mailbox dwords 24..31), right column
         uint32_t unf;
@@ -1070,19 +1127,7 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
             if (lane < 32) L.left_unf[lane] = rc;
         }
         // publish this MB's unfiltered bottom row (the row below's intra neighbours)
-        if (down_lds) {
-            // ring slot c % K last held column c-K, read by the row below up to
-            // its iteration c-K+1: wait until that iteration is done
-            if (c - RING_K + 2 > 0) {
-                unsigned spins = 0;
-                while (__hip_atomic_load(done_down, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < c - RING_K + 2) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }
-                }
-            }
-            if (lane >= 24 && lane < 32) lds_gran_st(ring_me + (c % RING_K) * 32 + lane, unf, (uint32_t)c + 1);
-        } else if (has_down && lane >= 24 && lane < 32) st_gran(mbx_me + (size_t)c * 32 + lane, unf, tag);
-
+        if (has_down && lane >= 24 && lane < 32) st_gran(mbx_me + (size_t)c * 32 + lane, unf, tag);
         if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
         // ---- vertical edges (need only this row's samples)
         if (dbf) {
@@ -1099,10 +1144,7 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
                                            : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
             const bool is_patch = li < 16 ? (li & 3) == 3 : (li < 24 && qq);
             const uint32_t ent = is_patch ? patch : prov;
-            if (c > 0 && lane < 24) {
-                if (down_lds) lds_gran_st(ring_me + ((c - 1) % RING_K) * 32 + lane, ent, (uint32_t)c);
-                else st_gran(mbx_me + (size_t)(c - 1) * 32 + lane, ent, tag);
-            }
+            if (c > 0 && lane < 24) st_gran(mbx_me + (size_t)(c - 1) * 32 + lane, ent, tag);
             if (prof && lane == 0) pmb[2] = wall_clock64();
         }
         if (prof) { tc1 = clock64(); pt[3] += tc1 - tc0; tc0 = tc1; }
@@ -1132,31 +1174,37 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
         if (prof) { tc1 = clock64(); pt[2] += tc1 - tc0; tc0 = tc1; }
 
         // ---- frame stores, once per sample
+        if (PIPE) {
+            // the stores of iterations < c have had a whole iteration to land:
+            // drain them and tell the next picture's MC (progress = c)
+            drain_vm();
+            if (lane == 0) st_sc1_u32(progress_me, (tag << 12) | (uint32_t)c);
+        }
         {
             const int yrows = last_row ? 16 : 12;
             const int crows = last_row ? 8 : 6;
             const bool last_col = c == W - 1;
             if (orow < yrows && (oq < 3 || last_col))
-                *(uint32_t *)(cur + yoff + c * 16) = *(const uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4];
+                st32<PIPE>(cur + yoff + c * 16, *(const uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4]);
             if (lane < 32 && crow < crows && (cq == 0 || last_col))
-                *(uint32_t *)(cplane + coff + c * 8) = *(const uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4];
+                st32<PIPE>(cplane + coff + c * 8, *(const uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
             if (c > 0) {    // left halo: MB (r,c-1) luma cols 12..15 / chroma cols 4..7
                 if (lane < 16) {
                     if (lane < yrows)
-                        *(uint32_t *)(cur + (size_t)(r * 16 + lane) * W16 + c * 16 - 4) = *(const uint32_t *)&L.ry[(lane + 4) * RY_S];
+                        st32<PIPE>(cur + (size_t)(r * 16 + lane) * W16 + c * 16 - 4, *(const uint32_t *)&L.ry[(lane + 4) * RY_S]);
                 } else if (lane < 32) {
                     const int k = lane - 16, comp = k >> 3, row = k & 7;
                     if (row < crows)
-                        *(uint32_t *)((comp ? curV : curU) + (size_t)(r * 8 + row) * CW + c * 8 - 4) = *(const uint32_t *)&(comp ? L.rv : L.ru)[(row + 2) * RC_S];
+                        st32<PIPE>((comp ? curV : curU) + (size_t)(r * 8 + row) * CW + c * 8 - 4, *(const uint32_t *)&(comp ? L.rv : L.ru)[(row + 2) * RC_S]);
                 }
             }
             if (has_up) {   // top halo: MB (r-1,c) luma rows 12..15, chroma rows 6..7 (now final)
                 if (lane >= 32 && lane < 48) {
                     const int k = lane - 32;
-                    *(uint32_t *)(cur + (size_t)(r * 16 - 4 + (k >> 2)) * W16 + c * 16 + (k & 3) * 4) = *(const uint32_t *)&L.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4];
+                    st32<PIPE>(cur + (size_t)(r * 16 - 4 + (k >> 2)) * W16 + c * 16 + (k & 3) * 4, *(const uint32_t *)&L.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
                 } else if (lane >= 48 && lane < 56) {
                     const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-                    *(uint32_t *)((comp ? curV : curU) + (size_t)(r * 8 - 2 + row) * CW + c * 8 + qq * 4) = *(const uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4];
+                    st32<PIPE>((comp ? curV : curU) + (size_t)(r * 8 - 2 + row) * CW + c * 8 + qq * 4, *(const uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4]);
                 }
             }
         }
@@ -1169,16 +1217,15 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
             *(uint32_t *)&D[(row + 2) * RC_S] = *(const uint32_t *)&D[(row + 2) * RC_S + 8];
         }
         wave_sync();
-        // this row no longer needs the row above's entries <= c
-        if (lane == 0) __hip_atomic_store(done_me, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (prof) { tc1 = clock64(); pt[4] += tc1 - tc0; }
     }
     // last entry of the row is final as it stands
     if (has_down) {
-        if (lane < 24) {
-            if (down_lds) lds_gran_st(ring_me + ((W - 1) % RING_K) * 32 + lane, prov, (uint32_t)W);
-            else st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, prov, tag);
-        }
+        if (lane < 24) st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, prov, tag);
+    }
+    if (PIPE) {
+        drain_vm();
+        if (lane == 0) st_sc1_u32(progress_me, (tag << 12) | (uint32_t)W);
     }
     if (prof && lane == 0) {
         unsigned long long *o = a.prof + ((size_t)r * a.npics + p) * 16;
@@ -1186,3 +1233,71 @@ __global__ __launch_bounds__(ROWS_PER_WG * 64) void k_rows(ReconArgs a)
         for (int i = 0; i < 8; i++) o[2 + i] = pt[i];
     }
 }
+
+__global__ __launch_bounds__(64) void k_rows(ReconArgs a)
+{
+    __shared__ RowLds L;
+    const int p = blockIdx.x % a.npics, r = blockIdx.x / a.npics;
+    if (r >= a.h) return;
+    row_unit<false, false>(a, p, r, L, threadIdx.x, nullptr);
+}
+
+// ---------------------------------------------------------------------------
+// k_wg: one workgroup per (picture, MB row): wave 0 is the row unit, waves
+// 1..NMC compute the row's MBs (deblocking record, residual, MC) round-robin
+// into the LDS ring, at most RING_K MBs ahead of the row unit.  No HBM round
+// trip between MC and reconstruction.
+//
+// The launch covers P pictures of S streams (picture index k*S + s); the host
+// orders the (k, r) pairs in a.order so that a workgroup only ever waits on
+// workgroups dispatched before it (dispatch follows blockIdx; every wait is
+// bounded): the row above (tagged granules) and, PIPE, the rows of earlier
+// pictures of the launch its MVs reach (per-row progress, sc1 stores/loads).
+// blockIdx = pair * S + s, so with round-robin placement stream s stays on
+// XCD s % 8 (speed only).
+// ---------------------------------------------------------------------------
+template <bool PIPE, int NMC>
+__global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
+{
+    __shared__ RowLds L;
+    __shared__ McScratch M[NMC];
+    __shared__ MbRing R;
+    const int S = a.S;
+    const int pair = blockIdx.x / S, s = blockIdx.x - pair * S;
+    const uint32_t kr = a.order[pair];
+    const int k = (int)(kr >> 16), r = (int)(kr & 0xFFFF);
+    const int p = k * S + s;
+    if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
+    if (threadIdx.x == 0) R.consumed = 0;
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wid == 0) {
+        // the row unit is the dependency chain: it wins issue over the MC
+        // waves sharing its SIMD
+        __builtin_amdgcn_s_setprio(3);
+        row_unit<PIPE, true>(a, p, r, L, lane, &R);
+        return;
+    }
+    McScratch &Mw = M[wid - 1];
+    for (int c = wid - 1; c < a.w; c += NMC) {
+        const int slot = c & (RING_K - 1);
+        if (c >= RING_K) {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RING_K + 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }   // bounded wait
+            }
+            wave_sync();
+        }
+        const unsigned long long t0 = a.prof ? clock64() : 0;
+        mc_core<PIPE>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot]);
+        wave_sync();
+        if (a.prof && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
+        if (lane == 0) lds_st(&R.flag[slot], c + 1);
+    }
+}
+#ifndef WG_NMC
+#define WG_NMC 3
+#endif
+template __global__ void k_wg<false, WG_NMC>(ReconArgs);
+template __global__ void k_wg<true, WG_NMC>(ReconArgs);

@@ -98,6 +98,16 @@ class Engine:
         if self._L.h264mi_engine_decode_device(self._h, npics, d_recs, d_coef, d_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device failed")
 
+    def set_pipeline(self, depth: int) -> None:
+        if self._L.h264mi_engine_set_pipeline(self._h, int(depth)) != 0:
+            raise RuntimeError("h264mi_engine_set_pipeline failed")
+
+    def decode_pipelined(self, nstreams: int, depth: int, d_recs: int, d_coef: int, d_pics: int,
+                         base_pic: int, lag_rows: int) -> None:
+        if self._L.h264mi_engine_decode_pipelined(self._h, nstreams, depth, d_recs, d_coef, d_pics,
+                                                  int(base_pic), int(lag_rows)) != 0:
+            raise RuntimeError("h264mi_engine_decode_pipelined failed")
+
     def read(self, stream: int, slot: int) -> np.ndarray:
         out = np.empty(self.frame_bytes, dtype=np.uint8)
         if self._L.h264mi_engine_read(self._h, stream, slot, out.ctypes.data) != 0:

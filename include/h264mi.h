@@ -148,6 +148,21 @@ int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
  * the summed durations of k_mb and of k_rows, in microseconds */
 int  h264mi_engine_set_timing(h264mi_engine *e, int max_batches);
 int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches);
+/* frame-pipelined batches: one launch reconstructs `depth` consecutive
+ * pictures of each of `nstreams` streams, and a picture's motion
+ * compensation starts as soon as the reference samples it reads are final
+ * (per-MB dependency tracking on the GPU).  set_pipeline sizes the
+ * per-picture buffers (nstreams x depth).  d_pics: nstreams*depth PicDesc,
+ * picture-major (k*nstreams + s).  Frame slots form a ring: picture k of
+ * the launch writes slot (base_pic + k) mod nslots of its stream and record
+ * ref[] fields name ring slots, so no picture of a launch overwrites a slot
+ * another picture of the launch reads (nslots >= depth + reference span).
+ * lag_rows: row k+1 of the launch's picture order trails by this many MB
+ * rows; it must exceed every MV's reference reach in MB rows by 2 (the
+ * caller computes it from the records; <= 0 = whole pictures in sequence). */
+int  h264mi_engine_set_pipeline(h264mi_engine *e, int depth);
+int  h264mi_engine_decode_pipelined(h264mi_engine *e, int nstreams, int depth, const void *d_recs,
+                                    const int16_t *d_coef, const void *d_pics, int base_pic, int lag_rows);
 /* diagnostics: per k_rows workgroup (row r of batch picture p at index
  * r * npics + p) 16 u64: wall-clock start/end (100 MHz) and shader-clock sums
  * of its phases, then 4 u64 per MB (hand-off timestamps); enable != 0 allocates, out != NULL copies the last launch */

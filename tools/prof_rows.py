@@ -1,5 +1,6 @@
 """Diagnostics: k_rows per-row phase clocks on the bench workload (not a test)."""
 import sys, os, ctypes as C, numpy as np
+os.environ.setdefault("H264MI_KERNEL", "classic")   # classic: k_rows phases; wg: k_wg (+ MC cycles per MB)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench
 from broadway_amd import _lib
@@ -8,7 +9,7 @@ L = _lib.mi()
 S = 8
 streams, caps = bench.prepare(3, [100 + i for i in range(S)], 6)
 w, h = caps[0].w_mbs, caps[0].h_mbs
-d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6)
+d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6, 1, 0)
 eng = Engine(w, h, S, nslots)
 L.h264mi_engine_profile(eng._h, 1, None, 0)
 for k in range(6):
@@ -23,7 +24,12 @@ for k in range(6):
     ph = a[:, :, 2:10] / w           # cycles per MB
     print(f"pic {k}: span {en.max():.1f} us; row start  r0 {st[0].mean():.1f} r1 {st[1].mean():.1f} r10 {st[10].mean():.1f} r67 {st[-1].mean():.1f}; "
           f"row dur r0 {(en[0]-st[0]).mean():.1f} r34 {(en[34]-st[34]).mean():.1f} r67 {(en[-1]-st[-1]).mean():.1f}")
-    print("   cycles/MB  pre(+intra wait) %.0f  V %.0f  H %.0f  publish %.0f  stores %.0f  top-wait %.0f  intra+unf %.0f" % tuple(ph.mean(axis=(0, 1)))[:7])
+    print("   cycles/MB  pre(+intra wait) %.0f  V %.0f  H %.0f  publish %.0f  stores %.0f  top-wait %.0f  intra+unf %.0f ring-wait %.0f" % tuple(ph.mean(axis=(0, 1))))
+    if os.environ["H264MI_KERNEL"] == "wg":
+        mbuf = (C.c_uint64 * (S * h * 16 + S * w * h * 4))()
+        L.h264mi_engine_profile(eng._h, 1, mbuf, len(mbuf))
+        mc = np.frombuffer(mbuf, dtype=np.uint64)[S * h * 16:].reshape(S, h, w, 4)[:, :, :, 3].astype(np.float64)
+        print("   MC wave cycles/MB mean %.0f p50 %.0f p90 %.0f max %.0f" % (mc.mean(), np.percentile(mc, 50), np.percentile(mc, 90), mc.max()))
     print("   row0 cycles/MB", " ".join("%.0f" % x for x in ph[0].mean(axis=0)), " row40", " ".join("%.0f" % x for x in ph[40].mean(axis=0)))
 
 # per-MB hand-off timing of the last picture batch (100 MHz clock -> us)
