@@ -32,6 +32,12 @@ struct h264mi_engine {
     uint32_t *d_progress;         // k_wg<PIPE>: per picture row drained-store progress
     uint32_t *d_order, *h_order;  // k_wg: (picture, row) dispatch order
     int classic;                  // single-picture launches: k_mb + k_rows (default) or k_wg (H264MI_KERNEL=wg)
+    // stream groups (h264mi_engine_set_groups): the pictures of a device-input
+    // batch split into G groups, each on its own HIP stream, so one group's
+    // k_mb overlaps the other groups' latency-bound k_rows
+    int ngroups;
+    hipStream_t gst[H264MI_MAX_GROUPS];
+    int stagger_pending;
     int order_depth, order_lag;
     uint8_t *d_dbrec;         // 64 B per batch MB
     int16_t *d_res;           // 384 x int16 per batch MB (intra residual)
@@ -106,6 +112,7 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
     e->h_coef_cap = e->coef_cap;
     e->timing = getenv("H264MI_TIMING") != NULL;
+    e->ngroups = 1;
     {
         const char *km = getenv("H264MI_KERNEL");
         e->classic = !(km && !strcmp(km, "wg"));
@@ -150,6 +157,8 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
     h264mi_engine_set_timing(e, 0);
+    for (int g = 0; g < H264MI_MAX_GROUPS; g++)
+        if (e->gst[g]) { (void)hipStreamSynchronize(e->gst[g]); (void)hipStreamDestroy(e->gst[g]); }
     if (e->st) (void)hipStreamDestroy(e->st);
     free(e);
 }
@@ -171,8 +180,18 @@ static int pipe_order(h264mi_engine *e, int depth, int lag)
     return 0;
 }
 
+// one-off offset of a group stream (stagger): spin on the wall clock (100 MHz)
+__global__ void k_delay(unsigned long long ticks)
+{
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+static int launch_groups(h264mi_engine *e, int npics, ReconArgs a);
+
 static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
-                        const PicDesc *d_pics, bool pipe = false, int depth = 1, int base_pic = 0, int lag = 0)
+                        const PicDesc *d_pics, bool pipe = false, int depth = 1, int base_pic = 0, int lag = 0,
+                        bool grouped = false)
 {
     ReconArgs a;
     memset(&a, 0, sizeof(a));
@@ -182,6 +201,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.coef = d_coef;
     a.mbx = e->d_mbx;
     if (++e->epoch >= (1u << 20)) {           // tags: granules epoch, progress (epoch << 12) | count
+        if (h264mi_engine_sync(e)) return -1; // group streams may still read the mailboxes
         HIPCHECK(hipMemsetAsync(e->d_mbx, 0, (size_t)e->pipe_cap * e->nmbs * 256, e->st));
         HIPCHECK(hipMemsetAsync(e->d_progress, 0, (size_t)e->pipe_cap * e->h * 4, e->st));
         e->epoch = 1;
@@ -198,6 +218,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.S = npics / depth;
     a.ring = e->nslots;
     a.base_pic = base_pic % e->nslots;
+    if (grouped && !pipe && e->classic && e->ngroups > 1 && npics >= e->ngroups) return launch_groups(e, npics, a);
     HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * npics, e->st));
     const bool wg = pipe || !e->classic;
     if (wg) {
@@ -229,6 +250,56 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     if (rec) (void)hipEventRecord(t2, e->st);
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
+    return 0;
+}
+
+// k_mb + k_rows per group of pictures, each group on its own stream.  Groups
+// use disjoint mailbox / error ranges (picture index p0.. of the batch);
+// deblocking records and residuals are per batch MB already.
+static int launch_groups(h264mi_engine *e, int npics, ReconArgs a)
+{
+    const int G = e->ngroups;
+    for (int g = 0; g < G; g++) {
+        const int p0 = g * npics / G, n = (g + 1) * npics / G - p0;
+        hipStream_t gs = e->gst[g];
+        if (e->stagger_pending && g > 0) {
+            // offset group g by g/G of an estimated picture latency, once:
+            // equal-length group cycles then keep the groups' k_mb apart
+            const double est_us = (e->w + 3.0 * e->h) * 2.8;
+            hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, gs, (unsigned long long)(est_us * 100.0 * g / G));
+        }
+        ReconArgs ag = a;
+        ag.pics = a.pics + p0;
+        ag.npics = n;
+        ag.mbx = e->d_mbx + (size_t)p0 * e->nmbs * 32;
+        ag.err = e->d_err + p0;
+        ag.prof = NULL;
+        HIPCHECK(hipMemsetAsync(ag.err, 0, sizeof(unsigned) * n, gs));
+        const bool rec = g == 0 && e->tev && e->tev_n < e->tev_cap;
+        hipEvent_t t0 = rec ? e->tev[3 * e->tev_n] : NULL, t1 = rec ? e->tev[3 * e->tev_n + 1] : NULL,
+                   t2 = rec ? e->tev[3 * e->tev_n + 2] : NULL;
+        if (rec) (void)hipEventRecord(t0, gs);
+        hipLaunchKernelGGL(k_mb, dim3(((n * e->nmbs + 7) / 8) * 8), dim3(64), 0, gs, ag);
+        HIPCHECK(hipGetLastError());
+        if (rec) (void)hipEventRecord(t1, gs);
+        hipLaunchKernelGGL(k_rows, dim3(n * e->h), dim3(64), 0, gs, ag);
+        HIPCHECK(hipGetLastError());
+        if (rec) { (void)hipEventRecord(t2, gs); e->tev_n++; }
+        HIPCHECK(hipMemcpyAsync(e->h_err + p0, ag.err, sizeof(unsigned) * n, hipMemcpyDeviceToHost, gs));
+    }
+    e->stagger_pending = 0;
+    return 0;
+}
+
+extern "C" int h264mi_engine_set_groups(h264mi_engine *e, int ngroups)
+{
+    if (!e || ngroups < 1 || ngroups > H264MI_MAX_GROUPS || ngroups > e->nstreams) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    if (h264mi_engine_sync(e)) return -1;
+    for (int g = 0; g < ngroups; g++)
+        if (!e->gst[g]) HIPCHECK(hipStreamCreateWithFlags(&e->gst[g], hipStreamNonBlocking));
+    e->ngroups = ngroups;
+    e->stagger_pending = ngroups > 1;
     return 0;
 }
 
@@ -276,7 +347,7 @@ extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const vo
 {
     if (!e || npics < 1 || npics > e->nstreams) return -1;
     HIPCHECK(hipSetDevice(e->dev));
-    return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics);
+    return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, false, 1, 0, 0, true);
 }
 
 extern "C" int h264mi_engine_set_pipeline(h264mi_engine *e, int depth)
@@ -307,6 +378,8 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     if (!e) return -1;
     HIPCHECK(hipSetDevice(e->dev));
     HIPCHECK(hipStreamSynchronize(e->st));
+    for (int g = 0; g < H264MI_MAX_GROUPS; g++)
+        if (e->gst[g]) HIPCHECK(hipStreamSynchronize(e->gst[g]));
     for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
     memset(e->h_err, 0, sizeof(unsigned) * e->pipe_cap);
     return 0;
@@ -352,7 +425,7 @@ extern "C" int h264mi_engine_set_timing(h264mi_engine *e, int max_batches)
 extern "C" int h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches)
 {
     if (!e || !e->tev) return -1;
-    HIPCHECK(hipStreamSynchronize(e->st));
+    if (h264mi_engine_sync(e)) return -1;
     double a = 0, b = 0;
     for (int i = 0; i < e->tev_n; i++) {
         float m0 = 0, m1 = 0;

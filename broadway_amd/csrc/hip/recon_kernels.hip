@@ -792,6 +792,7 @@ struct __attribute__((aligned(16))) RowLds {
     uint8_t tu[9 * TC_STRIDE];
     uint8_t tv[9 * TC_STRIDE];
     uint8_t left_unf[32];       // unfiltered right column of the previous MB: Y16 U8 V8
+    uint8_t junk[256];          // per-lane sink of unconditional LDS stores (lanes with nothing to store)
 };
 
 
@@ -801,7 +802,13 @@ __device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn
 // use p1..q1.  filterSamples / bS<4 / bS==4 of deblocking.c:1543-1736.  The
 // bS==4 arithmetic runs only when some lane of the wave has bS==4 on this
 // edge (wave-uniform branch); everything else is select-based.
-__device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int alpha, int beta, int tc0s,
+// keep a value computed where it stands: the filter updates below are cheap
+// enough to compute for every lane and select, instead of the compiler
+// sinking them into exec-masked blocks (each costs more scalar work than it
+// saves)
+#define MATERIALIZE(x) asm volatile("" : "+v"(x))
+
+__device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int alpha, int beta, uint32_t tc0s,
                                           bool chroma)
 {
     const int o = 4 * k;
@@ -810,29 +817,38 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int
     const int d0 = absd(p0, q0);
     const bool f = bS != 0 && d0 < alpha && absd(p1, p0) < beta && absd(q1, q0) < beta;
     const bool ap = !chroma && absd(p2, p0) < beta, aq = !chroma && absd(q2, q0) < beta;
-    // bS < 4
-    const int tc0 = (tc0s >> (((bS - 1) & 3) * 8)) & 255;
+    // bS < 4 (8.7.2.3)
+    const int tc0 = (int)__builtin_amdgcn_ubfe(tc0s, (uint32_t)((bS - 1) & 3) * 8, 8);
     const int tc = tc0 + (chroma ? 1 : (int)ap + (int)aq);
     const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
     const int avg = (p0 + q0 + 1) >> 1;
+    int n_p1 = p1 + clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1);
+    int n_q1 = q1 + clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1);
+    int n_p0 = clip255(p0 + d), n_q0 = clip255(q0 - d);
+    MATERIALIZE(n_p1); MATERIALIZE(n_q1); MATERIALIZE(n_p0); MATERIALIZE(n_q0);
     int r_p2 = p2, r_q2 = q2;
-    int r_p1 = f && ap ? p1 + clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1) : p1;
-    int r_q1 = f && aq ? q1 + clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1) : q1;
-    int r_p0 = f ? clip255(p0 + d) : p0;
-    int r_q0 = f ? clip255(q0 - d) : q0;
+    int r_p1 = f && ap ? n_p1 : p1;
+    int r_q1 = f && aq ? n_q1 : q1;
+    int r_p0 = f ? n_p0 : p0;
+    int r_q0 = f ? n_q0 : q0;
+    // bS == 4 (8.7.2.4): MB edges of intra MBs only -- skipped unless some lane needs it
     const bool b4 = f && bS >= 4;
     if (__builtin_amdgcn_ballot_w64(b4) != 0) {
         const int p3 = v[o], q3 = v[o + 7];
         const bool strong = d0 < ((alpha >> 2) + 2);
         const bool sp = ap && strong, sq = aq && strong;
-        const int s_p0 = sp ? (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3 : (2 * p1 + p0 + q1 + 2) >> 2;
-        const int s_q0 = sq ? (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3 : (2 * q1 + q0 + p1 + 2) >> 2;
-        r_p0 = b4 ? s_p0 : r_p0;
-        r_q0 = b4 ? s_q0 : r_q0;
-        r_p1 = b4 ? (sp ? (p2 + p1 + p0 + q0 + 2) >> 2 : p1) : r_p1;
-        r_q1 = b4 ? (sq ? (p0 + q0 + q1 + q2 + 2) >> 2 : q1) : r_q1;
-        r_p2 = b4 && sp ? (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3 : r_p2;
-        r_q2 = b4 && sq ? (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3 : r_q2;
+        int s_p0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, w_p0 = (2 * p1 + p0 + q1 + 2) >> 2;
+        int s_q0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, w_q0 = (2 * q1 + q0 + p1 + 2) >> 2;
+        int s_p1 = (p2 + p1 + p0 + q0 + 2) >> 2, s_q1 = (p0 + q0 + q1 + q2 + 2) >> 2;
+        int s_p2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, s_q2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+        MATERIALIZE(s_p0); MATERIALIZE(w_p0); MATERIALIZE(s_q0); MATERIALIZE(w_q0);
+        MATERIALIZE(s_p1); MATERIALIZE(s_q1); MATERIALIZE(s_p2); MATERIALIZE(s_q2);
+        r_p0 = b4 ? (sp ? s_p0 : w_p0) : r_p0;
+        r_q0 = b4 ? (sq ? s_q0 : w_q0) : r_q0;
+        r_p1 = b4 ? (sp ? s_p1 : p1) : r_p1;
+        r_q1 = b4 ? (sq ? s_q1 : q1) : r_q1;
+        r_p2 = b4 && sp ? s_p2 : r_p2;
+        r_q2 = b4 && sq ? s_q2 : r_q2;
     }
     v[o + 1] = r_p2; v[o + 2] = r_p1; v[o + 3] = r_p0;
     v[o + 4] = r_q0; v[o + 5] = r_q1; v[o + 6] = r_q2;
@@ -846,7 +862,7 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int
 // 32..63 mirror lanes 0..31 (same addresses, same values) so that every
 // access is unconditional.
 __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, uint8_t *ry, uint8_t *ru, uint8_t *rv,
-                                            int lane, bool mb_edge_on)
+                                            uint8_t *junk, int lane, bool mb_edge_on)
 {
     const int li = lane & 31;
     const bool chroma = li >= 16;
@@ -884,22 +900,24 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
         if (k == 0 && !mb_edge_on) b = 0;
         if (__builtin_amdgcn_ballot_w64(b != 0) == 0) continue;    // wave-uniform skip
         const uint2 t = k == 0 ? te : ti;
-        filt_line(v, k, b, (int)(t.x & 255), (int)((t.x >> 8) & 255), (int)((t.x >> 16) | (t.y << 16)), chroma);
+        filt_line(v, k, b, (int)(t.x & 255), (int)((t.x >> 8) & 255), (t.x >> 16) | (t.y << 16), chroma);
     }
-    if (lane >= 32) return;
+    // write-back without divergence: samples a lane does not own go to its
+    // junk slot; lanes 32..63 store exactly what lanes 0..31 store
     if (dir == 0) {
         uint32_t *row = (uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
+        uint32_t *jk = (uint32_t *)(junk + lane * 4);
 #pragma unroll
         for (int j = 0; j < 5; j++) {
             const uint32_t w = (uint32_t)v[4 * j] | ((uint32_t)v[4 * j + 1] << 8) | ((uint32_t)v[4 * j + 2] << 16) | ((uint32_t)v[4 * j + 3] << 24);
-            if (!chroma || j < 3) row[j] = w;
+            *((!chroma || j < 3) ? row + j : jk) = w;
         }
     } else {
         uint8_t *col = D + idx + 4 - (chroma ? 2 * RY_S : 0);
+        uint8_t *jk = junk + lane * 4;
 #pragma unroll
-        for (int j = 1; j < 19; j++) {
-            if (!chroma || j == 3 || j == 4 || j == 7 || j == 8) col[j * RY_S] = (uint8_t)v[j];
-        }
+        for (int j = 1; j < 19; j++)
+            *((!chroma || j == 3 || j == 4 || j == 7 || j == 8) ? col + j * RY_S : jk) = (uint8_t)v[j];
     }
 }
 
@@ -961,9 +979,52 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     const int orow = lane >> 2, oq = lane & 3;                                   // luma 16x16
     const int li = lane & 31;
     const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;          // chroma (lanes 32..63 mirror)
-    const size_t yoff = (size_t)(r * 16 + orow) * W16 + oq * 4;
-    const size_t coff = (size_t)(r * 8 + crow) * CW + cq * 4;
-    uint8_t *cplane = ccomp ? curV : curU;
+    // global accesses: uniform (SGPR) base + 32-bit per-lane offset
+    uint8_t *const ybase = cur + (size_t)r * 16 * W16;                   // MB row r, luma
+    uint8_t *const cbase = curU + (size_t)r * 8 * CW;                    // MB row r, Cb (Cr at +CW*CH)
+    const uint32_t yoff = (uint32_t)(orow * W16 + oq * 4);
+    const uint32_t coff = (uint32_t)(ccomp * CW * CH + crow * CW + cq * 4);
+    // common-case frame stores of iteration c (not the last row or column):
+    // set A (luma, 64 lanes): own rows 0..11 x cols 0..11 (lanes 0..35), the
+    // left MB's cols 12..15 rows 0..11 (36..47, c > 0), the row above's rows
+    // 12..15 (48..63, r > 0); set B (chroma, lanes 0..31): own rows 0..5 x
+    // cols 0..3 (0..11), left MB's cols 4..7 (12..23), the row above's rows
+    // 6..7 (24..31).  Offsets are relative to (row r*16-4 | r*8-2, col -4).
+    uint32_t sa_lds, sa_glb, sb_lds, sb_glb;
+    bool sa_left, sa_top, sb_left, sb_top, sb_on;
+    {
+        const int Lry = (int)(L.ry - (uint8_t *)&L), Lru = (int)(L.ru - (uint8_t *)&L), Lrv = (int)(L.rv - (uint8_t *)&L);
+        int row, col, lo;
+        if (lane < 36) { row = lane / 3; col = (lane % 3) * 4; }
+        else if (lane < 48) { row = lane - 36; col = -4; }
+        else { row = -4 + ((lane - 48) >> 2); col = ((lane - 48) & 3) * 4; }
+        sa_lds = (uint32_t)(Lry + (row + 4) * RY_S + 4 + col);
+        sa_glb = (uint32_t)((row + 4) * W16 + col + 4);
+        sa_left = lane >= 36 && lane < 48;
+        sa_top = lane >= 48;
+        int comp;
+        const int k = lane & 31;
+        if (k < 12) { comp = k / 6; row = k % 6; col = 0; }
+        else if (k < 24) { comp = (k - 12) / 6; row = (k - 12) % 6; col = -4; }
+        else { comp = (k - 24) >> 2; row = -2 + (((k - 24) >> 1) & 1); col = ((k - 24) & 1) * 4; }
+        lo = comp ? Lrv : Lru;
+        sb_lds = (uint32_t)(lo + (row + 2) * RC_S + 4 + col);
+        sb_glb = (uint32_t)(comp * CW * CH + (row + 2) * CW + col + 4);
+        sb_left = k >= 12 && k < 24;
+        sb_top = k >= 24;
+        sb_on = lane < 32;
+    }
+    // end-of-iteration shift (cols 12..15 / 4..7 -> the next MB's left halo):
+    // lanes 0..15 luma rows, 16..31 chroma rows, 32..63 into their junk slots
+    uint32_t sh_src, sh_dst;
+    {
+        uint8_t *D;
+        int off, step;
+        if (lane < 16) { D = L.ry; off = (lane + 4) * RY_S; step = 16; }
+        else { const int k = (lane - 16) & 15; D = (k >> 3) ? L.rv : L.ru; off = ((k & 7) + 2) * RC_S; step = 8; }
+        sh_src = (uint32_t)((int)(D - (uint8_t *)&L) + off + step);
+        sh_dst = lane < 32 ? (uint32_t)((int)(D - (uint8_t *)&L) + off) : (uint32_t)((int)(L.junk - (uint8_t *)&L) + lane * 4);
+    }
     // top-entry fetch lane map: lanes 0..31 entry c dword lane; 32: entry c+1
     // dword 24; 33..35: entry c-1 dwords 27/29/31; others: dummy (entry c dword 0)
     const int tsel = lane < 32 ? 0 : lane == 32 ? 1 : lane < 36 ? 2 : 0;
@@ -978,8 +1039,8 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         if (!RING) {
             const int g0 = rec_base + r * W;
             n_db = ((const uint32_t *)(a.dbrec + (size_t)g0 * 64))[lane & 15];
-            n_y = *(const uint32_t *)(cur + yoff);
-            n_c = *(const uint32_t *)(cplane + coff);
+            n_y = *(const uint32_t *)(ybase + yoff);
+            n_c = *(const uint32_t *)(cbase + coff);
             const uint32_t *rs = (const uint32_t *)(a.res + (size_t)g0 * 384);
             n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
         }
@@ -1021,8 +1082,8 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             if (!RING) {
                 const int gn = rec_base + r * W + cn;
                 n_db = ((const uint32_t *)(a.dbrec + (size_t)gn * 64))[lane & 15];
-                n_y = *(const uint32_t *)(cur + yoff + cn * 16);
-                n_c = *(const uint32_t *)(cplane + coff + cn * 8);
+                n_y = *(const uint32_t *)(ybase + cn * 16 + yoff);
+                n_c = *(const uint32_t *)(cbase + cn * 8 + coff);
                 const uint32_t *rs = (const uint32_t *)(a.res + (size_t)gn * 384);
                 n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
             }
@@ -1131,7 +1192,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
         // ---- vertical edges (need only this row's samples)
         if (dbf) {
-            deblock_dir(0, L.db, L.ry, L.ru, L.rv, lane, avail & DB_LEFT);
+            deblock_dir(0, L.db, L.ry, L.ru, L.rv, L.junk, lane, avail & DB_LEFT);
             wave_sync();
         }
         if (prof) { tc1 = clock64(); pt[1] += tc1 - tc0; tc0 = tc1; }
@@ -1161,7 +1222,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         }
         if (prof) { tc1 = clock64(); pt[5] += tc1 - tc0; tc0 = tc1; }
         if (dbf) {
-            deblock_dir(1, L.db, L.ry, L.ru, L.rv, lane, avail & DB_TOP);
+            deblock_dir(1, L.db, L.ry, L.ru, L.rv, L.junk, lane, avail & DB_TOP);
             wave_sync();
         }
         // provisional entry c (rows 12..15 final except columns 13..15)
@@ -1180,42 +1241,45 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             drain_vm();
             if (lane == 0) st_sc1_u32(progress_me, (tag << 12) | (uint32_t)c);
         }
-        {
+        if (!last_row && c != W - 1) {
+            // common case: two store instructions (see the lane maps above)
+            const uint32_t va = *(const uint32_t *)((const uint8_t *)&L + sa_lds);
+            const uint32_t vb = *(const uint32_t *)((const uint8_t *)&L + sb_lds);
+            uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
+            uint8_t *const cb = cbase + c * 8 - 2 * CW - 4;
+            if ((!sa_left || c > 0) && (!sa_top || has_up)) st32<PIPE>(yb + sa_glb, va);
+            if (sb_on && (!sb_left || c > 0) && (!sb_top || has_up)) st32<PIPE>(cb + sb_glb, vb);
+        } else {
             const int yrows = last_row ? 16 : 12;
             const int crows = last_row ? 8 : 6;
             const bool last_col = c == W - 1;
             if (orow < yrows && (oq < 3 || last_col))
-                st32<PIPE>(cur + yoff + c * 16, *(const uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4]);
+                st32<PIPE>(ybase + c * 16 + yoff, *(const uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4]);
             if (lane < 32 && crow < crows && (cq == 0 || last_col))
-                st32<PIPE>(cplane + coff + c * 8, *(const uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
+                st32<PIPE>(cbase + c * 8 + coff, *(const uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
             if (c > 0) {    // left halo: MB (r,c-1) luma cols 12..15 / chroma cols 4..7
                 if (lane < 16) {
                     if (lane < yrows)
-                        st32<PIPE>(cur + (size_t)(r * 16 + lane) * W16 + c * 16 - 4, *(const uint32_t *)&L.ry[(lane + 4) * RY_S]);
+                        st32<PIPE>(ybase + c * 16 - 4 + lane * W16, *(const uint32_t *)&L.ry[(lane + 4) * RY_S]);
                 } else if (lane < 32) {
                     const int k = lane - 16, comp = k >> 3, row = k & 7;
                     if (row < crows)
-                        st32<PIPE>((comp ? curV : curU) + (size_t)(r * 8 + row) * CW + c * 8 - 4, *(const uint32_t *)&(comp ? L.rv : L.ru)[(row + 2) * RC_S]);
+                        st32<PIPE>(cbase + c * 8 - 4 + comp * CW * CH + row * CW, *(const uint32_t *)&(comp ? L.rv : L.ru)[(row + 2) * RC_S]);
                 }
             }
             if (has_up) {   // top halo: MB (r-1,c) luma rows 12..15, chroma rows 6..7 (now final)
                 if (lane >= 32 && lane < 48) {
                     const int k = lane - 32;
-                    st32<PIPE>(cur + (size_t)(r * 16 - 4 + (k >> 2)) * W16 + c * 16 + (k & 3) * 4, *(const uint32_t *)&L.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
+                    st32<PIPE>(ybase + c * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&L.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
                 } else if (lane >= 48 && lane < 56) {
                     const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-                    st32<PIPE>((comp ? curV : curU) + (size_t)(r * 8 - 2 + row) * CW + c * 8 + qq * 4, *(const uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4]);
+                    st32<PIPE>(cbase + c * 8 + qq * 4 + comp * CW * CH + (row - 2) * CW, *(const uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4]);
                 }
             }
         }
         wave_sync();
         // ---- shift: this MB's cols 12..15 / 4..7 become the next MB's left halo
-        if (lane < 16) *(uint32_t *)&L.ry[(lane + 4) * RY_S] = *(const uint32_t *)&L.ry[(lane + 4) * RY_S + 16];
-        else if (lane < 32) {
-            const int k = lane - 16, comp = k >> 3, row = k & 7;
-            uint8_t *D = comp ? L.rv : L.ru;
-            *(uint32_t *)&D[(row + 2) * RC_S] = *(const uint32_t *)&D[(row + 2) * RC_S + 8];
-        }
+        *(uint32_t *)((uint8_t *)&L + sh_dst) = *(const uint32_t *)((const uint8_t *)&L + sh_src);
         wave_sync();
         if (prof) { tc1 = clock64(); pt[4] += tc1 - tc0; }
     }

@@ -98,6 +98,12 @@ class Engine:
         if self._L.h264mi_engine_decode_device(self._h, npics, d_recs, d_coef, d_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device failed")
 
+    def set_groups(self, ngroups: int) -> None:
+        """Split decode_device batches into `ngroups` picture groups on separate
+        HIP streams (k_mb of one group overlaps the others' k_rows)."""
+        if self._L.h264mi_engine_set_groups(self._h, int(ngroups)) != 0:
+            raise RuntimeError("h264mi_engine_set_groups failed")
+
     def set_pipeline(self, depth: int) -> None:
         if self._L.h264mi_engine_set_pipeline(self._h, int(depth)) != 0:
             raise RuntimeError("h264mi_engine_set_pipeline failed")

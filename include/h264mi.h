@@ -161,6 +161,14 @@ int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wav
  * rows; it must exceed every MV's reference reach in MB rows by 2 (the
  * caller computes it from the records; <= 0 = whole pictures in sequence). */
 int  h264mi_engine_set_pipeline(h264mi_engine *e, int depth);
+/* stream groups: decode_device batches are split into `ngroups` groups of
+ * pictures, each reconstructed on its own HIP stream (k_mb then k_rows), so
+ * one group's motion compensation overlaps the other groups' row kernels.
+ * The groups are offset once (a short delay kernel) so that, with equal
+ * per-picture cost, their k_mb phases stay apart.  The caller keeps
+ * d_recs / d_coef / d_pics unchanged until h264mi_engine_sync.  1 = off. */
+#define H264MI_MAX_GROUPS 8
+int  h264mi_engine_set_groups(h264mi_engine *e, int ngroups);
 int  h264mi_engine_decode_pipelined(h264mi_engine *e, int nstreams, int depth, const void *d_recs,
                                     const int16_t *d_coef, const void *d_pics, int base_pic, int lag_rows);
 /* diagnostics: per k_rows workgroup (row r of batch picture p at index
