@@ -31,6 +31,7 @@ struct h264mi_engine {
     int pipe_cap;                 // pictures per launch the per-picture buffers hold
     uint32_t *d_progress;         // k_wg<PIPE>: per picture row drained-store progress
     uint32_t *d_order, *h_order;  // k_wg: (picture, row) dispatch order
+    unsigned long long *d_gjunk;  // 64 KiB store sink (ReconArgs::gjunk)
     int classic;                  // single-picture launches: k_mb + k_rows (default) or k_wg (H264MI_KERNEL=wg)
     // stream groups (h264mi_engine_set_groups): the pictures of a device-input
     // batch split into G groups, each on its own HIP stream, so one group's
@@ -122,6 +123,7 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
               hipMalloc(&e->d_rec, sizeof(MbRec) * nstreams * e->nmbs) == hipSuccess &&
               hipMalloc(&e->d_coef, e->coef_cap * 32) == hipSuccess &&
               hipMalloc(&e->d_pics, sizeof(PicDesc) * nstreams) == hipSuccess &&
+              hipMalloc(&e->d_gjunk, 65536) == hipSuccess &&
 
               hipHostMalloc(&e->h_rec, sizeof(MbRec) * nstreams * e->nmbs, hipHostMallocDefault) == hipSuccess &&
               hipHostMalloc(&e->h_coef, e->h_coef_cap * 32, hipHostMallocDefault) == hipSuccess &&
@@ -150,7 +152,7 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->st) (void)hipStreamSynchronize(e->st);
     free_pic_buffers(e);
     (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
-    (void)hipFree(e->d_pics);
+    (void)hipFree(e->d_pics); (void)hipFree(e->d_gjunk);
     (void)hipHostFree(e->h_rec); (void)hipHostFree(e->h_coef); (void)hipHostFree(e->h_pics);
     if (e->ev_staged) (void)hipEventDestroy(e->ev_staged);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
@@ -200,6 +202,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.rec = d_rec;
     a.coef = d_coef;
     a.mbx = e->d_mbx;
+    a.gjunk = e->d_gjunk;
     if (++e->epoch >= (1u << 20)) {           // tags: granules epoch, progress (epoch << 12) | count
         if (h264mi_engine_sync(e)) return -1; // group streams may still read the mailboxes
         HIPCHECK(hipMemsetAsync(e->d_mbx, 0, (size_t)e->pipe_cap * e->nmbs * 256, e->st));
@@ -237,15 +240,17 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
         HIPCHECK(hipGetLastError());
         if (rec) (void)hipEventRecord(t1, e->st);
-        hipLaunchKernelGGL(k_rows, dim3(npics * e->h), dim3(64), 0, e->st, a);
+        if (a.prof) hipLaunchKernelGGL(k_rows<true>, dim3(npics * e->h), dim3(64), 0, e->st, a);
+        else hipLaunchKernelGGL(k_rows<false>, dim3(npics * e->h), dim3(64), 0, e->st, a);
         HIPCHECK(hipGetLastError());
     } else {
         // one launch: row workgroups with in-workgroup MC (k_wg); the k_mb
         // slot of the timing is empty
         if (rec) (void)hipEventRecord(t1, e->st);
         const dim3 grid(a.S * e->h * depth), blk(64 * (1 + WG_NMC));
-        if (pipe) hipLaunchKernelGGL((k_wg<true, WG_NMC>), grid, blk, 0, e->st, a);
-        else hipLaunchKernelGGL((k_wg<false, WG_NMC>), grid, blk, 0, e->st, a);
+        if (pipe) hipLaunchKernelGGL((k_wg<true, WG_NMC, false>), grid, blk, 0, e->st, a);
+        else if (a.prof) hipLaunchKernelGGL((k_wg<false, WG_NMC, true>), grid, blk, 0, e->st, a);
+        else hipLaunchKernelGGL((k_wg<false, WG_NMC, false>), grid, blk, 0, e->st, a);
         HIPCHECK(hipGetLastError());
     }
     if (rec) (void)hipEventRecord(t2, e->st);
@@ -282,7 +287,7 @@ static int launch_groups(h264mi_engine *e, int npics, ReconArgs a)
         hipLaunchKernelGGL(k_mb, dim3(((n * e->nmbs + 7) / 8) * 8), dim3(64), 0, gs, ag);
         HIPCHECK(hipGetLastError());
         if (rec) (void)hipEventRecord(t1, gs);
-        hipLaunchKernelGGL(k_rows, dim3(n * e->h), dim3(64), 0, gs, ag);
+        hipLaunchKernelGGL(k_rows<false>, dim3(n * e->h), dim3(64), 0, gs, ag);
         HIPCHECK(hipGetLastError());
         if (rec) { (void)hipEventRecord(t2, gs); e->tev_n++; }
         HIPCHECK(hipMemcpyAsync(e->h_err + p0, ag.err, sizeof(unsigned) * n, hipMemcpyDeviceToHost, gs));

@@ -48,6 +48,7 @@ struct ReconArgs {
     int S;                    // streams per pipeline stage
     int ring, base_pic;
     const uint32_t *order;    // k_wg: dispatch order of the P*H (picture, row) pairs, (k << 16) | r
+    unsigned long long *gjunk; // 64 KiB sink: 128 x 64 granules for lanes with nothing to store
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -951,7 +952,7 @@ __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v,
 // outputs come from the workgroup's MC waves through the LDS ring (k_wg);
 // otherwise from k_mb's HBM outputs (k_rows).  PIPE (RING only): frame
 // stores are sc1 and per-row progress is published for later pictures' MC.
-template <bool PIPE, bool RING>
+template <bool PIPE, bool RING, bool PROF>
 __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, MbRing *R)
 {
     static_assert(RING || !PIPE, "pipelined row units take MC outputs from the LDS ring");
@@ -1031,6 +1032,11 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     const int tdw = lane < 32 ? lane : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 0;
 
     uint32_t *progress_me = PIPE ? a.progress + (size_t)p * H + r : nullptr;
+    // global stores are unconditional: lanes with nothing to store write this
+    // row's sink granule instead.  Stores skipped by an exec-mask branch leave
+    // the waitcnt pass unable to count them, and it then waits for every
+    // store of the iteration (vmcnt(0)) before the next MB's prefetched data
+    unsigned long long *const sink = a.gjunk + ((p * H + r) & 127) * 64 + lane;
 
     // prefetch registers for MB (r, 0)
     uint32_t n_db = 0, n_y = 0, n_c = 0, n_r0 = 0, n_r1 = 0, n_r2 = 0;
@@ -1051,7 +1057,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
     }
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bool prof = a.prof != nullptr;
+    const bool prof = PROF && a.prof != nullptr;     // PROF = false: no clock code at all
     const unsigned long long tstart = prof ? wall_clock64() : 0;
     uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
 
@@ -1075,7 +1081,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         const int ce = tsel == 0 ? c : tsel == 1 ? min(c + 1, W - 1) : max(c - 1, 0);
         const unsigned long long *tga = mbx_up + (size_t)ce * 32 + tdw;
         unsigned long long gr = 0;
-        if (has_up) gr = ld_gran(tga);
+        gr = ld_gran(tga);          // r == 0: own row's mailbox, value unused
         // ---- prefetch MB (r, c+1) (clamped: the last iteration re-reads MB W-1)
         {
             const int cn = min(c + 1, W - 1);
@@ -1185,10 +1191,10 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             const uint8_t *rcp = li < 16 ? &L.ry[(li + 4) * RY_S + 19] : li < 24 ? &L.ru[(li - 16 + 2) * RC_S + 11] : &L.rv[(li - 24 + 2) * RC_S + 11];
             const uint8_t rc = *rcp;
             wave_sync();
-            if (lane < 32) L.left_unf[lane] = rc;
+            *(lane < 32 ? &L.left_unf[lane] : &L.junk[lane]) = rc;
         }
         // publish this MB's unfiltered bottom row (the row below's intra neighbours)
-        if (has_down && lane >= 24 && lane < 32) st_gran(mbx_me + (size_t)c * 32 + lane, unf, tag);
+        st_gran(has_down && lane >= 24 && lane < 32 ? mbx_me + (size_t)c * 32 + lane : sink, unf, tag);
         if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
         // ---- vertical edges (need only this row's samples)
         if (dbf) {
@@ -1199,13 +1205,13 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
 
         // ---- hand-off: the final rows of MB c-1 (entry dwords 0..23) are
         //      final now -- only this MB's vertical edges touch its columns 13..15
-        if (has_down) {
+        {
             const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
             const uint32_t patch = li < 16 ? *(const uint32_t *)&L.ry[(16 + (li >> 2)) * RY_S]
                                            : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
             const bool is_patch = li < 16 ? (li & 3) == 3 : (li < 24 && qq);
             const uint32_t ent = is_patch ? patch : prov;
-            if (c > 0 && lane < 24) st_gran(mbx_me + (size_t)(c - 1) * 32 + lane, ent, tag);
+            st_gran(has_down && c > 0 && lane < 24 ? mbx_me + (size_t)(c - 1) * 32 + lane : sink, ent, tag);
             if (prof && lane == 0) pmb[2] = wall_clock64();
         }
         if (prof) { tc1 = clock64(); pt[3] += tc1 - tc0; tc0 = tc1; }
@@ -1239,7 +1245,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             // the stores of iterations < c have had a whole iteration to land:
             // drain them and tell the next picture's MC (progress = c)
             drain_vm();
-            if (lane == 0) st_sc1_u32(progress_me, (tag << 12) | (uint32_t)c);
+            st_sc1_u32(lane == 0 ? progress_me : (uint32_t *)sink, (tag << 12) | (uint32_t)c);
         }
         if (!last_row && c != W - 1) {
             // common case: two store instructions (see the lane maps above)
@@ -1247,8 +1253,10 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             const uint32_t vb = *(const uint32_t *)((const uint8_t *)&L + sb_lds);
             uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
             uint8_t *const cb = cbase + c * 8 - 2 * CW - 4;
-            if ((!sa_left || c > 0) && (!sa_top || has_up)) st32<PIPE>(yb + sa_glb, va);
-            if (sb_on && (!sb_left || c > 0) && (!sb_top || has_up)) st32<PIPE>(cb + sb_glb, vb);
+            const bool oka = (!sa_left || c > 0) && (!sa_top || has_up);
+            const bool okb = sb_on && (!sb_left || c > 0) && (!sb_top || has_up);
+            st32<PIPE>(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
+            st32<PIPE>(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
         } else {
             const int yrows = last_row ? 16 : 12;
             const int crows = last_row ? 8 : 6;
@@ -1298,12 +1306,13 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     }
 }
 
+template <bool PROF>
 __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
 {
     __shared__ RowLds L;
     const int p = blockIdx.x % a.npics, r = blockIdx.x / a.npics;
     if (r >= a.h) return;
-    row_unit<false, false>(a, p, r, L, threadIdx.x, nullptr);
+    row_unit<false, false, PROF>(a, p, r, L, threadIdx.x, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1320,7 +1329,7 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
 // blockIdx = pair * S + s, so with round-robin placement stream s stays on
 // XCD s % 8 (speed only).
 // ---------------------------------------------------------------------------
-template <bool PIPE, int NMC>
+template <bool PIPE, int NMC, bool PROF>
 __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
 {
     __shared__ RowLds L;
@@ -1339,7 +1348,7 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
         // the row unit is the dependency chain: it wins issue over the MC
         // waves sharing its SIMD
         __builtin_amdgcn_s_setprio(3);
-        row_unit<PIPE, true>(a, p, r, L, lane, &R);
+        row_unit<PIPE, true, PROF>(a, p, r, L, lane, &R);
         return;
     }
     McScratch &Mw = M[wid - 1];
@@ -1353,15 +1362,18 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
             }
             wave_sync();
         }
-        const unsigned long long t0 = a.prof ? clock64() : 0;
+        const unsigned long long t0 = PROF ? clock64() : 0;
         mc_core<PIPE>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot]);
         wave_sync();
-        if (a.prof && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
+        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
     }
 }
 #ifndef WG_NMC
 #define WG_NMC 3
 #endif
-template __global__ void k_wg<false, WG_NMC>(ReconArgs);
-template __global__ void k_wg<true, WG_NMC>(ReconArgs);
+template __global__ void k_wg<false, WG_NMC, false>(ReconArgs);
+template __global__ void k_wg<false, WG_NMC, true>(ReconArgs);
+template __global__ void k_wg<true, WG_NMC, false>(ReconArgs);
+template __global__ void k_rows<false>(ReconArgs);
+template __global__ void k_rows<true>(ReconArgs);
