@@ -809,18 +809,24 @@ __device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn
 // saves)
 #define MATERIALIZE(x) asm volatile("" : "+v"(x))
 
-__device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int alpha, int beta, uint32_t tc0s,
-                                          bool chroma)
+// One edge of one line (8.7.2.3 / 8.7.2.4).  Per-lane constants: alpha,
+// beta; beta_ap = beta for luma, 0 for chroma (so a_p / a_q are false and
+// the p1 / q1 updates off); tcs = tc0 by bS in bytes 1..3 (+1 for chroma,
+// where tc = tc0 + 1), byte 0 = 0.  MBEDGE: the MB edge, the only one that
+// can carry bS = 4.
+template <bool MBEDGE>
+__device__ __forceinline__ void filt_line(int (&v)[20], const int k, const int bS, const int alpha, const int beta,
+                                          const int beta_ap, const uint32_t tcs)
 {
     const int o = 4 * k;
     const int p2 = v[o + 1], p1 = v[o + 2], p0 = v[o + 3];
     const int q0 = v[o + 4], q1 = v[o + 5], q2 = v[o + 6];
     const int d0 = absd(p0, q0);
-    const bool f = bS != 0 && d0 < alpha && absd(p1, p0) < beta && absd(q1, q0) < beta;
-    const bool ap = !chroma && absd(p2, p0) < beta, aq = !chroma && absd(q2, q0) < beta;
-    // bS < 4 (8.7.2.3)
-    const int tc0 = (int)__builtin_amdgcn_ubfe(tc0s, (uint32_t)((bS - 1) & 3) * 8, 8);
-    const int tc = tc0 + (chroma ? 1 : (int)ap + (int)aq);
+    const bool f = bS != 0 && d0 < alpha && max(absd(p1, p0), absd(q1, q0)) < beta;
+    const bool ap = absd(p2, p0) < beta_ap, aq = absd(q2, q0) < beta_ap;
+    // bS < 4
+    const int tc0 = (int)__builtin_amdgcn_ubfe(tcs, (uint32_t)bS << 3, 8);    // bS = 4: offset 32 -> byte 0 (unused)
+    const int tc = tc0 + (int)ap + (int)aq;
     const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
     const int avg = (p0 + q0 + 1) >> 1;
     int n_p1 = p1 + clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1);
@@ -832,24 +838,26 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, int bS, int
     int r_q1 = f && aq ? n_q1 : q1;
     int r_p0 = f ? n_p0 : p0;
     int r_q0 = f ? n_q0 : q0;
-    // bS == 4 (8.7.2.4): MB edges of intra MBs only -- skipped unless some lane needs it
-    const bool b4 = f && bS >= 4;
-    if (__builtin_amdgcn_ballot_w64(b4) != 0) {
-        const int p3 = v[o], q3 = v[o + 7];
-        const bool strong = d0 < ((alpha >> 2) + 2);
-        const bool sp = ap && strong, sq = aq && strong;
-        int s_p0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, w_p0 = (2 * p1 + p0 + q1 + 2) >> 2;
-        int s_q0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, w_q0 = (2 * q1 + q0 + p1 + 2) >> 2;
-        int s_p1 = (p2 + p1 + p0 + q0 + 2) >> 2, s_q1 = (p0 + q0 + q1 + q2 + 2) >> 2;
-        int s_p2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, s_q2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
-        MATERIALIZE(s_p0); MATERIALIZE(w_p0); MATERIALIZE(s_q0); MATERIALIZE(w_q0);
-        MATERIALIZE(s_p1); MATERIALIZE(s_q1); MATERIALIZE(s_p2); MATERIALIZE(s_q2);
-        r_p0 = b4 ? (sp ? s_p0 : w_p0) : r_p0;
-        r_q0 = b4 ? (sq ? s_q0 : w_q0) : r_q0;
-        r_p1 = b4 ? (sp ? s_p1 : p1) : r_p1;
-        r_q1 = b4 ? (sq ? s_q1 : q1) : r_q1;
-        r_p2 = b4 && sp ? s_p2 : r_p2;
-        r_q2 = b4 && sq ? s_q2 : r_q2;
+    if (MBEDGE) {
+        // bS == 4: MB edges next to intra MBs only -- skipped unless some lane needs it
+        const bool b4 = f && bS >= 4;
+        if (__builtin_amdgcn_ballot_w64(b4) != 0) {
+            const int p3 = v[o], q3 = v[o + 7];
+            const bool strong = d0 < ((alpha >> 2) + 2);
+            const bool sp = ap && strong, sq = aq && strong;
+            int s_p0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, w_p0 = (2 * p1 + p0 + q1 + 2) >> 2;
+            int s_q0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, w_q0 = (2 * q1 + q0 + p1 + 2) >> 2;
+            int s_p1 = (p2 + p1 + p0 + q0 + 2) >> 2, s_q1 = (p0 + q0 + q1 + q2 + 2) >> 2;
+            int s_p2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, s_q2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+            MATERIALIZE(s_p0); MATERIALIZE(w_p0); MATERIALIZE(s_q0); MATERIALIZE(w_q0);
+            MATERIALIZE(s_p1); MATERIALIZE(s_q1); MATERIALIZE(s_p2); MATERIALIZE(s_q2);
+            r_p0 = b4 ? (sp ? s_p0 : w_p0) : r_p0;
+            r_q0 = b4 ? (sq ? s_q0 : w_q0) : r_q0;
+            r_p1 = b4 ? (sp ? s_p1 : p1) : r_p1;
+            r_q1 = b4 ? (sq ? s_q1 : q1) : r_q1;
+            r_p2 = b4 && sp ? s_p2 : r_p2;
+            r_q2 = b4 && sq ? s_q2 : r_q2;
+        }
     }
     v[o + 1] = r_p2; v[o + 2] = r_p1; v[o + 3] = r_p0;
     v[o + 4] = r_q0; v[o + 5] = r_q1; v[o + 6] = r_q2;
@@ -870,11 +878,18 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
     const int idx = chroma ? (li & 7) : (li & 15);
     const int seg = chroma ? idx >> 1 : idx >> 2;
     uint8_t *D = chroma ? ((li & 8) ? rv : ru) : ry;
-    // this line's four bS nibbles and the two threshold sets
-    const uint32_t bsw = *(const uint16_t *)(db + dir * 8 + seg * 2);
+    // this line's four bS nibbles (chroma: its edges 0, 1 sit on luma edges
+    // 0, 2) and the two threshold sets {alpha, beta, tc0(bS 1..3), indexA}
+    uint32_t bsw = *(const uint16_t *)(db + dir * 8 + seg * 2);
+    if (chroma) bsw = (bsw & 15) | ((bsw >> 4) & 0xF0);
+    if (!mb_edge_on) bsw &= ~15u;
     const uint8_t *pe = db + 16 + ((chroma ? 3 : 0) + 1 + dir) * 8;    // MB edge class
     const uint8_t *pi = db + 16 + (chroma ? 3 : 0) * 8;                  // internal class
     const uint2 te = *(const uint2 *)pe, ti = *(const uint2 *)pi;
+    const uint32_t cplus = chroma ? 0x01010100u : 0u;
+    const int alpha_e = te.x & 255, beta_e = (te.x >> 8) & 255, alpha_i = ti.x & 255, beta_i = (ti.x >> 8) & 255;
+    const uint32_t tcs_e = (((te.x >> 8) & 0xFFFF00u) | (te.y << 24)) + cplus;
+    const uint32_t tcs_i = (((ti.x >> 8) & 0xFFFF00u) | (ti.y << 24)) + cplus;
     // one stride for both planes (RC_S == RY_S): every access below is
     // base + immediate.  Chroma lines read past their 12/10 samples into
     // neighbouring LDS (values unused) and write back only what they own.
@@ -893,15 +908,16 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
 #pragma unroll
         for (int j = 0; j < 20; j++) v[j] = col[j * RY_S];
     }
+    {
+        const int b = (int)(bsw & 15);
+        if (__builtin_amdgcn_ballot_w64(b != 0) != 0)     // wave-uniform skip
+            filt_line<true>(v, 0, b, alpha_e, beta_e, chroma ? 0 : beta_e, tcs_e);
+    }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        // chroma edge k sits on luma edge 2k; chroma has no edges 2, 3
-        int b = (int)(bsw >> ((chroma ? 2 * k : k) * 4)) & 15;
-        if (chroma && k >= 2) b = 0;
-        if (k == 0 && !mb_edge_on) b = 0;
-        if (__builtin_amdgcn_ballot_w64(b != 0) == 0) continue;    // wave-uniform skip
-        const uint2 t = k == 0 ? te : ti;
-        filt_line(v, k, b, (int)(t.x & 255), (int)((t.x >> 8) & 255), (t.x >> 16) | (t.y << 16), chroma);
+    for (int k = 1; k < 4; k++) {
+        const int b = (int)((bsw >> (4 * k)) & 15);
+        if (__builtin_amdgcn_ballot_w64(b != 0) == 0) continue;
+        filt_line<false>(v, k, b, alpha_i, beta_i, chroma ? 0 : beta_i, tcs_i);
     }
     // write-back without divergence: samples a lane does not own go to its
     // junk slot; lanes 32..63 store exactly what lanes 0..31 store
