@@ -98,6 +98,21 @@ template <bool SC1> __device__ __forceinline__ void st32(void *p, uint32_t v)
     if (SC1) st_sc1_u32((uint32_t *)p, v);
     else *(uint32_t *)p = v;
 }
+// pin a uniform pointer to SGPRs, so that base[32-bit lane offset] becomes a
+// saddr access (no per-lane 64-bit address arithmetic)
+// (global address space kept explicit: a generic pointer would turn the
+// access into a FLAT one, counted by lgkmcnt as well)
+typedef const __attribute__((address_space(1))) uint8_t *gcu8p;
+__device__ __forceinline__ gcu8p uni(const void *p)
+{
+    gcu8p g = (gcu8p)p;
+    asm volatile("" : "+s"(g));
+    return g;
+}
+__device__ __forceinline__ uint32_t ldg32(gcu8p base, uint32_t off)
+{
+    return *(const __attribute__((address_space(1))) uint32_t *)(base + off);
+}
 __device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 __device__ __forceinline__ int clip255(int v) { return min(max(v, 0), 255); }
@@ -649,8 +664,66 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
 #define I4SCHED0 0xFEDC765410ull
 #define I4SCHED1 0xFFBA9832FFull
 
+// Intra 4x4 prediction as a table (8.3.1.2.1-9): every mode and position is
+// v = (A + wB*B + wC*C + rnd) >> sh over the block's 13 neighbours Sx[0..12]
+// (Sx[3-k] = p[-1,k], Sx[4] = p[-1,-1], Sx[5+k] = p[k,-1]), or DC.  Entry:
+// byte offsets of A, B, C in the gathered neighbour array (Sx[i] at i, or
+// i + 3 for i >= 5, so left and top are aligned dwords), wB, wC, sh, DC flag.
+__device__ uint32_t i4_entry(int mode, int x, int y)
+{
+    int a = 0, b = 0, c = 0, wb = 0, wc = 0, sh = 0;
+    bool dc = false;
+    auto copy = [&](int i) { a = b = c = i; wb = 0; wc = 0; sh = 0; };
+    auto k11 = [&](int i, int j) { a = i; b = j; c = i; wb = 1; wc = 0; sh = 1; };
+    auto k121 = [&](int i, int j, int k) { a = i; b = j; c = k; wb = 2; wc = 1; sh = 2; };
+    auto k13 = [&](int i, int j) { a = i; b = j; c = i; wb = 3; wc = 0; sh = 2; };
+    switch (mode) {
+    case 0: copy(5 + x); break;                                   // vertical
+    case 1: copy(3 - y); break;                                   // horizontal
+    case 2: dc = true; copy(0); break;                            // DC
+    case 3:                                                       // diagonal down left
+        if (x == 3 && y == 3) k13(11, 12);
+        else k121(5 + x + y, 6 + x + y, 7 + x + y);
+        break;
+    case 4: { const int d = x - y; k121(3 + d, 4 + d, 5 + d); break; }    // diagonal down right
+    case 5: {                                                     // vertical right
+        const int z = 2 * x - y, i = x - (y >> 1);
+        if (z >= 0 && !(z & 1)) k11(4 + i, 5 + i);
+        else if (z > 0) k121(3 + i, 4 + i, 5 + i);
+        else if (z == -1) k121(3, 4, 5);
+        else k121(4 - y, 5 - y, 6 - y);
+        break;
+    }
+    case 6: {                                                     // horizontal down
+        const int z = 2 * y - x, i = y - (x >> 1);
+        if (z >= 0 && !(z & 1)) k11(4 - i, 3 - i);
+        else if (z > 0) k121(5 - i, 4 - i, 3 - i);
+        else if (z == -1) k121(3, 4, 5);
+        else k121(4 + x, 3 + x, 2 + x);
+        break;
+    }
+    case 7: {                                                     // vertical left
+        const int i = x + (y >> 1);
+        if (!(y & 1)) k11(5 + i, 6 + i);
+        else k121(5 + i, 6 + i, 7 + i);
+        break;
+    }
+    default: {                                                    // horizontal up
+        const int z = x + 2 * y, i = y + (x >> 1);
+        if (z > 5) copy(0);
+        else if (z == 5) k13(1, 0);
+        else if (!(z & 1)) k11(3 - i, 2 - i);
+        else k121(3 - i, 2 - i, 1 - i);
+        break;
+    }
+    }
+    auto off = [](int i) { return i <= 4 ? i : i + 3; };
+    return (uint32_t)(off(a) | off(b) << 4 | off(c) << 8 | wb << 12 | wc << 14 | sh << 16) | (dc ? 1u << 20 : 0u);
+}
+
 __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
-                           uint8_t *ty, uint8_t *tu, uint8_t *tv, int lane)
+                           uint8_t *ty, uint8_t *tu, uint8_t *tv, const uint32_t *i4tab, uint8_t *sx, uint8_t *junk,
+                           int lane)
 {
     const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C;
     if (mbtype == MBT_I16) {
@@ -688,29 +761,50 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
 #pragma unroll
         for (int i = 0; i < 4; i++) ty[(y + 1) * TY_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
     } else {
+        // 10-step sub-wavefront, two blocks per step (I4SCHED0/1): lanes
+        // 0..15 = slot 0, 16..31 = slot 1 (lanes 32..63 mirror, writing to
+        // their junk slots).  Per step: gather each block's 13 neighbours into
+        // sx[slot], then one table-driven formula per sample.
+        const int slot = (lane >> 4) & 1, pos = lane & 15;
+        const int px = pos & 3, py = pos >> 2;
+        const bool lo = lane < 32;
 #pragma unroll 1
         for (int step = 0; step < 10; step++) {
-            const int slot = lane >> 4;
-            int v = 0;
-            int b = -1;
-            if (slot == 0) b = (int)(I4SCHED0 >> (step * 4)) & 15;
-            else if (slot == 1) { b = (int)(I4SCHED1 >> (step * 4)) & 15; if (b == 15) b = -1; }
-            const int px = lane & 3, py = (lane >> 2) & 3;
-            if (b >= 0) {
-                const int bx = blk_x(b), by = blk_y(b);
-                const bool avL = bx > 0 || aA;
-                const bool avT = by > 0 || aB;
-                bool avTR;
-                if (b == 3 || b == 7 || b == 11 || b == 13 || b == 15) avTR = false;
-                else if (by == 0) avTR = bx == 3 ? aC : aB;
-                else avTR = true;
-                const int mode = (int)(i4 >> (b * 4)) & 15;
-                const uint8_t *T = ty + (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;
-                const int pr = i4_pred(T, TY_STRIDE, mode, px, py, avT, avL, avTR);
-                v = clip255(pr + (has_res ? res[(by * 4 + py) * 16 + bx * 4 + px] : 0));
+            const int s0 = (int)(I4SCHED0 >> (step * 4)) & 15, s1 = (int)(I4SCHED1 >> (step * 4)) & 15;
+            const bool valid = slot == 0 || s1 != 15;
+            const int b = slot ? (s1 & 15) : s0;
+            const int bx = blk_x(b), by = blk_y(b);
+            const int t0 = (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;           // tile offset of the block's (0,0)
+            // top-right availability: blocks 3, 7, 11, 13, 15 never; the top
+            // block row from the MB above (or above-right for block 5)
+            const bool avTR = (b == 3 || b == 7 || b == 11 || b == 13 || b == 15) ? false
+                              : by == 0 ? (bx == 3 ? (bool)(avail & AV_C) : (bool)(avail & AV_B)) : true;
+            {   // gather: lane pos = neighbour index i
+                const int i = pos;
+                int src;
+                if (i <= 3) src = t0 + (3 - i) * TY_STRIDE - 1;
+                else if (i == 4) src = t0 - TY_STRIDE - 1;
+                else src = t0 - TY_STRIDE + min(i - 5, avTR ? 7 : 3);
+                const int dst = i <= 4 ? i : i + 3;
+                const uint8_t v = ty[min(src, 17 * TY_STRIDE - 1)];
+                *(lo && valid && i < 13 ? &sx[slot * 16 + dst] : &junk[lane]) = v;
             }
             wave_sync();
-            if (b >= 0) ty[(blk_y(b) * 4 + py + 1) * TY_STRIDE + blk_x(b) * 4 + px + 1] = (uint8_t)v;
+            const int mode = (int)(i4 >> (b * 4)) & 15;
+            const uint32_t e = i4tab[(mode < 9 ? mode : 0) * 16 + pos];
+            const uint8_t *S = sx + slot * 16;
+            const int A = S[e & 15], B = S[(e >> 4) & 15], C = S[(e >> 8) & 15];
+            const int sh = (int)((e >> 16) & 3);
+            int v = (A + (int)((e >> 12) & 3) * B + (int)((e >> 14) & 1) * C + ((1 << sh) >> 1)) >> sh;
+            if (__builtin_amdgcn_ballot_w64((e >> 20) & 1) != 0) {
+                const uint32_t lw = *(const uint32_t *)S, tw = *(const uint32_t *)(S + 8);
+                const int sl = (int)__builtin_amdgcn_sad_u8(lw, 0u, 0u), st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
+                const bool avT = by > 0 || (avail & AV_B), avL = bx > 0 || (avail & AV_A);
+                const int dcv = avT && avL ? (st + sl + 4) >> 3 : avL ? (sl + 2) >> 2 : avT ? (st + 2) >> 2 : 128;
+                v = (e >> 20) & 1 ? dcv : v;
+            }
+            if (has_res) v = clip255(v + res[(by * 4 + py) * 16 + bx * 4 + px]);
+            *(lo && valid ? &ty[t0 + py * TY_STRIDE + px] : &junk[lane]) = (uint8_t)v;
             wave_sync();
         }
     }
@@ -794,6 +888,8 @@ struct __attribute__((aligned(16))) RowLds {
     uint8_t tv[9 * TC_STRIDE];
     uint8_t left_unf[32];       // unfiltered right column of the previous MB: Y16 U8 V8
     uint8_t junk[256];          // per-lane sink of unconditional LDS stores (lanes with nothing to store)
+    uint32_t i4tab[9 * 16];     // intra 4x4 prediction table (i4_entry), mode x position
+    uint8_t sx[32];             // gathered neighbours of the two blocks of an intra 4x4 step
 };
 
 
@@ -1044,8 +1140,15 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     }
     // top-entry fetch lane map: lanes 0..31 entry c dword lane; 32: entry c+1
     // dword 24; 33..35: entry c-1 dwords 27/29/31; others: dummy (entry c dword 0)
-    const int tsel = lane < 32 ? 0 : lane == 32 ? 1 : lane < 36 ? 2 : 0;
+    const int tdsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;   // entry c + tdsel (clamped)
     const int tdw = lane < 32 ? lane : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 0;
+    // LDS slots of MB c's own samples: luma all lanes, chroma lanes 0..31
+    // (32..63 into their junk slots); deblocking record lanes 0..15
+    const uint32_t own_y_lds = (uint32_t)((int)(L.ry - (uint8_t *)&L) + (orow + 4) * RY_S + 4 + oq * 4);
+    const uint32_t own_c_lds = lane < 32 ? (uint32_t)((int)((ccomp ? L.rv : L.ru) - (uint8_t *)&L) + (crow + 2) * RC_S + 4 + cq * 4)
+                                         : (uint32_t)((int)(L.junk - (uint8_t *)&L) + lane * 4);
+    const uint32_t db_lds = lane < 16 ? (uint32_t)((int)(L.db - (uint8_t *)&L) + lane * 4)
+                                      : (uint32_t)((int)(L.junk - (uint8_t *)&L) + lane * 4);
 
     uint32_t *progress_me = PIPE ? a.progress + (size_t)p * H + r : nullptr;
     // global stores are unconditional: lanes with nothing to store write this
@@ -1074,11 +1177,11 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     }
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool prof = PROF && a.prof != nullptr;     // PROF = false: no clock code at all
+    for (int e = lane; e < 9 * 16; e += WAVE) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
     const unsigned long long tstart = prof ? wall_clock64() : 0;
     uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
 
     for (int c = 0; c < W; c++) {
-        const uint32_t db_w = n_db, n_y0 = n_y, n_c0 = n_c, res0 = n_r0, res1 = n_r1, res2 = n_r2;
         const uint32_t h0 = __builtin_amdgcn_readfirstlane(n_h0), h1 = __builtin_amdgcn_readfirstlane(n_h1);
         const uint32_t cbits = __builtin_amdgcn_readfirstlane(n_h2), qcoef = __builtin_amdgcn_readfirstlane(n_h3);
         const uint64_t i4 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(n_h5) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(n_h4);
@@ -1088,59 +1191,64 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         unsigned long long tc0 = prof ? clock64() : 0, tc1;
         unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
         if (prof && lane == 0) pmb[0] = wall_clock64();
+        // ---- MB c's own samples / residual / deblocking record into LDS, from
+        //      the registers the previous iteration prefetched them into (before
+        //      this iteration's prefetch reuses them).  Unconditional: intra
+        //      MBs overwrite the samples, inter MBs never read the residual.
+        const int slot = c & (RING_K - 1);
+        {
+            uint32_t own_y = n_y, own_c = n_c, own_db = n_db;
+            if (RING) {
+                unsigned spins = 0;
+                const unsigned long long tw = prof ? clock64() : 0;
+                while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
+                }
+                wave_sync();
+                if (prof) pt[7] += clock64() - tw;
+                own_y = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
+                own_c = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
+                own_db = ((const uint32_t *)R->db[slot])[lane & 15];
+            }
+            uint8_t *const Lb = (uint8_t *)&L;
+            *(uint32_t *)(Lb + db_lds) = own_db;
+            *(uint32_t *)(Lb + own_y_lds) = own_y;
+            *(uint32_t *)(Lb + own_c_lds) = own_c;
+            if (!RING) {
+                ((uint32_t *)L.res)[lane] = n_r0;
+                ((uint32_t *)L.res)[64 + lane] = n_r1;
+                ((uint32_t *)L.res)[128 + lane] = n_r2;
+            }
+            if (qtype == MBT_IPCM) {
+                const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)coef_base + qcoef) * 16);
+                const uint32_t py = src[lane], pc = src[64 + li];
+                *(uint32_t *)(Lb + own_y_lds) = py;
+                *(uint32_t *)(Lb + own_c_lds) = pc;
+            }
+        }
         // speculative read of the row above's granules (issued before the
         // prefetch: vmcnt retires in order, so waiting for it must not wait
-        // for the prefetch); re-read until the needed ones
-        // carry this epoch.  Lanes 24..35 (unfiltered samples: intra
-        // neighbours) are published right after the row above reconstructs
-        // an MB; lanes 0..23 (final rows) after its next MB's vertical edges.
-        const int ce = tsel == 0 ? c : tsel == 1 ? min(c + 1, W - 1) : max(c - 1, 0);
-        const unsigned long long *tga = mbx_up + (size_t)ce * 32 + tdw;
-        unsigned long long gr = 0;
-        gr = ld_gran(tga);          // r == 0: own row's mailbox, value unused
+        // for the prefetch); re-read until the needed ones carry this epoch.
+        // Lanes 24..35 (unfiltered samples: intra neighbours) are published
+        // right after the row above reconstructs an MB; lanes 0..23 (final
+        // rows) after its next MB's vertical edges.
+        const int ce = min(max(c + tdsel, 0), W - 1);
+        const unsigned long long *tga = mbx_up + ce * 32 + tdw;
+        unsigned long long gr = ld_gran(tga);     // r == 0: own row's mailbox, value unused
         // ---- prefetch MB (r, c+1) (clamped: the last iteration re-reads MB W-1)
         {
             const int cn = min(c + 1, W - 1);
             if (!RING) {
                 const int gn = rec_base + r * W + cn;
-                n_db = ((const uint32_t *)(a.dbrec + (size_t)gn * 64))[lane & 15];
-                n_y = *(const uint32_t *)(ybase + cn * 16 + yoff);
-                n_c = *(const uint32_t *)(cbase + cn * 8 + coff);
-                const uint32_t *rs = (const uint32_t *)(a.res + (size_t)gn * 384);
-                n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
+                n_db = ldg32(uni(a.dbrec + (size_t)gn * 64), (uint32_t)(lane & 15) * 4);
+                n_y = ldg32(uni(ybase + cn * 16), yoff);
+                n_c = ldg32(uni(cbase + cn * 8), coff);
+                const gcu8p rs = uni(a.res + (size_t)gn * 384);
+                n_r0 = ldg32(rs, lane * 4); n_r1 = ldg32(rs, 256 + lane * 4); n_r2 = ldg32(rs, 512 + lane * 4);
             }
             const cu32p rw = recw + cn * 24;
             n_h0 = rw[0]; n_h1 = rw[1]; n_h2 = rw[2]; n_h3 = rw[3]; n_h4 = rw[4]; n_h5 = rw[5];
-        }
-        // ---- RING: wait for the MC waves to fill MB c's slot
-        const int slot = c & (RING_K - 1);
-        uint32_t own_y = n_y0, own_c = n_c0;
-        if (RING) {
-            unsigned spins = 0;
-            const unsigned long long tw = prof ? clock64() : 0;
-            while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
-            }
-            wave_sync();
-            if (prof) pt[7] += clock64() - tw;
-            own_y = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
-            own_c = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
-        }
-        // ---- own samples / residual / deblocking record into LDS
-        if (lane < 16) ((uint32_t *)L.db)[lane] = RING ? ((const uint32_t *)R->db[slot])[lane] : db_w;
-        if (qtype == MBT_IPCM) {
-            const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)coef_base + qcoef) * 16);
-            const uint32_t py = src[lane], pc = src[64 + li];
-            *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = py;
-            if (lane < 32) *(uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4] = pc;
-        } else if (!intra) {
-            *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = own_y;
-            if (lane < 32) *(uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4] = own_c;
-        } else if (!RING && cbits) {
-            ((uint32_t *)L.res)[lane] = res0;
-            ((uint32_t *)L.res)[64 + lane] = res1;
-            ((uint32_t *)L.res)[128 + lane] = res2;
         }
 
         // ---- row above: wait until entry c is final, then fetch it (+ the
@@ -1182,7 +1290,8 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
                 L.tv[(k + 1) * TC_STRIDE] = L.left_unf[24 + k];
             }
             wave_sync();
-            intra_tile(qtype, avail, pred, i4, RING ? R->res[slot] : L.res, cbits != 0, L.ty, L.tu, L.tv, lane);
+            intra_tile(qtype, avail, pred, i4, RING ? R->res[slot] : L.res, cbits != 0, L.ty, L.tu, L.tv, L.i4tab, L.sx,
+                       L.junk, lane);
             {   // tile samples start at column 1: byte reads (LDS dword reads must be aligned)
                 const uint8_t *sy = &L.ty[(orow + 1) * TY_STRIDE + 1 + oq * 4];
                 *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = sy[0] | (sy[1] << 8) | (sy[2] << 16) | ((uint32_t)sy[3] << 24);
