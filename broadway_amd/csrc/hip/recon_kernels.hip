@@ -768,43 +768,44 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
         const int slot = (lane >> 4) & 1, pos = lane & 15;
         const int px = pos & 3, py = pos >> 2;
         const bool lo = lane < 32;
+        // gather offsets relative to the block's (0,0): neighbour i = pos;
+        // top-right samples (i > 8) fall back to p[3,-1] when unavailable
+        const int rel = pos <= 3 ? (3 - pos) * TY_STRIDE - 1 : pos == 4 ? -TY_STRIDE - 1 : -TY_STRIDE + min(pos - 5, 7);
+        const int rel_notr = pos > 8 ? -TY_STRIDE + 3 : rel;
+        const int gdst = pos <= 4 ? pos : pos + 3;
+        // blocks whose top-right neighbour is available: 2,6,8,9,10,12,14
+        // always; 0,1,4 from the MB above; 5 from the MB above-right
+        const uint32_t trmask = 0x5744u | ((avail & AV_B) ? 0x13u : 0u) | ((avail & AV_C) ? 0x20u : 0u);
+        const bool aA4 = avail & AV_A, aB4 = avail & AV_B;
 #pragma unroll 1
         for (int step = 0; step < 10; step++) {
             const int s0 = (int)(I4SCHED0 >> (step * 4)) & 15, s1 = (int)(I4SCHED1 >> (step * 4)) & 15;
-            const bool valid = slot == 0 || s1 != 15;
-            const int b = slot ? (s1 & 15) : s0;
+            const bool valid = lo && (slot == 0 || s1 != 15);
+            const int b = slot ? s1 : s0;                               // 15 = none for slot 1 (block 15 is slot 0's)
             const int bx = blk_x(b), by = blk_y(b);
-            const int t0 = (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;           // tile offset of the block's (0,0)
-            // top-right availability: blocks 3, 7, 11, 13, 15 never; the top
-            // block row from the MB above (or above-right for block 5)
-            const bool avTR = (b == 3 || b == 7 || b == 11 || b == 13 || b == 15) ? false
-                              : by == 0 ? (bx == 3 ? (bool)(avail & AV_C) : (bool)(avail & AV_B)) : true;
-            {   // gather: lane pos = neighbour index i
-                const int i = pos;
-                int src;
-                if (i <= 3) src = t0 + (3 - i) * TY_STRIDE - 1;
-                else if (i == 4) src = t0 - TY_STRIDE - 1;
-                else src = t0 - TY_STRIDE + min(i - 5, avTR ? 7 : 3);
-                const int dst = i <= 4 ? i : i + 3;
-                const uint8_t v = ty[min(src, 17 * TY_STRIDE - 1)];
-                *(lo && valid && i < 13 ? &sx[slot * 16 + dst] : &junk[lane]) = v;
-            }
-            wave_sync();
+            const int t0 = (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;       // tile offset of the block's (0,0)
+            const bool avTR = (trmask >> b) & 1;
             const int mode = (int)(i4 >> (b * 4)) & 15;
+            // independent LDS reads first: table entry, residual, gathered neighbour
             const uint32_t e = i4tab[(mode < 9 ? mode : 0) * 16 + pos];
+            const int rv = has_res ? res[(by * 4 + py) * 16 + bx * 4 + px] : 0;
+            const uint8_t g = ty[t0 + (avTR ? rel : rel_notr)];
+            *(valid && pos < 13 ? &sx[slot * 16 + gdst] : &junk[lane]) = g;
+            wave_sync();
             const uint8_t *S = sx + slot * 16;
             const int A = S[e & 15], B = S[(e >> 4) & 15], C = S[(e >> 8) & 15];
+            const uint32_t lw = *(const uint32_t *)S, tw = *(const uint32_t *)(S + 8);
             const int sh = (int)((e >> 16) & 3);
             int v = (A + (int)((e >> 12) & 3) * B + (int)((e >> 14) & 1) * C + ((1 << sh) >> 1)) >> sh;
-            if (__builtin_amdgcn_ballot_w64((e >> 20) & 1) != 0) {
-                const uint32_t lw = *(const uint32_t *)S, tw = *(const uint32_t *)(S + 8);
-                const int sl = (int)__builtin_amdgcn_sad_u8(lw, 0u, 0u), st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
-                const bool avT = by > 0 || (avail & AV_B), avL = bx > 0 || (avail & AV_A);
-                const int dcv = avT && avL ? (st + sl + 4) >> 3 : avL ? (sl + 2) >> 2 : avT ? (st + 2) >> 2 : 128;
-                v = (e >> 20) & 1 ? dcv : v;
-            }
-            if (has_res) v = clip255(v + res[(by * 4 + py) * 16 + bx * 4 + px]);
-            *(lo && valid ? &ty[t0 + py * TY_STRIDE + px] : &junk[lane]) = (uint8_t)v;
+            // DC
+            const int sl = (int)__builtin_amdgcn_sad_u8(lw, 0u, 0u), st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
+            const bool avT = by > 0 || aB4, avL = bx > 0 || aA4;
+            const int dsum = (avT ? st : 0) + (avL ? sl : 0);
+            const int dsh = (avT && avL) ? 3 : 2;
+            const int dcv = (avT || avL) ? (dsum + (1 << (dsh - 1))) >> dsh : 128;
+            v = (e >> 20) & 1 ? dcv : v;
+            v = clip255(v + rv);
+            *(valid ? &ty[t0 + py * TY_STRIDE + px] : &junk[lane]) = (uint8_t)v;
             wave_sync();
         }
     }
