@@ -464,9 +464,8 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
     uint8_t *s_out = px;
 
     const int mbx = mb % a.w, mby = mb / a.w;
-    mb_dbrec(a, gmb, r, lane, db);
-
     if (r.type >= MBT_I4x4) {
+        mb_dbrec(a, gmb, r, lane, db);
         if (r.type != MBT_IPCM && r.cbits) {
             int e = 0;
             mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
@@ -514,7 +513,49 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         }
     }
 
+    // Reference windows with aligned dword loads (h264bsdPredictSamples
+    // reads, reconstruct.c:1819-1941; out-of-picture samples clamp like
+    // h264bsdFillBlock, :2222-2314).  Luma: block b = lane>>2 owns window rows
+    // (lane&3)+4k, 3 dwords each from the aligned column ax; chroma: lanes
+    // 0..31 = (block, plane), 3 rows x 2 dwords.  A window crossing the
+    // picture's left/right edge is rebuilt per sample (offset 0).  The loads
+    // are issued first; the deblocking record and the residual are computed
+    // while they are in flight.
     const uint8_t *frames = a.frames;
+    const int lb = lane >> 2, lsub = lane & 3;
+    const int l_x0 = mbx * 16 + blk_x(lb) * 4 + (r.mv[lb][0] >> 2) - 2;
+    const int l_y0 = mby * 16 + blk_y(lb) * 4 + (r.mv[lb][1] >> 2) - 2;
+    const int l_ax = clip3(0, W16 - 12, l_x0 & ~3);
+    const bool l_in = l_x0 >= 0 && l_x0 + 8 <= W16 - 1;
+    uint32_t lw[3][3];
+    {
+        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[lb >> 2]) * a.frame_bytes;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const int wy = lsub + 4 * k;
+            const int y = clip3(0, H16 - 1, l_y0 + min(wy, 8));
+            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + l_ax);
+            lw[k][0] = ld32<PIPE>(src); lw[k][1] = ld32<PIPE>(src + 1); lw[k][2] = ld32<PIPE>(src + 2);
+        }
+    }
+    const int cb = (lane & 31) >> 1, ccomp = lane & 1;
+    const int c_x0 = mbx * 8 + blk_x(cb) * 2 + (r.mv[cb][0] >> 3);
+    const int c_y0 = mby * 8 + blk_y(cb) * 2 + (r.mv[cb][1] >> 3);
+    const int c_ax = clip3(0, CW - 8, c_x0 & ~3);
+    const bool c_in = c_x0 >= 0 && c_x0 + 2 <= CW - 1;
+    uint32_t cw[3][2];
+    {
+        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[cb >> 2]) * a.frame_bytes +
+                             (unsigned long long)W16 * H16 + (unsigned long long)ccomp * CW * CH;
+#pragma unroll
+        for (int wy = 0; wy < 3; wy++) {
+            const int y = clip3(0, CH - 1, c_y0 + wy);
+            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + c_ax);
+            cw[wy][0] = ld32<PIPE>(src); cw[wy][1] = ld32<PIPE>(src + 1);
+        }
+    }
+
+    mb_dbrec(a, gmb, r, lane, db);
     int e = 0;
     if (r.cbits) {
         mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
@@ -522,65 +563,41 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
     }
 
-    // Reference windows with aligned dword loads (h264bsdPredictSamples
-    // reads, reconstruct.c:1819-1941; out-of-picture samples clamp like
-    // h264bsdFillBlock, :2222-2314).  Luma: block b = lane>>2 owns window rows
-    // (lane&3)+4k, 3 dwords each from the aligned column ax; chroma: lanes
-    // 0..31 = (block, plane), 3 rows x 2 dwords.  A window crossing the
-    // picture's left/right edge is rebuilt per sample (offset 0).
-    {
-        const int b = lane >> 2, sub = lane & 3;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes;
-        const int x0 = mbx * 16 + blk_x(b) * 4 + (mvx >> 2) - 2;
-        const int y0 = mby * 16 + blk_y(b) * 4 + (mvy >> 2) - 2;
-        const int ax = clip3(0, W16 - 12, x0 & ~3);
-        const bool inside = x0 >= 0 && x0 + 8 <= W16 - 1;
-        for (int wy = sub; wy < 9; wy += 4) {
-            const int y = clip3(0, H16 - 1, y0 + wy);
-            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + ax);
-            uint32_t d0 = ld32<PIPE>(src), d1 = ld32<PIPE>(src + 1), d2 = ld32<PIPE>(src + 2);
-            if (!inside) {
-                uint32_t o[3] = {0, 0, 0};
 #pragma unroll
-                for (int i = 0; i < 9; i++) {
-                    const int k = clip3(0, W16 - 1, x0 + i) - ax;
-                    const uint32_t w = k < 4 ? d0 : (k < 8 ? d1 : d2);
-                    o[i >> 2] |= ((w >> ((k & 3) * 8)) & 255u) << ((i & 3) * 8);
-                }
-                d0 = o[0]; d1 = o[1]; d2 = o[2];
+    for (int k = 0; k < 3; k++) {
+        const int wy = lsub + 4 * k;
+        if (wy >= 9) break;
+        uint32_t d0 = lw[k][0], d1 = lw[k][1], d2 = lw[k][2];
+        if (!l_in) {
+            uint32_t o[3] = {0, 0, 0};
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+                const int kk = clip3(0, W16 - 1, l_x0 + i) - l_ax;
+                const uint32_t w = kk < 4 ? d0 : (kk < 8 ? d1 : d2);
+                o[i >> 2] |= ((w >> ((kk & 3) * 8)) & 255u) << ((i & 3) * 8);
             }
-            M.wraw[b][wy][0] = d0; M.wraw[b][wy][1] = d1; M.wraw[b][wy][2] = d2;
+            d0 = o[0]; d1 = o[1]; d2 = o[2];
         }
-        if (sub == 0) M.wxo[b] = (uint8_t)(inside ? x0 - ax : 0);
+        M.wraw[lb][wy][0] = d0; M.wraw[lb][wy][1] = d1; M.wraw[lb][wy][2] = d2;
     }
+    if (lsub == 0) M.wxo[lb] = (uint8_t)(l_in ? l_x0 - l_ax : 0);
     if (lane < 32) {
-        const int b = lane >> 1, comp = lane & 1;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[b >> 2]) * a.frame_bytes +
-                             (unsigned long long)W16 * H16 + (unsigned long long)comp * CW * CH;
-        const int x0 = mbx * 8 + blk_x(b) * 2 + (mvx >> 3);
-        const int y0 = mby * 8 + blk_y(b) * 2 + (mvy >> 3);
-        const int ax = clip3(0, CW - 8, x0 & ~3);
-        const bool inside = x0 >= 0 && x0 + 2 <= CW - 1;
 #pragma unroll
         for (int wy = 0; wy < 3; wy++) {
-            const int y = clip3(0, CH - 1, y0 + wy);
-            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + ax);
-            uint32_t d0 = ld32<PIPE>(src), d1 = ld32<PIPE>(src + 1);
-            if (!inside) {
+            uint32_t d0 = cw[wy][0], d1 = cw[wy][1];
+            if (!c_in) {
                 uint32_t o = 0;
 #pragma unroll
                 for (int i = 0; i < 3; i++) {
-                    const int k = clip3(0, CW - 1, x0 + i) - ax;
-                    const uint32_t w = k < 4 ? d0 : d1;
-                    o |= ((w >> ((k & 3) * 8)) & 255u) << (i * 8);
+                    const int kk = clip3(0, CW - 1, c_x0 + i) - c_ax;
+                    const uint32_t w = kk < 4 ? d0 : d1;
+                    o |= ((w >> ((kk & 3) * 8)) & 255u) << (i * 8);
                 }
                 d0 = o;
             }
-            M.craw[comp][b][wy][0] = d0; M.craw[comp][b][wy][1] = d1;
+            M.craw[ccomp][cb][wy][0] = d0; M.craw[ccomp][cb][wy][1] = d1;
         }
-        M.cxo[comp][b] = (uint8_t)(inside ? x0 - ax : 0);
+        M.cxo[ccomp][cb] = (uint8_t)(c_in ? c_x0 - c_ax : 0);
     }
     wave_sync();
 
@@ -1438,6 +1455,8 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
     __shared__ RowLds L;
     const int p = blockIdx.x % a.npics, r = blockIdx.x / a.npics;
     if (r >= a.h) return;
+    // the row chain wins issue over concurrent k_mb waves (stream groups)
+    __builtin_amdgcn_s_setprio(3);
     row_unit<false, false, PROF>(a, p, r, L, threadIdx.x, nullptr);
 }
 
