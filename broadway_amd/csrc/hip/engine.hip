@@ -32,7 +32,8 @@ struct h264mi_engine {
     uint32_t *d_progress;         // k_wg<PIPE>: per picture row drained-store progress
     uint32_t *d_order, *h_order;  // k_wg: (picture, row) dispatch order
     unsigned long long *d_gjunk;  // 64 KiB store sink (ReconArgs::gjunk)
-    int classic;                  // single-picture launches: k_mb + k_rows (default) or k_wg (H264MI_KERNEL=wg)
+    int classic;                  // single-picture launches: k_wg (default) or k_mb + k_rows (H264MI_KERNEL=classic)
+    int wg_nmc;                   // MC waves per k_wg workgroup (H264MI_WG_NMC: 2, 3 or 4)
     // stream groups (h264mi_engine_set_groups): the pictures of a device-input
     // batch split into G groups, each on its own HIP stream, so one group's
     // k_mb overlaps the other groups' latency-bound k_rows
@@ -116,7 +117,9 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->ngroups = 1;
     {
         const char *km = getenv("H264MI_KERNEL");
-        e->classic = !(km && !strcmp(km, "wg"));
+        e->classic = km && !strcmp(km, "classic");
+        const char *nm = getenv("H264MI_WG_NMC");
+        e->wg_nmc = nm ? atoi(nm) : 3;
     }
     bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
 
@@ -247,10 +250,19 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         // one launch: row workgroups with in-workgroup MC (k_wg); the k_mb
         // slot of the timing is empty
         if (rec) (void)hipEventRecord(t1, e->st);
-        const dim3 grid(a.S * e->h * depth), blk(64 * (1 + WG_NMC));
-        if (pipe) hipLaunchKernelGGL((k_wg<true, WG_NMC, false>), grid, blk, 0, e->st, a);
-        else if (a.prof) hipLaunchKernelGGL((k_wg<false, WG_NMC, true>), grid, blk, 0, e->st, a);
-        else hipLaunchKernelGGL((k_wg<false, WG_NMC, false>), grid, blk, 0, e->st, a);
+        const dim3 grid(a.S * e->h * depth);
+        const int nmc = e->wg_nmc;
+        if (pipe) {
+            if (nmc == 2) hipLaunchKernelGGL((k_wg<true, 2, false>), grid, dim3(192), 0, e->st, a);
+            else if (nmc == 4) hipLaunchKernelGGL((k_wg<true, 4, false>), grid, dim3(320), 0, e->st, a);
+            else hipLaunchKernelGGL((k_wg<true, 3, false>), grid, dim3(256), 0, e->st, a);
+        } else if (a.prof) {
+            hipLaunchKernelGGL((k_wg<false, 3, true>), grid, dim3(256), 0, e->st, a);
+        } else {
+            if (nmc == 2) hipLaunchKernelGGL((k_wg<false, 2, false>), grid, dim3(192), 0, e->st, a);
+            else if (nmc == 4) hipLaunchKernelGGL((k_wg<false, 4, false>), grid, dim3(320), 0, e->st, a);
+            else hipLaunchKernelGGL((k_wg<false, 3, false>), grid, dim3(256), 0, e->st, a);
+        }
         HIPCHECK(hipGetLastError());
     }
     if (rec) (void)hipEventRecord(t2, e->st);

@@ -1514,11 +1514,12 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
     }
 }
-#ifndef WG_NMC
-#define WG_NMC 3
-#endif
-template __global__ void k_wg<false, WG_NMC, false>(ReconArgs);
-template __global__ void k_wg<false, WG_NMC, true>(ReconArgs);
-template __global__ void k_wg<true, WG_NMC, false>(ReconArgs);
+template __global__ void k_wg<false, 2, false>(ReconArgs);
+template __global__ void k_wg<false, 3, false>(ReconArgs);
+template __global__ void k_wg<false, 4, false>(ReconArgs);
+template __global__ void k_wg<false, 3, true>(ReconArgs);
+template __global__ void k_wg<true, 2, false>(ReconArgs);
+template __global__ void k_wg<true, 3, false>(ReconArgs);
+template __global__ void k_wg<true, 4, false>(ReconArgs);
 template __global__ void k_rows<false>(ReconArgs);
 template __global__ void k_rows<true>(ReconArgs);

@@ -62,7 +62,19 @@ def test_decoder_js_api_holds_reordered_pictures():
     assert 0 < len(got) < len(c["frames"]) and got == c["frames"][:len(got)]
 
 
-def test_engine_multistream_batch_vs_oracle_replay():
+# single-picture launch kernels: k_wg with 2/3/4 MC waves per row workgroup
+# (default 3), and the two-kernel k_mb + k_rows path
+KERNEL_MODES = [("wg", "3"), ("wg", "2"), ("wg", "4"), ("classic", "3")]
+
+
+@pytest.fixture(params=KERNEL_MODES, ids=lambda m: m[0] + m[1])
+def kernel_mode(request, monkeypatch):
+    monkeypatch.setenv("H264MI_KERNEL", request.param[0])
+    monkeypatch.setenv("H264MI_WG_NMC", request.param[1])
+    return request.param
+
+
+def test_engine_multistream_batch_vs_oracle_replay(kernel_mode):
     streams = [gen.generate(2, 40 + i, nframes=6, w_mbs=10, h_mbs=6, crop_bottom=0, slices=2, gop=4)
                for i in range(4)]
     caps = [Capture(s) for s in streams]
@@ -81,7 +93,7 @@ def test_engine_multistream_batch_vs_oracle_replay():
     assert eng.errors() == 0
 
 
-def test_engine_bench_streams_vs_reference():
+def test_engine_bench_streams_vs_reference(kernel_mode):
     """The bench workload (configs[3]: 8 concurrent 1080p streams, one picture
     of each per launch), 12 pictures, every frame vs the reference MD5s."""
     names = [f"bench_1080p_s{s}" for s in range(100, 108)]
@@ -99,6 +111,38 @@ def test_engine_bench_streams_vs_reference():
             got = hashlib.md5(eng.read(s, p.cur_slot).tobytes()).hexdigest()
             assert got == CASES[names[s]]["frames"][k], f"stream {s} picture {k}"
     assert eng.errors() == 0
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_engine_pipelined_vs_reference(depth):
+    """Frame-pipelined launches (k_wg<PIPE>: `depth` consecutive pictures of
+    each of the 8 bench streams per launch, per-row progress waits on the
+    reference samples) on 12 pictures, every frame vs the reference MD5s."""
+    import bench
+    names = [f"bench_1080p_s{s}" for s in range(100, 108)]
+    n = 12
+    _, caps = bench.prepare(3, [CASES[x]["seed"] for x in names], n)
+    L = _lib.mi()
+    S, w, h = len(caps), caps[0].w_mbs, caps[0].h_mbs
+    ring = depth + 17
+    d_recs, d_coef, d_pics, pic_rec_bytes, nslots, _ = bench.upload(L, caps, n, depth, ring)
+    try:
+        eng = Engine(w, h, S, nslots)
+        eng.set_pipeline(depth)
+        for k in range(n // depth):
+            lag = bench.row_reach(caps, k * depth, (k + 1) * depth) + 2
+            eng.decode_pipelined(S, depth, d_recs + k * depth * pic_rec_bytes, d_coef, d_pics + k * depth * S * 32,
+                                 k * depth, lag)
+        eng.sync()
+        for s in range(S):
+            for k in range(n):
+                got = hashlib.md5(eng.read(s, k % ring).tobytes()).hexdigest()
+                assert got == CASES[names[s]]["frames"][k], f"stream {s} picture {k}"
+        assert eng.errors() == 0
+        eng.close()
+    finally:
+        for p in (d_recs, d_coef, d_pics):
+            L.h264mi_device_free(p)
 
 
 def test_2160p_vs_reference():

@@ -3,7 +3,7 @@
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of the bench command
   profiles/<tag>_pmc.json           FETCH_SIZE / WRITE_SIZE per launch (separate passes)
-  profiles/traffic.json             HBM bytes per reconstruction step (k_mb + k_rows),
+  profiles/traffic.json             HBM bytes per reconstruction step (k_wg, or k_mb + k_rows),
                                     read by bench.py for roofline.traffic
 
 Units and corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE / WRITE_SIZE are
@@ -19,11 +19,17 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def kname(full):
+    """'void k_wg<false, 3, false>(ReconArgs)' -> 'k_wg'"""
+    n = full.split("(")[0].split("<")[0]
+    return n.split()[-1]
+
+
 def per_launch(path, counter):
     d = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] == counter:
-            d[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+            d[kname(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return {k: (sum(v) / len(v), len(v)) for k, v in d.items()}
 
 
@@ -36,7 +42,8 @@ def main(tag):
     write = per_launch(os.path.join(src, "pmc_write", "bench_counter_collection.csv"), "WRITE_SIZE")
     kernels = {}
     step = 0.0
-    for k in ("k_mb", "k_rows"):
+    step_kernels = ("k_wg",) if "k_wg" in fetch else ("k_mb", "k_rows")
+    for k in step_kernels:
         f_kib, n = fetch[k]
         w_kib, _ = write[k]
         hbm = (2 * f_kib + w_kib) * 1024
