@@ -1110,6 +1110,9 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     const int orow = lane >> 2, oq = lane & 3;                                   // luma 16x16
     const int li = lane & 31;
     const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;          // chroma (lanes 32..63 mirror)
+    // final-rows entry dword of this lane: 0..23; lanes with li 24..31 repeat
+    // li 16..23, so every lane of the publishing store carries real data
+    const int le = li < 24 ? li : li - 8;
     // global accesses: uniform (SGPR) base + 32-bit per-lane offset
     uint8_t *const ybase = cur + (size_t)r * 16 * W16;                   // MB row r, luma
     uint8_t *const cbase = curU + (size_t)r * 8 * CW;                    // MB row r, Cb (Cr at +CW*CH)
@@ -1122,7 +1125,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     // cols 0..3 (0..11), left MB's cols 4..7 (12..23), the row above's rows
     // 6..7 (24..31).  Offsets are relative to (row r*16-4 | r*8-2, col -4).
     uint32_t sa_lds, sa_glb, sb_lds, sb_glb;
-    bool sa_left, sa_top, sb_left, sb_top, sb_on;
+    bool sa_left, sa_top, sb_left, sb_top;
     {
         const int Lry = (int)(L.ry - (uint8_t *)&L), Lru = (int)(L.ru - (uint8_t *)&L), Lrv = (int)(L.rv - (uint8_t *)&L);
         int row, col, lo;
@@ -1143,7 +1146,6 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         sb_glb = (uint32_t)(comp * CW * CH + (row + 2) * CW + col + 4);
         sb_left = k >= 12 && k < 24;
         sb_top = k >= 24;
-        sb_on = lane < 32;
     }
     // end-of-iteration shift (cols 12..15 / 4..7 -> the next MB's left halo):
     // lanes 0..15 luma rows, 16..31 chroma rows, 32..63 into their junk slots
@@ -1279,7 +1281,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-                gr = ld_gran(tga);
+                if (mine) gr = ld_gran(tga);          // re-poll only the granules still needed
             }
             top = (uint32_t)gr;
             if (prof && lane == 0) pmb[1] = wall_clock64();
@@ -1337,7 +1339,9 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             *(lane < 32 ? &L.left_unf[lane] : &L.junk[lane]) = rc;
         }
         // publish this MB's unfiltered bottom row (the row below's intra neighbours)
-        st_gran(has_down && lane >= 24 && lane < 32 ? mbx_me + (size_t)c * 32 + lane : sink, unf, tag);
+        // (every lane: lanes with equal li & 7 hold the same dword, so the
+        // duplicates store identical data to the same granule)
+        st_gran(has_down ? mbx_me + (size_t)c * 32 + 24 + (li & 7) : sink, unf, tag);
         if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
         // ---- vertical edges (need only this row's samples)
         if (dbf) {
@@ -1349,12 +1353,12 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         // ---- hand-off: the final rows of MB c-1 (entry dwords 0..23) are
         //      final now -- only this MB's vertical edges touch its columns 13..15
         {
-            const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-            const uint32_t patch = li < 16 ? *(const uint32_t *)&L.ry[(16 + (li >> 2)) * RY_S]
+            const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
+            const uint32_t patch = le < 16 ? *(const uint32_t *)&L.ry[(16 + (le >> 2)) * RY_S]
                                            : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
-            const bool is_patch = li < 16 ? (li & 3) == 3 : (li < 24 && qq);
+            const bool is_patch = le < 16 ? (le & 3) == 3 : qq;
             const uint32_t ent = is_patch ? patch : prov;
-            st_gran(has_down && c > 0 && lane < 24 ? mbx_me + (size_t)(c - 1) * 32 + lane : sink, ent, tag);
+            st_gran(has_down && c > 0 ? mbx_me + (size_t)(c - 1) * 32 + le : sink, ent, tag);
             if (prof && lane == 0) pmb[2] = wall_clock64();
         }
         if (prof) { tc1 = clock64(); pt[3] += tc1 - tc0; tc0 = tc1; }
@@ -1376,10 +1380,10 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
         }
         // provisional entry c (rows 12..15 final except columns 13..15)
         if (has_down) {
-            const int k = li - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-            const uint32_t pl = *(const uint32_t *)&L.ry[(16 + ((li >> 2) & 3)) * RY_S + 4 + (li & 3) * 4];
+            const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
+            const uint32_t pl = *(const uint32_t *)&L.ry[(16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4];
             const uint32_t pc = *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S + 4 + qq * 4];
-            prov = li < 16 ? pl : pc;
+            prov = le < 16 ? pl : pc;
         }
         if (prof) { tc1 = clock64(); pt[2] += tc1 - tc0; tc0 = tc1; }
 
@@ -1388,7 +1392,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             // the stores of iterations < c have had a whole iteration to land:
             // drain them and tell the next picture's MC (progress = c)
             drain_vm();
-            st_sc1_u32(lane == 0 ? progress_me : (uint32_t *)sink, (tag << 12) | (uint32_t)c);
+            st_sc1_u32(progress_me, (tag << 12) | (uint32_t)c);      // every lane: same dword, same value
         }
         if (!last_row && c != W - 1) {
             // common case: two store instructions (see the lane maps above)
@@ -1397,7 +1401,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
             uint8_t *const cb = cbase + c * 8 - 2 * CW - 4;
             const bool oka = (!sa_left || c > 0) && (!sa_top || has_up);
-            const bool okb = sb_on && (!sb_left || c > 0) && (!sb_top || has_up);
+            const bool okb = (!sb_left || c > 0) && (!sb_top || has_up);     // lanes 32..63 repeat 0..31
             st32<PIPE>(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
             st32<PIPE>(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
         } else {

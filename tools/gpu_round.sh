@@ -15,3 +15,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o bench -- python3 bench.py --no-cpu-baseline --no-verify > /dev/null 2> $OUT/pmc_fetch.err || { tail -20 $OUT/pmc_fetch.err; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o bench -- python3 bench.py --no-cpu-baseline --no-verify > /dev/null 2> $OUT/pmc_write.err || { tail -20 $OUT/pmc_write.err; exit 1; }
 find $OUT -name "*.csv" | head -20
+# FETCH_SIZE calibration for this kernel's access widths (tools/ubench/fetch_calib.hip)
+if [ -x tools/ubench/fetch_calib ]; then
+  timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/calib -o calib -- tools/ubench/fetch_calib > $OUT/calib.log 2>&1 || { tail -20 $OUT/calib.log; exit 1; }
+fi
