@@ -443,9 +443,18 @@ __device__ void mb_dbrec(const ReconArgs &a, int gmb, const MbRec &q, int lane, 
 // per-wave LDS scratch of the MB reconstruction (reference windows)
 struct McScratch {
     int32_t dc[24];
-    uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
-    uint32_t craw[2][16][3][2];  // chroma windows: 8 bytes per row
-    uint8_t wxo[16], cxo[2][16];
+    union {
+        struct {                         // inter: reference windows
+            uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
+            uint32_t craw[2][16][3][2];  // chroma windows: 8 bytes per row
+            uint8_t wxo[16], cxo[2][16];
+        };
+        struct {                         // intra (k_wg MC waves): prediction tiles with halo
+            uint8_t ty[17 * TY_STRIDE], tu[9 * TC_STRIDE], tv[9 * TC_STRIDE];
+            uint8_t sx[32];
+            uint8_t junk[256];
+        };
+    };
 };
 
 // MB `mb` of picture p (one wave): deblocking record -> db[64]; residual ->
@@ -1197,7 +1206,8 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
     }
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool prof = PROF && a.prof != nullptr;     // PROF = false: no clock code at all
-    for (int e = lane; e < 9 * 16; e += WAVE) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
+    if (!RING)       // (k_wg builds it in its prologue, for the MC waves too)
+        for (int e = lane; e < 9 * 16; e += WAVE) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
     const unsigned long long tstart = prof ? wall_clock64() : 0;
     uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
 
@@ -1227,6 +1237,8 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
                 }
                 wave_sync();
                 if (prof) pt[7] += clock64() - tw;
+                // MB c reconstructed: MB c-1's slot (its left neighbour) is free
+                if (lane == 0) lds_st(&R->consumed, c);
                 own_y = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
                 own_c = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
                 own_db = ((const uint32_t *)R->db[slot])[lane & 15];
@@ -1240,7 +1252,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
                 ((uint32_t *)L.res)[64 + lane] = n_r1;
                 ((uint32_t *)L.res)[128 + lane] = n_r2;
             }
-            if (qtype == MBT_IPCM) {
+            if (!RING && qtype == MBT_IPCM) {      // (RING: the MC wave put the samples in the slot)
                 const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)coef_base + qcoef) * 16);
                 const uint32_t py = src[lane], pc = src[64 + li];
                 *(uint32_t *)(Lb + own_y_lds) = py;
@@ -1286,11 +1298,11 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             top = (uint32_t)gr;
             if (prof && lane == 0) pmb[1] = wall_clock64();
         };
-        const bool early = has_up && intra && qtype != MBT_IPCM;
+        const bool early = !RING && has_up && intra && qtype != MBT_IPCM;
         if (early) fetch_top(true);
         if (prof) { tc1 = clock64(); pt[0] += tc1 - tc0; tc0 = tc1; }
 
-        if (intra && qtype != MBT_IPCM) {
+        if (!RING && intra && qtype != MBT_IPCM) {     // (RING: reconstructed by the MC waves)
             const bool aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
             const uint32_t b0 = top & 255, b1 = (top >> 8) & 255, b2 = (top >> 16) & 255, b3 = top >> 24;
             if (lane >= 24 && lane < 32) {
@@ -1324,12 +1336,11 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             }
         }
         wave_sync();
-        // MB c's ring slot is no longer read: hand it back to the MC waves
-        if (RING && lane == 0) lds_st(&R->consumed, c + 1);
 
         // ---- unfiltered edges: bottom row (mailbox dwords 24..31), right column
-        uint32_t unf;
-        {
+        //      (RING: published by the MC waves)
+        if (!RING) {
+            uint32_t unf;
             const int k = li & 7;     // lanes 24..31 (mirrored for the rest)
             const uint8_t *ub = k < 4 ? &L.ry[19 * RY_S + 4 + k * 4] : k < 6 ? &L.ru[9 * RC_S + 4 + (k - 4) * 4] : &L.rv[9 * RC_S + 4 + (k - 6) * 4];
             unf = *(const uint32_t *)ub;
@@ -1337,11 +1348,11 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             const uint8_t rc = *rcp;
             wave_sync();
             *(lane < 32 ? &L.left_unf[lane] : &L.junk[lane]) = rc;
+            // publish this MB's unfiltered bottom row (the row below's intra neighbours)
+            // (every lane: lanes with equal li & 7 hold the same dword, so the
+            // duplicates store identical data to the same granule)
+            st_gran(has_down ? mbx_me + (size_t)c * 32 + 24 + (li & 7) : sink, unf, tag);
         }
-        // publish this MB's unfiltered bottom row (the row below's intra neighbours)
-        // (every lane: lanes with equal li & 7 hold the same dword, so the
-        // duplicates store identical data to the same granule)
-        st_gran(has_down ? mbx_me + (size_t)c * 32 + 24 + (li & 7) : sink, unf, tag);
         if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
         // ---- vertical edges (need only this row's samples)
         if (dbf) {
@@ -1478,6 +1489,85 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
 // blockIdx = pair * S + s, so with round-robin placement stream s stays on
 // XCD s % 8 (speed only).
 // ---------------------------------------------------------------------------
+// k_wg MC wave, intra MB c of row r: unfiltered neighbours -> prediction
+// tile -> the MB's ring slot (reconstruction runs ahead of the deblocking
+// row unit; intra prediction reads unfiltered samples only).  Left: MB c-1's
+// slot, once its flag shows it reconstructed.  Top: the row above's mailbox
+// entries c-1..c+1, dwords 24..31 (unfiltered bottom rows, published by that
+// row's MC waves), polled until their tags carry this launch's epoch.
+__device__ void mc_intra(const ReconArgs &a, int p, int r, int c, int lane, McScratch &M, MbRing &R,
+                         const uint32_t *i4tab)
+{
+    const int W = a.w, H = a.h;
+    const PicDesc &pd = a.pics[p];
+    const MbRec &rec = a.rec[pd.rec_base + r * W + c];
+    const int qtype = rec.type, avail = rec.avail, pred = rec.pred;
+    const uint64_t i4 = *(const uint64_t *)rec.i4;
+    const int slot = c & (RING_K - 1);
+    const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
+    const uint32_t tag = a.epoch;
+    if (aA) {
+        unsigned spins = 0;
+        while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[(c - 1) & (RING_K - 1)])) != c) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }   // bounded wait
+        }
+        wave_sync();
+    }
+    uint32_t top = 0;
+    if (r > 0 && (aB || aC || aD)) {
+        // lanes 24..31: entry c dwords 24..31 (B); 32: entry c+1 dword 24 (C);
+        // 33..35: entry c-1 dwords 27/29/31 (D)
+        const int dsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;
+        const int dw = lane < 32 ? (lane & 31) : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 24;
+        const int ce = min(max(c + dsel, 0), W - 1);
+        const unsigned long long *g = a.mbx + ((size_t)p * H + r - 1) * W * 32 + ce * 32 + dw;
+        const bool mine = (lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD);
+        unsigned long long gr = ld_gran(g);
+        unsigned spins = 0;
+        while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 20)) { if (lane == 0) atomicOr(a.err + p, 2u); break; }   // bounded wait
+            if (mine) gr = ld_gran(g);
+        }
+        top = (uint32_t)gr;
+    }
+    const uint8_t *lp = R.px[(c - 1) & (RING_K - 1)];
+    {   // tile halo: top row (incl. top-left / top-right), left column
+        const uint32_t b0 = top & 255, b1 = (top >> 8) & 255, b2 = (top >> 16) & 255, b3 = top >> 24;
+        if (lane >= 24 && lane < 32) {
+            if (aB) {
+                const int k = lane - 24;
+                uint8_t *dst = k < 4 ? &M.ty[1 + k * 4] : (k < 6 ? &M.tu[1 + (k - 4) * 4] : &M.tv[1 + (k - 6) * 4]);
+                dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
+            }
+        } else if (lane == 32) {
+            if (aC) { M.ty[17] = b0; M.ty[18] = b1; M.ty[19] = b2; M.ty[20] = b3; }
+        } else if (lane < 36) {
+            if (aD) (lane == 33 ? M.ty[0] : lane == 34 ? M.tu[0] : M.tv[0]) = b3;
+        } else if (lane >= 40 && lane < 56) {
+            if (aA) M.ty[(lane - 39) * TY_STRIDE] = lp[(lane - 40) * 16 + 15];
+        } else if (lane >= 56) {
+            const int k = lane - 56;
+            if (aA) { M.tu[(k + 1) * TC_STRIDE] = lp[256 + k * 8 + 7]; M.tv[(k + 1) * TC_STRIDE] = lp[320 + k * 8 + 7]; }
+        }
+    }
+    wave_sync();
+    intra_tile(qtype, avail, pred, i4, R.res[slot], rec.cbits != 0, M.ty, M.tu, M.tv, i4tab, M.sx, M.junk, lane);
+    uint8_t *px = R.px[slot];
+    {   // tile -> slot (tile samples start at column 1: byte reads)
+        const int orow = lane >> 2, oq = lane & 3;
+        const uint8_t *sy = &M.ty[(orow + 1) * TY_STRIDE + 1 + oq * 4];
+        *(uint32_t *)&px[orow * 16 + oq * 4] = sy[0] | (sy[1] << 8) | (sy[2] << 16) | ((uint32_t)sy[3] << 24);
+    }
+    if (lane < 32) {
+        const int comp = (lane >> 4) & 1, crow = (lane >> 1) & 7, cq = lane & 1;
+        const uint8_t *sp = &(comp ? M.tv : M.tu)[(crow + 1) * TC_STRIDE + 1 + cq * 4];
+        *(uint32_t *)&px[256 + comp * 64 + crow * 8 + cq * 4] = sp[0] | (sp[1] << 8) | (sp[2] << 16) | ((uint32_t)sp[3] << 24);
+    }
+    wave_sync();
+}
+
 template <bool PIPE, int NMC, bool PROF>
 __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
 {
@@ -1491,6 +1581,7 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
     const int p = k * S + s;
     if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
     if (threadIdx.x == 0) R.consumed = 0;
+    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 1)) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
     __syncthreads();
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wid == 0) {
@@ -1512,8 +1603,23 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
             wave_sync();
         }
         const unsigned long long t0 = PROF ? clock64() : 0;
-        mc_core<PIPE>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot]);
+        const int type = mc_core<PIPE>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot]);
+        if (type == MBT_IPCM) {
+            const PicDesc &pd = a.pics[p];
+            const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
+            ((uint32_t *)R.px[slot])[lane] = src[lane];
+            if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
+        } else if (type >= MBT_I4x4) {
+            mc_intra(a, p, r, c, lane, Mw, R, L.i4tab);
+        }
         wave_sync();
+        {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
+            const int k = lane & 7;
+            const uint8_t *px = R.px[slot];
+            const uint32_t v = *(const uint32_t *)&px[k < 4 ? 240 + k * 4 : k < 6 ? 312 + (k - 4) * 4 : 376 + (k - 6) * 4];
+            if (r + 1 < a.h)
+                st_gran(a.mbx + ((size_t)p * a.h + r) * a.w * 32 + c * 32 + 24 + k, v, a.epoch);
+        }
         if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
     }

@@ -6,7 +6,6 @@ run() {
   timeout -k 10 300 env $1 python bench.py --no-cpu-baseline $2 > gpurun_out/pe.log 2>&1 || { tail -20 gpurun_out/pe.log; exit 1; }
   python3 -c "import json,sys;d=json.loads(open('gpurun_out/pe.log').read().strip().splitlines()[-1]);print(sys.argv[1], d['value'], d['roofline']['achieved'], d['kernels'], d['bitexact_check'])" "$1 $2"
 }
-run "X=1" ""
-export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/px/f -o b -- python3 bench.py --no-cpu-baseline --no-verify --steps 8 > /dev/null 2>&1
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/px/w -o b -- python3 bench.py --no-cpu-baseline --no-verify --steps 8 > /dev/null 2>&1
+run "H264MI_WG_NMC=3" ""
+run "H264MI_WG_NMC=2" ""
+H264MI_KERNEL=wg timeout -k 10 120 python tools/prof_rows.py > gpurun_out/prof_wg.log 2>&1
