@@ -1495,7 +1495,7 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
 // slot, once its flag shows it reconstructed.  Top: the row above's mailbox
 // entries c-1..c+1, dwords 24..31 (unfiltered bottom rows, published by that
 // row's MC waves), polled until their tags carry this launch's epoch.
-__device__ void mc_intra(const ReconArgs &a, int p, int r, int c, int lane, McScratch &M, MbRing &R,
+__device__ __attribute__((noinline)) void mc_intra(const ReconArgs &a, int p, int r, int c, int lane, McScratch &M, MbRing &R,
                          const uint32_t *i4tab)
 {
     const int W = a.w, H = a.h;
