@@ -391,45 +391,55 @@ __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int
 // GetLumaEdgeThresholds :1381-1449, GetChromaEdgeThresholds :1460-1532.
 // ---------------------------------------------------------------------------
 // computes the record into s_db (LDS, 64 B)
-__device__ void mb_dbrec(const ReconArgs &a, int gmb, const MbRec &q, int lane, uint8_t *s_db)
+// Deblocking record of MB gmb (GetBoundaryStrengths, deblocking.c:1134-1370;
+// thresholds :1381-1532).  The MB's record and its left / top neighbours'
+// are staged in LDS (srec, 72 dwords) by one coalesced load per lane, so the
+// per-lane bS decisions read LDS instead of issuing dependent global loads;
+// the threshold-table loads are issued before the bS work.
+__device__ void mb_dbrec(const ReconArgs &a, int gmb, const MbRec &q, int lane, uint8_t *s_db, uint32_t *srec)
 {
     const bool fl = q.avail & DB_LEFT, ft = q.avail & DB_TOP;
-    if (lane < 32) {
-        const int dir = lane >> 4, kk = (lane >> 2) & 3, e = lane & 3;
-        int bS = 0;
-        const bool on = (q.avail & DB_INNER) && (e > 0 || (dir == 0 ? fl : ft));
+    {
+        const uint32_t *rq = (const uint32_t *)(a.rec + gmb);
+        const uint32_t *rl = (const uint32_t *)(a.rec + (fl ? gmb - 1 : gmb));
+        const uint32_t *rt = (const uint32_t *)(a.rec + (ft ? gmb - a.w : gmb));
+        const uint32_t v0 = lane < 24 ? rq[lane] : lane < 48 ? rl[lane - 24] : rt[lane - 48];
+        const uint32_t v1 = rt[16 + (lane & 7)];
+        srec[lane] = v0;
+        if (lane < 8) srec[64 + lane] = v1;
+    }
+    wave_sync();
+    const MbRec *Q = (const MbRec *)srec;
+    // thresholds: lanes 32..37 = luma classes 0..2 (internal, left, top), chroma 3..5
+    const int k = lane - 32;
+    const bool thr = k >= 0 && k < 6;
+    const bool chroma = k >= 3;
+    const int cls = chroma ? k - 3 : k;
+    const MbRec *PN = (const MbRec *)(srec + ((cls == 1 && fl) ? 24 : (cls == 2 && ft) ? 48 : 0));
+    const int qpp = chroma ? PN->qpc : PN->qp, qq = chroma ? Q->qpc : Q->qp;
+    const int qpav = (qpp + qq + 1) >> 1;
+    const int ia = clip3(0, 51, qpav + Q->offA), ib = clip3(0, 51, qpav + Q->offB);
+    const uint32_t al = cAlpha[ia], be = cBeta[ib], t0 = cTc0[ia][0], t1 = cTc0[ia][1], t2 = cTc0[ia][2];
+    // bS: lanes 0..31 = (dir, line segment kk, edge e)
+    int bS = 0;
+    {
+        const int dir = (lane >> 4) & 1, kk = (lane >> 2) & 3, e = lane & 3;
+        const bool on = lane < 32 && (Q->avail & DB_INNER) && (e > 0 || (dir == 0 ? fl : ft));
         if (on) {
-            const MbRec &pm = e > 0 ? q : (dir == 0 ? a.rec[gmb - 1] : a.rec[gmb - a.w]);
+            const MbRec &pm = *(const MbRec *)(srec + (e > 0 ? 0 : dir == 0 ? 24 : 48));
             const int bq = dir == 0 ? blk_of(e, kk) : blk_of(kk, e);
             const int bp = e == 0 ? (dir == 0 ? blk_of(3, kk) : blk_of(kk, 3))
                                   : (dir == 0 ? blk_of(e - 1, kk) : blk_of(kk, e - 1));
-            bS = bs_of(pm, bp, q, bq, e == 0);
+            bS = bs_of(pm, bp, *Q, bq, e == 0);
         }
-        // pack two nibbles per byte: even lane owns the low nibble
-        const int hi = __shfl_down(bS, 1, 64);
-        if (!(lane & 1)) s_db[lane >> 1] = (uint8_t)(bS | (hi << 4));
-    } else if (lane < 38) {
-        const int k = lane - 32;               // 0..2 luma classes, 3..5 chroma
-        const bool chroma = k >= 3;
-        const int cls = chroma ? k - 3 : k;
-        int qpp;
-        if (cls == 0) qpp = chroma ? q.qpc : q.qp;
-        else {
-            const bool has = cls == 1 ? fl : ft;
-            const MbRec *pm = has ? &a.rec[cls == 1 ? gmb - 1 : gmb - a.w] : &q;
-            qpp = chroma ? pm->qpc : pm->qp;
-        }
-        const int qq = chroma ? q.qpc : q.qp;
-        const int qpav = (qpp + qq + 1) >> 1;
-        const int ia = clip3(0, 51, qpav + q.offA), ib = clip3(0, 51, qpav + q.offB);
-        uint8_t *o = s_db + 16 + k * 8;
-        o[0] = cAlpha[ia];
-        o[1] = cBeta[ib];
-        o[2] = cTc0[ia][0];
-        o[3] = cTc0[ia][1];
-        o[4] = cTc0[ia][2];
-        o[5] = (uint8_t)ia;
-        o[6] = o[7] = 0;
+    }
+    // pack two nibbles per byte: even lane owns the low nibble
+    const int hi = __shfl_down(bS, 1, 64);
+    if (lane < 32 && !(lane & 1)) s_db[lane >> 1] = (uint8_t)(bS | (hi << 4));
+    if (thr) {
+        uint32_t *o = (uint32_t *)(s_db + 16 + k * 8);
+        o[0] = al | be << 8 | t0 << 16 | t1 << 24;
+        o[1] = t2 | (uint32_t)ia << 8;
     }
     wave_sync();
 }
@@ -443,6 +453,7 @@ __device__ void mb_dbrec(const ReconArgs &a, int gmb, const MbRec &q, int lane, 
 // per-wave LDS scratch of the MB reconstruction (reference windows)
 struct McScratch {
     int32_t dc[24];
+    uint32_t srec[72];               // deblocking record inputs: this MB's, left and top records
     union {
         struct {                         // inter: reference windows
             uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
@@ -462,10 +473,13 @@ struct McScratch {
 // MBs: 6-tap / bilinear MC + residual, clipped, -> px[384] (luma 16x16, Cb
 // 8x8, Cr 8x8).  All outputs in LDS.  PIPE: reference samples written by a
 // picture of this launch are waited for (per-row progress) and read sc1.
-template <bool PIPE>
+// PROF: *ph receives four 16-bit shader-cycle durations: deblocking record,
+// residual, window landing + LDS staging, interpolation (inter MBs)
+template <bool PIPE, bool PROF = false>
 __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M, uint8_t *px, int16_t *res,
-                       uint8_t *db)
+                       uint8_t *db, unsigned long long *ph = nullptr)
 {
+    unsigned long long tp0 = PROF ? clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0;
     const PicDesc pd = a.pics[p];
     const int gmb = pd.rec_base + mb;
     const MbRec &r = a.rec[gmb];
@@ -474,7 +488,7 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
 
     const int mbx = mb % a.w, mby = mb / a.w;
     if (r.type >= MBT_I4x4) {
-        mb_dbrec(a, gmb, r, lane, db);
+        mb_dbrec(a, gmb, r, lane, db, M.srec);
         if (r.type != MBT_IPCM && r.cbits) {
             int e = 0;
             mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
@@ -564,13 +578,15 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         }
     }
 
-    mb_dbrec(a, gmb, r, lane, db);
+    mb_dbrec(a, gmb, r, lane, db, M.srec);
+    if (PROF) tp1 = clock64();
     int e = 0;
     if (r.cbits) {
         mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
     } else {
         for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
     }
+    if (PROF) tp2 = clock64();
 
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -609,6 +625,7 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         M.cxo[ccomp][cb] = (uint8_t)(c_in ? c_x0 - c_ax : 0);
     }
     wave_sync();
+    if (PROF) tp3 = clock64();
 
     {   // luma: lane -> (block, row)
         const int b = lane >> 2, yy = lane & 3;
@@ -635,6 +652,11 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
     wave_sync();
 
     if (lane == 0 && e) atomicOr(a.err + p, 1u);
+    if (PROF && ph) {
+        const unsigned long long tp4 = clock64();
+        auto d16 = [](unsigned long long d) { return d > 65535 ? 65535ull : d; };
+        *ph = d16(tp1 - tp0) | d16(tp2 - tp1) << 16 | d16(tp3 - tp2) << 32 | d16(tp4 - tp3) << 48;
+    }
     return r.type;
 }
 
@@ -1296,7 +1318,7 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
                 if (mine) gr = ld_gran(tga);          // re-poll only the granules still needed
             }
             top = (uint32_t)gr;
-            if (prof && lane == 0) pmb[1] = wall_clock64();
+            if (prof && !RING && lane == 0) pmb[1] = wall_clock64();   // (RING: slot 1 holds the MC phases)
         };
         const bool early = !RING && has_up && intra && qtype != MBT_IPCM;
         if (early) fetch_top(true);
@@ -1603,7 +1625,9 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
             wave_sync();
         }
         const unsigned long long t0 = PROF ? clock64() : 0;
-        const int type = mc_core<PIPE>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot]);
+        unsigned long long ph = 0;
+        const int type = mc_core<PIPE, PROF>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], &ph);
+        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 1] = ph;
         if (type == MBT_IPCM) {
             const PicDesc &pd = a.pics[p];
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);

@@ -30,6 +30,10 @@ for k in range(6):
         L.h264mi_engine_profile(eng._h, 1, mbuf, len(mbuf))
         mc = np.frombuffer(mbuf, dtype=np.uint64)[S * h * 16:].reshape(S, h, w, 4)[:, :, :, 3].astype(np.float64)
         print("   MC wave cycles/MB mean %.0f p50 %.0f p90 %.0f max %.0f" % (mc.mean(), np.percentile(mc, 50), np.percentile(mc, 90), mc.max()))
+        mph = np.frombuffer(mbuf, dtype=np.uint64)[S * h * 16:].reshape(S, h, w, 4)[:, :, :, 1]
+        parts = [((mph >> np.uint64(16 * i)) & np.uint64(0xFFFF)).astype(np.float64) for i in range(4)]
+        parts = [x[mph > 0] for x in parts]
+        print("   MC phases (mean cycles): dbrec %.0f residual %.0f windows %.0f interp %.0f" % tuple(x.mean() for x in parts))
     print("   row0 cycles/MB", " ".join("%.0f" % x for x in ph[0].mean(axis=0)), " row40", " ".join("%.0f" % x for x in ph[40].mean(axis=0)))
 
 # per-MB hand-off timing of the last picture batch (100 MHz clock -> us)
