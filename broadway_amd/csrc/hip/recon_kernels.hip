@@ -1083,10 +1083,16 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
     }
 }
 
-__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// (global address space explicit: a generic pointer would make these FLAT
+// accesses, which lgkmcnt counts too -- every LDS wait would then wait for them)
+typedef __attribute__((address_space(1))) unsigned long long g_u64;
+__device__ __forceinline__ unsigned long long ld_gran(const unsigned long long *p)
+{
+    return __hip_atomic_load((const g_u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void st_gran(unsigned long long *p, uint32_t v, uint32_t tag)
 {
-    __hip_atomic_store(p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((g_u64 *)p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // LDS hand-off ring between the MC waves of a row workgroup and its row
@@ -1517,39 +1523,40 @@ __global__ __launch_bounds__(64) void k_rows(ReconArgs a)
 // slot, once its flag shows it reconstructed.  Top: the row above's mailbox
 // entries c-1..c+1, dwords 24..31 (unfiltered bottom rows, published by that
 // row's MC waves), polled until their tags carry this launch's epoch.
-__device__ __attribute__((noinline)) void mc_intra(const ReconArgs &a, int p, int r, int c, int lane, McScratch &M, MbRing &R,
-                         const uint32_t *i4tab)
+// (out of line to keep the kernel's VGPR count for 3 workgroups per CU; the
+// arguments are plain values: a reference to the kernel's ReconArgs would
+// force the whole argument block into private memory)
+__device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const unsigned long long *mbx_up, unsigned *perr,
+                                                   int W, int c, uint32_t tag, bool has_up, int lane, McScratch &M,
+                                                   MbRing &R, const uint32_t *i4tab)
 {
-    const int W = a.w, H = a.h;
-    const PicDesc &pd = a.pics[p];
-    const MbRec &rec = a.rec[pd.rec_base + r * W + c];
+    const MbRec &rec = *mbrec;
     const int qtype = rec.type, avail = rec.avail, pred = rec.pred;
     const uint64_t i4 = *(const uint64_t *)rec.i4;
     const int slot = c & (RING_K - 1);
     const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
-    const uint32_t tag = a.epoch;
     if (aA) {
         unsigned spins = 0;
         while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[(c - 1) & (RING_K - 1)])) != c) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }   // bounded wait
+            if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
         }
         wave_sync();
     }
     uint32_t top = 0;
-    if (r > 0 && (aB || aC || aD)) {
+    if (has_up && (aB || aC || aD)) {
         // lanes 24..31: entry c dwords 24..31 (B); 32: entry c+1 dword 24 (C);
         // 33..35: entry c-1 dwords 27/29/31 (D)
         const int dsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;
         const int dw = lane < 32 ? (lane & 31) : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 24;
         const int ce = min(max(c + dsel, 0), W - 1);
-        const unsigned long long *g = a.mbx + ((size_t)p * H + r - 1) * W * 32 + ce * 32 + dw;
+        const unsigned long long *g = mbx_up + ce * 32 + dw;
         const bool mine = (lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD);
         unsigned long long gr = ld_gran(g);
         unsigned spins = 0;
         while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 20)) { if (lane == 0) atomicOr(a.err + p, 2u); break; }   // bounded wait
+            if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
             if (mine) gr = ld_gran(g);
         }
         top = (uint32_t)gr;
@@ -1634,7 +1641,9 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
             ((uint32_t *)R.px[slot])[lane] = src[lane];
             if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
         } else if (type >= MBT_I4x4) {
-            mc_intra(a, p, r, c, lane, Mw, R, L.i4tab);
+            const PicDesc &pd = a.pics[p];
+            mc_intra(a.rec + pd.rec_base + r * a.w + c, a.mbx + ((size_t)p * a.h + (r > 0 ? r - 1 : 0)) * a.w * 32,
+                     a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, L.i4tab);
         }
         wave_sync();
         {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
