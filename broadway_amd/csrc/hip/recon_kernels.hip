@@ -395,21 +395,23 @@ __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int
 // thresholds :1381-1532).  The MB's record and its left / top neighbours'
 // are staged in LDS (srec, 72 dwords) by one coalesced load per lane, so the
 // per-lane bS decisions read LDS instead of issuing dependent global loads;
-// the threshold-table loads are issued before the bS work.
-__device__ void mb_dbrec(const ReconArgs &a, int gmb, const MbRec &q, int lane, uint8_t *s_db, uint32_t *srec)
+// the threshold-table loads are issued before the bS work.  srec is staged
+// by the caller (stage_recs_load).
+// the MB's, left and top records in LDS (srec: dwords 0..23, 24..47, 48..71)
+__device__ __forceinline__ void stage_recs_load(const ReconArgs &a, int gmb, int mbx, int mby, int lane, uint32_t &v0,
+                                                uint32_t &v1)
 {
-    const bool fl = q.avail & DB_LEFT, ft = q.avail & DB_TOP;
-    {
-        const uint32_t *rq = (const uint32_t *)(a.rec + gmb);
-        const uint32_t *rl = (const uint32_t *)(a.rec + (fl ? gmb - 1 : gmb));
-        const uint32_t *rt = (const uint32_t *)(a.rec + (ft ? gmb - a.w : gmb));
-        const uint32_t v0 = lane < 24 ? rq[lane] : lane < 48 ? rl[lane - 24] : rt[lane - 48];
-        const uint32_t v1 = rt[16 + (lane & 7)];
-        srec[lane] = v0;
-        if (lane < 8) srec[64 + lane] = v1;
-    }
-    wave_sync();
+    const uint32_t *rq = (const uint32_t *)(a.rec + gmb);
+    const uint32_t *rl = (const uint32_t *)(a.rec + (mbx > 0 ? gmb - 1 : gmb));
+    const uint32_t *rt = (const uint32_t *)(a.rec + (mby > 0 ? gmb - a.w : gmb));
+    v0 = *(lane < 24 ? rq + lane : lane < 48 ? rl + (lane - 24) : rt + (lane - 48));
+    v1 = rt[16 + (lane & 7)];
+}
+
+__device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint32_t *srec)
+{
     const MbRec *Q = (const MbRec *)srec;
+    const bool fl = Q->avail & DB_LEFT, ft = Q->avail & DB_TOP;
     // thresholds: lanes 32..37 = luma classes 0..2 (internal, left, top), chroma 3..5
     const int k = lane - 32;
     const bool thr = k >= 0 && k < 6;
@@ -475,26 +477,41 @@ struct McScratch {
 // picture of this launch are waited for (per-row progress) and read sc1.
 // PROF: *ph receives four 16-bit shader-cycle durations: deblocking record,
 // residual, window landing + LDS staging, interpolation (inter MBs)
+// pre0/pre1: the staged-record words of this MB when has_pre (loaded one MB
+// ahead by the caller); next_mb >= 0: load the next MB's into pre0/pre1 once
+// this MB's are in LDS.
 template <bool PIPE, bool PROF = false>
 __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M, uint8_t *px, int16_t *res,
-                       uint8_t *db, unsigned long long *ph = nullptr)
+                       uint8_t *db, unsigned long long *ph = nullptr, bool has_pre = false, uint32_t *pre = nullptr,
+                       int next_mb = -1)
 {
     unsigned long long tp0 = PROF ? clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0;
     const PicDesc pd = a.pics[p];
     const int gmb = pd.rec_base + mb;
-    const MbRec &r = a.rec[gmb];
+    const int mbx = mb % a.w, mby = mb / a.w;
+    {
+        uint32_t v0, v1;
+        if (has_pre) { v0 = pre[0]; v1 = pre[1]; }
+        else stage_recs_load(a, gmb, mbx, mby, lane, v0, v1);
+        M.srec[lane] = v0;
+        if (lane < 8) M.srec[64 + lane] = v1;
+        if (next_mb >= 0) stage_recs_load(a, pd.rec_base + next_mb, next_mb % a.w, next_mb / a.w, lane, pre[0], pre[1]);
+    }
+    wave_sync();
+    const MbRec &r = *(const MbRec *)M.srec;
+    const int rtype = __builtin_amdgcn_readfirstlane(r.type);
+    const uint32_t rcbits = __builtin_amdgcn_readfirstlane(r.cbits);
     int16_t *s_res = res;
     uint8_t *s_out = px;
 
-    const int mbx = mb % a.w, mby = mb / a.w;
-    if (r.type >= MBT_I4x4) {
-        mb_dbrec(a, gmb, r, lane, db, M.srec);
-        if (r.type != MBT_IPCM && r.cbits) {
+    if (rtype >= MBT_I4x4) {
+        mb_dbrec(a, lane, db, M.srec);
+        if (rtype != MBT_IPCM && rcbits) {
             int e = 0;
             mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
             if (e && lane == 0) atomicOr(a.err + p, 1u);
         }
-        return r.type;
+        return rtype;
     }
 
     const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
@@ -578,10 +595,10 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         }
     }
 
-    mb_dbrec(a, gmb, r, lane, db, M.srec);
+    mb_dbrec(a, lane, db, M.srec);
     if (PROF) tp1 = clock64();
     int e = 0;
-    if (r.cbits) {
+    if (rcbits) {
         mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
     } else {
         for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
@@ -657,7 +674,7 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         auto d16 = [](unsigned long long d) { return d > 65535 ? 65535ull : d; };
         *ph = d16(tp1 - tp0) | d16(tp2 - tp1) << 16 | d16(tp3 - tp2) << 32 | d16(tp4 - tp3) << 48;
     }
-    return r.type;
+    return rtype;
 }
 
 // k_mb: every MB of the batch in parallel, one wave per MB.  XCD-aware MB
@@ -1621,6 +1638,8 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
         return;
     }
     McScratch &Mw = M[wid - 1];
+    uint32_t pre[2] = {0, 0};
+    bool has_pre = false;
     for (int c = wid - 1; c < a.w; c += NMC) {
         const int slot = c & (RING_K - 1);
         if (c >= RING_K) {
@@ -1633,7 +1652,9 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
         }
         const unsigned long long t0 = PROF ? clock64() : 0;
         unsigned long long ph = 0;
-        const int type = mc_core<PIPE, PROF>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], &ph);
+        const int type = mc_core<PIPE, PROF>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], &ph,
+                                             has_pre, pre, c + NMC < a.w ? r * a.w + c + NMC : -1);
+        has_pre = true;
         if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 1] = ph;
         if (type == MBT_IPCM) {
             const PicDesc &pd = a.pics[p];

@@ -7,5 +7,4 @@ run() {
   python3 -c "import json,sys;d=json.loads(open('gpurun_out/pe.log').read().strip().splitlines()[-1]);print(sys.argv[1], d['value'], d['roofline']['achieved'], d['kernels']['k_wg']['avg_launch_us'], d['bitexact_check'])" "$1 $2"
 }
 run "H264MI_WG_NMC=3" ""
-run "H264MI_WG_NMC=4" ""
 H264MI_KERNEL=wg timeout -k 10 120 python tools/prof_rows.py > gpurun_out/prof_wg.log 2>&1
