@@ -34,6 +34,7 @@ struct h264mi_engine {
     unsigned long long *d_gjunk;  // 64 KiB store sink (ReconArgs::gjunk)
     int classic;                  // single-picture launches: k_wg (default) or k_mb + k_rows (H264MI_KERNEL=classic)
     int wg_nmc;                   // MC waves per k_wg workgroup (H264MI_WG_NMC: 2, 3 or 4)
+    int wg_pp;                    // single-picture k_wg launches: two ping-pong row units (k_wgpp, default; H264MI_WG_PP=0: one)
     // stream groups (h264mi_engine_set_groups): the pictures of a device-input
     // batch split into G groups, each on its own HIP stream, so one group's
     // k_mb overlaps the other groups' latency-bound k_rows
@@ -41,8 +42,14 @@ struct h264mi_engine {
     hipStream_t gst[H264MI_MAX_GROUPS];
     int stagger_pending;
     int order_depth, order_lag;
-    uint8_t *d_dbrec;         // 64 B per batch MB
-    int16_t *d_res;           // 384 x int16 per batch MB (intra residual)
+    uint8_t *d_dbrec;         // 64 B per batch MB (x2: k_prep double buffer)
+    int16_t *d_res;           // 384 x int16 per batch MB (x2)
+    // k_prep (deblocking records + residuals one batch ahead, on its own
+    // stream): buffer half prep_parity, ordered by events
+    int prep;                 // H264MI_PREP (default 1)
+    int prep_parity;
+    hipStream_t st2;
+    hipEvent_t ev_in, ev_prep, ev_wgdone[2];
     MbRec *d_rec;
     int16_t *d_coef;
     size_t coef_cap;          // blocks
@@ -80,8 +87,8 @@ static int alloc_pic_buffers(h264mi_engine *e, int cap)
 {
     const size_t np = (size_t)cap, mbs = np * e->nmbs, rows = np * e->h;
     bool ok = hipMalloc(&e->d_mbx, mbs * 256) == hipSuccess &&
-              hipMalloc(&e->d_dbrec, mbs * 64) == hipSuccess &&
-              hipMalloc(&e->d_res, mbs * 768) == hipSuccess &&
+              hipMalloc(&e->d_dbrec, 2 * mbs * 64) == hipSuccess &&
+              hipMalloc(&e->d_res, 2 * mbs * 768) == hipSuccess &&
               hipMalloc(&e->d_err, sizeof(unsigned) * np) == hipSuccess &&
               hipMalloc(&e->d_progress, rows * 4) == hipSuccess &&
               hipHostMalloc(&e->h_err, sizeof(unsigned) * np, hipHostMallocDefault) == hipSuccess &&
@@ -119,7 +126,14 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         const char *km = getenv("H264MI_KERNEL");
         e->classic = km && !strcmp(km, "classic");
         const char *nm = getenv("H264MI_WG_NMC");
-        e->wg_nmc = nm ? atoi(nm) : 3;
+        const char *pp = getenv("H264MI_WG_PP");
+        e->wg_pp = pp ? atoi(pp) : 1;
+        // MC waves per workgroup: 2 with the ping-pong row units (4 waves,
+        // three workgroups per CU keep every row of 8 1080p pictures
+        // resident), 3 with one row unit
+        e->wg_nmc = nm ? atoi(nm) : (e->wg_pp ? 2 : 3);
+        const char *pr = getenv("H264MI_PREP");
+        e->prep = pr ? atoi(pr) : 1;
     }
     bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
 
@@ -135,7 +149,12 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
               hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess &&
-              hipEventCreate(&e->ev2) == hipSuccess;
+              hipEventCreate(&e->ev2) == hipSuccess &&
+              hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_wgdone[0], hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_wgdone[1], hipEventDisableTiming) == hipSuccess;
     ok = ok && alloc_pic_buffers(e, nstreams) == 0;
     if (!ok) {
         fprintf(stderr, "h264mi: engine allocation failed\n");
@@ -153,6 +172,7 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
 {
     if (!e) return;
     if (e->st) (void)hipStreamSynchronize(e->st);
+    if (e->st2) (void)hipStreamSynchronize(e->st2);
     free_pic_buffers(e);
     (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
     (void)hipFree(e->d_pics); (void)hipFree(e->d_gjunk);
@@ -161,6 +181,11 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
+    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
+    for (int i = 0; i < 2; i++)
+        if (e->ev_wgdone[i]) (void)hipEventDestroy(e->ev_wgdone[i]);
+    if (e->st2) (void)hipStreamDestroy(e->st2);
     h264mi_engine_set_timing(e, 0);
     for (int g = 0; g < H264MI_MAX_GROUPS; g++)
         if (e->gst[g]) { (void)hipStreamSynchronize(e->gst[g]); (void)hipStreamDestroy(e->gst[g]); }
@@ -232,6 +257,26 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         if (pipe_order(e, depth, lag < 1 ? e->h : lag)) return -1;
         a.order = e->d_order;
     }
+    // k_prep: this batch's deblocking records and residuals on st2, into the
+    // buffer half the launch before last read (ev_wgdone); device-resident
+    // input (bench) lets it overlap the previous batch's k_wg
+    const bool prep = wg && !pipe && e->prep;
+    const int pbuf = e->prep_parity;
+    if (prep) {
+        e->prep_parity ^= 1;
+        const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
+        a.dbrec = e->d_dbrec + pbuf * mbs * 64;
+        a.res = e->d_res + pbuf * mbs * 384;
+        if (!grouped) {     // host-staged input: the upload is on st
+            HIPCHECK(hipEventRecord(e->ev_in, e->st));
+            HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_in, 0));
+        }
+        HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_wgdone[pbuf], 0));
+        hipLaunchKernelGGL(k_prep, dim3((npics * e->nmbs + 3) / 4), dim3(256), 0, e->st2, a);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipEventRecord(e->ev_prep, e->st2));
+        HIPCHECK(hipStreamWaitEvent(e->st, e->ev_prep, 0));
+    }
     hipEvent_t t0 = e->ev0, t1 = e->ev1, t2 = e->ev2;
     if (e->tev && e->tev_n < e->tev_cap) {
         t0 = e->tev[3 * e->tev_n]; t1 = e->tev[3 * e->tev_n + 1]; t2 = e->tev[3 * e->tev_n + 2];
@@ -256,6 +301,16 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
             if (nmc == 2) hipLaunchKernelGGL((k_wg<true, 2, false>), grid, dim3(192), 0, e->st, a);
             else if (nmc == 4) hipLaunchKernelGGL((k_wg<true, 4, false>), grid, dim3(320), 0, e->st, a);
             else hipLaunchKernelGGL((k_wg<true, 3, false>), grid, dim3(256), 0, e->st, a);
+        } else if (e->wg_pp && prep) {
+            if (a.prof) {
+                if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, true, true>), grid, dim3(256), 0, e->st, a);
+                else hipLaunchKernelGGL((k_wgpp<3, true, true>), grid, dim3(320), 0, e->st, a);
+            } else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, false, true>), grid, dim3(256), 0, e->st, a);
+            else hipLaunchKernelGGL((k_wgpp<3, false, true>), grid, dim3(320), 0, e->st, a);
+        } else if (prep) {
+            if (a.prof) hipLaunchKernelGGL((k_wg<false, 3, true, true>), grid, dim3(256), 0, e->st, a);
+            else if (nmc == 2) hipLaunchKernelGGL((k_wg<false, 2, false, true>), grid, dim3(192), 0, e->st, a);
+            else hipLaunchKernelGGL((k_wg<false, 3, false, true>), grid, dim3(256), 0, e->st, a);
         } else if (a.prof) {
             hipLaunchKernelGGL((k_wg<false, 3, true>), grid, dim3(256), 0, e->st, a);
         } else {
@@ -267,6 +322,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     if (rec) (void)hipEventRecord(t2, e->st);
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
+    if (prep) HIPCHECK(hipEventRecord(e->ev_wgdone[pbuf], e->st));
     return 0;
 }
 
@@ -372,6 +428,7 @@ extern "C" int h264mi_engine_set_pipeline(h264mi_engine *e, int depth)
     if (!e || depth < 1) return -1;
     HIPCHECK(hipSetDevice(e->dev));
     HIPCHECK(hipStreamSynchronize(e->st));
+    HIPCHECK(hipStreamSynchronize(e->st2));
     const int cap = e->nstreams * depth;
     if (cap == e->pipe_cap) return 0;
     free_pic_buffers(e);
@@ -395,6 +452,7 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     if (!e) return -1;
     HIPCHECK(hipSetDevice(e->dev));
     HIPCHECK(hipStreamSynchronize(e->st));
+    HIPCHECK(hipStreamSynchronize(e->st2));
     for (int g = 0; g < H264MI_MAX_GROUPS; g++)
         if (e->gst[g]) HIPCHECK(hipStreamSynchronize(e->gst[g]));
     for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;

@@ -72,6 +72,30 @@ __constant__ uint8_t cTc0[52][3] = {
     {4, 6, 9}, {5, 7, 10}, {6, 8, 11}, {6, 8, 13}, {7, 10, 14}, {8, 11, 16},
     {9, 12, 18}, {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
 
+// Per-wave register tables: lane i holds entry i, looked up with
+// ds_bpermute (an LDS-crossbar lane shuffle: LDS latency, no VMEM).  A
+// per-lane index into a __constant__ array would be a VMEM load, and since
+// vmcnt retires in order, waiting for it would also wait for every
+// reference-window load issued before it.  Lookups run with all lanes active.
+struct Tabs {
+    uint32_t ab;    // lane i < 52: alpha[i] | beta[i] << 8 | tc0[i][0] << 16 | tc0[i][1] << 24
+    uint32_t c2;    // lane i < 52: tc0[i][2]
+    uint32_t ls;    // lane i < 18: levelScale[i / 3][i % 3]
+};
+__device__ __forceinline__ Tabs load_tabs(int lane)
+{
+    Tabs t;
+    const int i = lane < 52 ? lane : 0;
+    t.ab = cAlpha[i] | (uint32_t)cBeta[i] << 8 | (uint32_t)cTc0[i][0] << 16 | (uint32_t)cTc0[i][1] << 24;
+    t.c2 = cTc0[i][2];
+    t.ls = lane < 18 ? cLevelScale[lane / 3][lane % 3] : 0;
+    return t;
+}
+__device__ __forceinline__ uint32_t tab_at(uint32_t reg, int idx)
+{
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(idx << 2, (int)reg);
+}
+
 // ordering of LDS traffic between the lanes of one wave (waves of k_rows
 // work independently; k_mb workgroups are a single wave)
 // A wave's LDS instructions execute in issue order, so lanes of one wave see
@@ -126,12 +150,20 @@ __device__ __forceinline__ int blk_of(int x4, int y4) { return ((y4 >> 1) * 2 + 
 // res: LDS int16[384] (luma 16x16 raster, Cb 8x8, Cr 8x8). dc: LDS int32[24].
 // Returns (through *err) a nonzero flag if a sample leaves [-512,511].
 // ---------------------------------------------------------------------------
-__device__ void mb_residual(const MbRec &r, const int16_t *__restrict__ coef, int16_t *res,
-                            int32_t *dc, int lane, int *range_err)
+// base: the MB's coded blocks in cbits order (staged in LDS by the caller).
+// ls: the levelScale register table (Tabs::ls).
+__device__ void mb_residual(const MbRec &r, const int16_t *base, int16_t *res,
+                            int32_t *dc, int lane, int *range_err, uint32_t ls)
 {
     const uint32_t cb = r.cbits;
-    const int16_t *base = coef + (size_t)r.coef * 16;
     const bool i16 = r.type == MBT_I16;
+    // levelScale lookups (all lanes active): luma DC scale, chroma DC scale,
+    // and this lane's three AC scales (luma lanes qp, chroma lanes qpc)
+    const int qp_l = r.qp, qp_c = r.qpc;
+    const int ls_ldc = (int)tab_at(ls, (qp_l % 6) * 3), ls_cdc = (int)tab_at(ls, (qp_c % 6) * 3);
+    const int qm_mine = (lane < 16 ? qp_l : qp_c) % 6;
+    const int ls_ac0 = (int)tab_at(ls, qm_mine * 3), ls_ac1 = (int)tab_at(ls, qm_mine * 3 + 1),
+              ls_ac2 = (int)tab_at(ls, qm_mine * 3 + 2);
     if (lane < 16) {
         int32_t v = 0;
         if (i16 && (cb & (1u << 24))) {
@@ -151,7 +183,7 @@ __device__ void mb_residual(const MbRec &r, const int16_t *__restrict__ coef, in
                 s += neg ? -(int32_t)d[sp] : (int32_t)d[sp];
             }
             const int q6 = r.qp / 6;
-            const int32_t x = s * (int32_t)cLevelScale[r.qp % 6][0];
+            const int32_t x = s * ls_ldc;
             v = q6 >= 2 ? x << (q6 - 2) : ((x << q6) + 2) >> 2;
         }
         dc[lane] = v;
@@ -163,7 +195,7 @@ __device__ void mb_residual(const MbRec &r, const int16_t *__restrict__ coef, in
             const int16_t *d = base + __popc(cb & (bit - 1)) * 16;
             const int32_t c0 = d[0], c1 = d[1], c2 = d[2], c3 = d[3];
             f = b == 0 ? c0 + c1 + c2 + c3 : b == 1 ? c0 - c1 + c2 - c3 : b == 2 ? c0 + c1 - c2 - c3 : c0 - c1 - c2 + c3;
-            f = ((f * (int32_t)cLevelScale[r.qpc % 6][0]) << (r.qpc / 6)) >> 1;
+            f = ((f * ls_cdc) << (r.qpc / 6)) >> 1;
         }
         dc[lane] = f;
     }
@@ -188,7 +220,7 @@ __device__ void mb_residual(const MbRec &r, const int16_t *__restrict__ coef, in
                                s == 11 ? 10 : s == 12 ? 7 : s == 13 ? 11 : s == 14 ? 14 : 15;
                 const int cls = (!(rr & 1) && !((rr >> 2) & 1)) ? 0 : (((rr & 1) && ((rr >> 2) & 1)) ? 1 : 2);
                 if (s == 0 && skip0) continue;
-                d[rr] = (int32_t)c[s] * ((int32_t)cLevelScale[qm][cls] << q6);
+                d[rr] = (int32_t)c[s] * ((cls == 0 ? ls_ac0 : cls == 1 ? ls_ac1 : ls_ac2) << q6);
             }
             nz = true;
         }
@@ -286,6 +318,64 @@ __device__ __forceinline__ void luma_row4(const uint8_t *win, int yy, int fx, in
 #undef W
 #undef B1
 #undef H1
+}
+
+// Register form of luma_row4 (same outputs, h264bsdPredictSamples' 16
+// positions, reconstruct.c:1863-1929): the 6 window rows the lane's output
+// row reads (rows yy..yy+5 of its block's window; row yy+2 holds G) come in
+// as 3 dwords each, realigned by xo bytes, and every candidate -- G, the
+// horizontal half-sample b of rows 0/+1, the vertical half-sample h of
+// columns x/x+1, the centre j -- is computed for all lanes alike; the
+// position only selects.  j (6 horizontal 6-taps per output, then one
+// vertical) runs only if some lane of the wave needs it (wave-uniform).
+// Replaces per-sample LDS byte reads under lane-divergent position branches.
+__device__ __forceinline__ void luma_row4_reg(const uint32_t (*wr)[3], int xo, int fx, int fy, bool need_j, int out[4])
+{
+    int sm[6][9];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const uint32_t d0 = wr[i][0], d1 = wr[i][1], d2 = wr[i][2];
+        const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)xo);
+        const uint32_t a1 = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)xo);
+#pragma unroll
+        for (int x = 0; x < 4; x++) { sm[i][x] = (a0 >> (8 * x)) & 255; sm[i][4 + x] = (a1 >> (8 * x)) & 255; }
+        sm[i][8] = (int)__builtin_amdgcn_ubfe(d2, (uint32_t)xo * 8, 8);
+    }
+    // horizontal taps over row i, output column x: window columns x..x+5
+#define HT(i, x) tap6(sm[i][(x)], sm[i][(x) + 1], sm[i][(x) + 2], sm[i][(x) + 3], sm[i][(x) + 4], sm[i][(x) + 5])
+    int bh[4], bh1[4], hv[5], jj[4];
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        bh[x] = clip255((HT(2, x) + 16) >> 5);
+        bh1[x] = clip255((HT(3, x) + 16) >> 5);
+    }
+#pragma unroll
+    for (int x = 0; x < 5; x++)
+        hv[x] = clip255((tap6(sm[0][x + 2], sm[1][x + 2], sm[2][x + 2], sm[3][x + 2], sm[4][x + 2], sm[5][x + 2]) + 16) >> 5);
+#pragma unroll
+    for (int x = 0; x < 4; x++) jj[x] = 0;
+    if (need_j) {
+#pragma unroll
+        for (int x = 0; x < 4; x++) {
+            const int j1 = tap6(HT(0, x), HT(1, x), HT(2, x), HT(3, x), HT(4, x), HT(5, x));
+            jj[x] = clip255((j1 + 512) >> 10);
+        }
+    }
+#undef HT
+    const bool fy0 = fy == 0, fx0 = fx == 0, half = fx == 2 || fy == 2;
+#pragma unroll
+    for (int x = 0; x < 4; x++) {
+        const int G = sm[2][x + 2], Gx = sm[2][x + 3], Gy = sm[3][x + 2];
+        const int bs = fy == 3 ? bh1[x] : bh[x];
+        const int hs = fx == 3 ? hv[x + 1] : hv[x];
+        int A, B;
+        if (fx0 && fy0) { A = G; B = G; }
+        else if (fy0) { A = bh[x]; B = fx == 1 ? G : fx == 2 ? bh[x] : Gx; }
+        else if (fx0) { A = hv[x]; B = fy == 1 ? G : fy == 2 ? hv[x] : Gy; }
+        else if (half) { A = jj[x]; B = (fx == 2 && fy == 2) ? jj[x] : (fy == 2 ? hs : bs); }
+        else { A = bs; B = hs; }
+        out[x] = (A + B + 1) >> 1;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -408,7 +498,7 @@ __device__ __forceinline__ void stage_recs_load(const ReconArgs &a, int gmb, int
     v1 = rt[16 + (lane & 7)];
 }
 
-__device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint32_t *srec)
+__device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint32_t *srec, const Tabs &T)
 {
     const MbRec *Q = (const MbRec *)srec;
     const bool fl = Q->avail & DB_LEFT, ft = Q->avail & DB_TOP;
@@ -421,7 +511,8 @@ __device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint
     const int qpp = chroma ? PN->qpc : PN->qp, qq = chroma ? Q->qpc : Q->qp;
     const int qpav = (qpp + qq + 1) >> 1;
     const int ia = clip3(0, 51, qpav + Q->offA), ib = clip3(0, 51, qpav + Q->offB);
-    const uint32_t al = cAlpha[ia], be = cBeta[ib], t0 = cTc0[ia][0], t1 = cTc0[ia][1], t2 = cTc0[ia][2];
+    const uint32_t wa = tab_at(T.ab, ia), wb = tab_at(T.ab, ib), t2 = tab_at(T.c2, ia);
+    const uint32_t al = wa & 255, be = (wb >> 8) & 255, t0 = (wa >> 16) & 255, t1 = wa >> 24;
     // bS: lanes 0..31 = (dir, line segment kk, edge e)
     int bS = 0;
     {
@@ -456,6 +547,7 @@ __device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint
 struct McScratch {
     int32_t dc[24];
     uint32_t srec[72];               // deblocking record inputs: this MB's, left and top records
+    uint32_t coef[216];              // the MB's coded blocks (<= 27 x 32 B), staged by one coalesced load
     union {
         struct {                         // inter: reference windows
             uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
@@ -480,10 +572,13 @@ struct McScratch {
 // pre0/pre1: the staged-record words of this MB when has_pre (loaded one MB
 // ahead by the caller); next_mb >= 0: load the next MB's into pre0/pre1 once
 // this MB's are in LDS.
-template <bool PIPE, bool PROF = false>
+// PREP: the deblocking record and the residual were computed ahead by k_prep
+// (a.dbrec / a.res); they are loaded (issued after the reference windows)
+// instead of computed.
+template <bool PIPE, bool PROF = false, bool PREP = false>
 __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M, uint8_t *px, int16_t *res,
-                       uint8_t *db, unsigned long long *ph = nullptr, bool has_pre = false, uint32_t *pre = nullptr,
-                       int next_mb = -1)
+                       uint8_t *db, const Tabs &T, unsigned long long *ph = nullptr, bool has_pre = false,
+                       uint32_t *pre = nullptr, int next_mb = -1)
 {
     unsigned long long tp0 = PROF ? clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0;
     const PicDesc pd = a.pics[p];
@@ -503,12 +598,54 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
     const uint32_t rcbits = __builtin_amdgcn_readfirstlane(r.cbits);
     int16_t *s_res = res;
     uint8_t *s_out = px;
+    // the MB's coded blocks: issued first (before the reference windows), so
+    // that waiting for them (vmcnt retires in order) never waits for a window
+    const int ncw = (PREP || rtype == MBT_IPCM) ? 0 : __popc(rcbits & 0x7FFFFFFu) * 8;
+    const bool has_res = rtype != MBT_IPCM && rcbits != 0;
+    // PREP: this MB's k_prep outputs (loads issued where they are first needed)
+    const gcu8p pdb = uni(a.dbrec + (size_t)gmb * 64);
+    const gcu8p pres = uni(a.res + (size_t)gmb * 384);
+    auto load_prep = [&](uint32_t &dbw, uint32_t &r0, uint32_t &r1, uint32_t &r2) {
+        dbw = ldg32(pdb, (uint32_t)(lane & 15) * 4);
+        r0 = r1 = r2 = 0;
+        if (has_res) { r0 = ldg32(pres, lane * 4); r1 = ldg32(pres, 256 + lane * 4); r2 = ldg32(pres, 512 + lane * 4); }
+    };
+    auto store_prep = [&](uint32_t dbw, uint32_t r0, uint32_t r1, uint32_t r2, bool zero_res) {
+        if (lane < 16) ((uint32_t *)db)[lane] = dbw;
+        if (lane == 15 && (dbw >> 24)) atomicOr(a.err + p, 1u);        // k_prep's range-error byte
+        if (has_res || zero_res) {
+            ((uint32_t *)s_res)[lane] = r0; ((uint32_t *)s_res)[64 + lane] = r1; ((uint32_t *)s_res)[128 + lane] = r2;
+        }
+    };
+    uint32_t cq0 = 0, cq1 = 0, cq2 = 0, cq3 = 0;
+    {
+        const uint32_t *csrc = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + (uint32_t)__builtin_amdgcn_readfirstlane(r.coef)) * 16);
+        if (lane < ncw) cq0 = csrc[lane];
+        if (lane + 64 < ncw) cq1 = csrc[lane + 64];
+        if (lane + 128 < ncw) cq2 = csrc[lane + 128];
+        if (lane + 192 < ncw) cq3 = csrc[lane + 192];
+    }
+    auto stage_coef = [&]() {
+        if (lane < ncw) M.coef[lane] = cq0;
+        if (lane + 64 < ncw) M.coef[lane + 64] = cq1;
+        if (lane + 128 < ncw) M.coef[lane + 128] = cq2;
+        if (lane + 192 < ncw) M.coef[lane + 192] = cq3;
+        wave_sync();
+    };
 
+    if (PREP && rtype >= MBT_I4x4) {
+        uint32_t dbw, r0, r1, r2;
+        load_prep(dbw, r0, r1, r2);
+        store_prep(dbw, r0, r1, r2, false);
+        wave_sync();
+        return rtype;
+    }
     if (rtype >= MBT_I4x4) {
-        mb_dbrec(a, lane, db, M.srec);
+        mb_dbrec(a, lane, db, M.srec, T);
         if (rtype != MBT_IPCM && rcbits) {
             int e = 0;
-            mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
+            stage_coef();
+            mb_residual(r, (const int16_t *)M.coef, s_res, M.dc, lane, &e, T.ls);
             if (e && lane == 0) atomicOr(a.err + p, 1u);
         }
         return rtype;
@@ -595,13 +732,21 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         }
     }
 
-    mb_dbrec(a, lane, db, M.srec);
-    if (PROF) tp1 = clock64();
     int e = 0;
-    if (rcbits) {
-        mb_residual(r, a.coef + (size_t)pd.coef_base * 16, s_res, M.dc, lane, &e);
+    if (PREP) {
+        uint32_t dbw, r0, r1, r2;
+        load_prep(dbw, r0, r1, r2);
+        if (PROF) tp1 = clock64();
+        store_prep(dbw, r0, r1, r2, true);
     } else {
-        for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
+        mb_dbrec(a, lane, db, M.srec, T);
+        if (PROF) tp1 = clock64();
+        if (rcbits) {
+            stage_coef();
+            mb_residual(r, (const int16_t *)M.coef, s_res, M.dc, lane, &e, T.ls);
+        } else {
+            for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
+        }
     }
     if (PROF) tp2 = clock64();
 
@@ -648,7 +793,9 @@ __device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M
         const int b = lane >> 2, yy = lane & 3;
         const int mvx = r.mv[b][0], mvy = r.mv[b][1];
         int o[4];
-        luma_row4((const uint8_t *)&M.wraw[b][0][0] + M.wxo[b], yy, mvx & 3, mvy & 3, o);
+        const int fx = mvx & 3, fy = mvy & 3;
+        const bool need_j = __builtin_amdgcn_ballot_w64(fx != 0 && fy != 0 && (fx == 2 || fy == 2)) != 0;
+        luma_row4_reg(&M.wraw[b][yy], M.wxo[b], fx, fy, need_j, o);
         const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
 #pragma unroll
         for (int x = 0; x < 4; x++) s_out[by * 16 + bx + x] = (uint8_t)clip255(o[x] + s_res[by * 16 + bx + x]);
@@ -696,7 +843,8 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
     const int p = gidx / nmbs, mb = gidx - p * nmbs, lane = threadIdx.x;
     const PicDesc &pd = a.pics[p];
     const int gmb = pd.rec_base + mb;
-    const int type = mc_core<false>(a, p, mb, lane, M, s_px, s_res, s_db);
+    const Tabs T = load_tabs(lane);
+    const int type = mc_core<false>(a, p, mb, lane, M, s_px, s_res, s_db, T);
     if (lane < 16) ((uint32_t *)(a.dbrec + (size_t)gmb * 64))[lane] = ((const uint32_t *)s_db)[lane];
     if (type >= MBT_I4x4) {
         if (type != MBT_IPCM && a.rec[gmb].cbits) {
@@ -716,6 +864,69 @@ __global__ __launch_bounds__(64) void k_mb(ReconArgs a)
         const int comp = lane >> 4, row = (lane >> 1) & 7, q2 = lane & 1;
         uint8_t *cp = cur + (size_t)W16 * H16 + (size_t)comp * CW * CH;
         *(uint32_t *)(cp + (size_t)(mby * 8 + row) * CW + mbx * 8 + q2 * 4) = *(const uint32_t *)(s_px + 256 + comp * 64 + row * 8 + q2 * 4);
+    }
+}
+
+// k_prep: the per-MB work that does not depend on any reconstructed sample --
+// deblocking record (bS + thresholds) and residual (dequant + inverse
+// transforms) -- for every MB of a batch, fully parallel (four MBs per
+// workgroup, one wave each).  Runs on its own stream one batch ahead of k_wg,
+// filling the GPU beside the latency-bound row chain; k_wg's MC waves then
+// only load its outputs.  Outputs: a.dbrec (64 B per MB; byte 63 = residual
+// range error, a byte no consumer reads otherwise), a.res (384 x int16, for
+// MBs with coded blocks).
+__global__ __launch_bounds__(256) void k_prep(ReconArgs a)
+{
+    __shared__ McScratch M[4];
+    __shared__ int16_t s_res[4][384];
+    __shared__ uint8_t s_db[4][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nmbs = a.w * a.h;
+    const int gidx = blockIdx.x * 4 + wv;
+    if (gidx >= a.npics * nmbs) return;            // wave-uniform; no workgroup barrier follows
+    const int p = gidx / nmbs, mb = gidx - p * nmbs;
+    const PicDesc &pd = a.pics[p];
+    const int gmb = pd.rec_base + mb;
+    McScratch &Mw = M[wv];
+    const Tabs T = load_tabs(lane);
+    {
+        uint32_t v0, v1;
+        stage_recs_load(a, gmb, mb % a.w, mb / a.w, lane, v0, v1);
+        Mw.srec[lane] = v0;
+        if (lane < 8) Mw.srec[64 + lane] = v1;
+    }
+    wave_sync();
+    const MbRec &r = *(const MbRec *)Mw.srec;
+    const int rtype = __builtin_amdgcn_readfirstlane(r.type);
+    const uint32_t rcbits = __builtin_amdgcn_readfirstlane(r.cbits);
+    const bool has_res = rtype != MBT_IPCM && rcbits != 0;
+    const int ncw = has_res ? __popc(rcbits & 0x7FFFFFFu) * 8 : 0;
+    uint32_t cq0 = 0, cq1 = 0, cq2 = 0, cq3 = 0;
+    {
+        const uint32_t *csrc = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + (uint32_t)__builtin_amdgcn_readfirstlane(r.coef)) * 16);
+        if (lane < ncw) cq0 = csrc[lane];
+        if (lane + 64 < ncw) cq1 = csrc[lane + 64];
+        if (lane + 128 < ncw) cq2 = csrc[lane + 128];
+        if (lane + 192 < ncw) cq3 = csrc[lane + 192];
+    }
+    mb_dbrec(a, lane, s_db[wv], Mw.srec, T);
+    int e = 0;
+    if (has_res) {
+        if (lane < ncw) Mw.coef[lane] = cq0;
+        if (lane + 64 < ncw) Mw.coef[lane + 64] = cq1;
+        if (lane + 128 < ncw) Mw.coef[lane + 128] = cq2;
+        if (lane + 192 < ncw) Mw.coef[lane + 192] = cq3;
+        wave_sync();
+        mb_residual(r, (const int16_t *)Mw.coef, s_res[wv], Mw.dc, lane, &e, T.ls);
+        const uint32_t *src = (const uint32_t *)s_res[wv];
+        uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
+        dst[lane] = src[lane]; dst[64 + lane] = src[64 + lane]; dst[128 + lane] = src[128 + lane];
+    }
+    const int any_e = __builtin_amdgcn_ballot_w64(e != 0) != 0;
+    if (lane < 16) {
+        uint32_t w = ((const uint32_t *)s_db[wv])[lane];
+        if (lane == 15) w = (w & 0x00FFFFFFu) | (any_e ? 0x01000000u : 0u);
+        ((uint32_t *)(a.dbrec + (size_t)gmb * 64))[lane] = w;
     }
 }
 
@@ -1032,8 +1243,14 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, const int b
 // direction, so no cross-lane ordering is needed inside a direction.  Lanes
 // 32..63 mirror lanes 0..31 (same addresses, same values) so that every
 // access is unconditional.
+struct NoMid { __device__ __forceinline__ void operator()() const {} };
+// Mid (dir 0): called once the MB edge (edge 0) is filtered and its samples
+// (region cols -4..-1, the left MB's cols 12..15, now final) are written back
+// -- the row hand-off publishes from there without waiting for the internal
+// edges (edges 1..3 touch only this MB's columns 1..14)
+template <class Mid = NoMid>
 __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, uint8_t *ry, uint8_t *ru, uint8_t *rv,
-                                            uint8_t *junk, int lane, bool mb_edge_on)
+                                            uint8_t *junk, int lane, bool mb_edge_on, const Mid &mid = Mid())
 {
     const int li = lane & 31;
     const bool chroma = li >= 16;
@@ -1075,6 +1292,14 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
         if (__builtin_amdgcn_ballot_w64(b != 0) != 0)     // wave-uniform skip
             filt_line<true>(v, 0, b, alpha_e, beta_e, chroma ? 0 : beta_e, tcs_e);
     }
+    if (dir == 0) {
+        // cols -4..-1 are final after the MB edge: write them back now, then
+        // let the caller publish
+        uint32_t *row = (uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
+        row[0] = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+        wave_sync();
+        mid();
+    }
 #pragma unroll
     for (int k = 1; k < 4; k++) {
         const int b = (int)((bsw >> (4 * k)) & 15);
@@ -1087,7 +1312,7 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
         uint32_t *row = (uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
         uint32_t *jk = (uint32_t *)(junk + lane * 4);
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
+        for (int j = 1; j < 5; j++) {
             const uint32_t w = (uint32_t)v[4 * j] | ((uint32_t)v[4 * j + 1] << 8) | ((uint32_t)v[4 * j + 2] << 16) | ((uint32_t)v[4 * j + 3] << 24);
             *((!chroma || j < 3) ? row + j : jk) = w;
         }
@@ -1399,16 +1624,12 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             st_gran(has_down ? mbx_me + (size_t)c * 32 + 24 + (li & 7) : sink, unf, tag);
         }
         if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
-        // ---- vertical edges (need only this row's samples)
-        if (dbf) {
-            deblock_dir(0, L.db, L.ry, L.ru, L.rv, L.junk, lane, avail & DB_LEFT);
-            wave_sync();
-        }
-        if (prof) { tc1 = clock64(); pt[1] += tc1 - tc0; tc0 = tc1; }
-
-        // ---- hand-off: the final rows of MB c-1 (entry dwords 0..23) are
-        //      final now -- only this MB's vertical edges touch its columns 13..15
-        {
+        // ---- vertical edges (need only this row's samples), with the
+        //      hand-off in between: the final rows of MB c-1 (entry dwords
+        //      0..23) are final once this MB's left edge is filtered -- the
+        //      internal edges never touch MB c-1 -- so they go to the row
+        //      below before the internal edges run
+        auto publish = [&]() {
             const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
             const uint32_t patch = le < 16 ? *(const uint32_t *)&L.ry[(16 + (le >> 2)) * RY_S]
                                            : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
@@ -1416,8 +1637,11 @@ __device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, 
             const uint32_t ent = is_patch ? patch : prov;
             st_gran(has_down && c > 0 ? mbx_me + (size_t)(c - 1) * 32 + le : sink, ent, tag);
             if (prof && lane == 0) pmb[2] = wall_clock64();
-        }
-        if (prof) { tc1 = clock64(); pt[3] += tc1 - tc0; tc0 = tc1; }
+        };
+        if (dbf) deblock_dir(0, L.db, L.ry, L.ru, L.rv, L.junk, lane, avail & DB_LEFT, publish);
+        else publish();
+        wave_sync();
+        if (prof) { tc1 = clock64(); pt[1] += tc1 - tc0; tc0 = tc1; }
 
         // ---- top halo, horizontal edges
         if (has_up) {
@@ -1614,7 +1838,7 @@ __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const uns
     wave_sync();
 }
 
-template <bool PIPE, int NMC, bool PROF>
+template <bool PIPE, int NMC, bool PROF, bool PREP = false>
 __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
 {
     __shared__ RowLds L;
@@ -1638,6 +1862,7 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
         return;
     }
     McScratch &Mw = M[wid - 1];
+    const Tabs T = load_tabs(lane);
     uint32_t pre[2] = {0, 0};
     bool has_pre = false;
     for (int c = wid - 1; c < a.w; c += NMC) {
@@ -1652,7 +1877,7 @@ __global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
         }
         const unsigned long long t0 = PROF ? clock64() : 0;
         unsigned long long ph = 0;
-        const int type = mc_core<PIPE, PROF>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], &ph,
+        const int type = mc_core<PIPE, PROF, PREP>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], T, &ph,
                                              has_pre, pre, c + NMC < a.w ? r * a.w + c + NMC : -1);
         has_pre = true;
         if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 1] = ph;
@@ -1685,5 +1910,370 @@ template __global__ void k_wg<false, 3, true>(ReconArgs);
 template __global__ void k_wg<true, 2, false>(ReconArgs);
 template __global__ void k_wg<true, 3, false>(ReconArgs);
 template __global__ void k_wg<true, 4, false>(ReconArgs);
+template __global__ void k_wg<false, 2, false, true>(ReconArgs);
+template __global__ void k_wg<false, 3, false, true>(ReconArgs);
+template __global__ void k_wg<false, 3, true, true>(ReconArgs);
 template __global__ void k_rows<false>(ReconArgs);
 template __global__ void k_rows<true>(ReconArgs);
+
+// ---------------------------------------------------------------------------
+// k_wgpp: k_wg with TWO row-unit waves per MB row, ping-pong: wave w
+// deblocks the MBs c with c % 2 == w.  The deblocking chain along a row is
+// strictly sequential (V(c) reads MB c-1's columns 12..15 after H(c-1); H(c)
+// follows V(c)), but each MB also carries work off that chain: taking its
+// samples and deblocking record out of the MC ring, the speculative
+// row-above read, the frame stores, the provisional mailbox entry.  With two
+// waves, MB c+1's wave does its off-chain part while MB c's wave runs the
+// chain, so the row advances at the chain's pace (copy + V + top + H) rather
+// than at the pace of everything one wave does per MB.
+//
+// Each wave owns one LDS region (the MB's samples with a 4-column left and
+// 4-row top halo) used for its MBs in turn.  Hand-offs (LDS flags, both
+// monotonic):
+//   hdone  = c + 1  once H(c) is done: MB c's region holds its final columns
+//                   12..15 for V(c+1), and its rows 12..15 (provisional
+//                   mailbox entry, columns 0..11 final)
+//   copied = c + 1  once MB c+1's wave has read both: MB c's region is free
+// The row hand-off to the row below (mailbox granules) and the frame stores
+// are exactly those of row_unit (each sample stored once, by the MB that
+// finalises it).  Reference: h264bsdFilterPicture (deblocking.c:574-639),
+// filter order per MB vertical then horizontal edges (:603-637).
+// ---------------------------------------------------------------------------
+struct __attribute__((aligned(16))) PPRegion {
+    uint8_t db[64];
+    uint8_t ry[20 * RY_S];      // rows -4..15, cols -4..15
+    uint8_t ru[10 * RC_S];      // rows -2..7, cols -4..7
+    uint8_t rv[10 * RC_S];
+};
+struct __attribute__((aligned(16))) PPLds {
+    PPRegion G[2];
+    uint8_t junk[2][256];
+    int hdone, copied, pdone;
+    uint32_t i4tab[9 * 16];
+    unsigned long long ptw1[8];     // PROF: wave 1's phase sums, added by wave 0
+};
+
+template <bool PROF>
+__device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing *R)
+{
+    const int W = a.w, H = a.h;
+    const PicDesc *pdp = a.pics + p;
+    const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
+    const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
+    const int W16 = W * 16, H16 = H * 16, CW = W16 / 2, CH = H16 / 2;
+    uint8_t *cur = a.frames + (unsigned long long)fslot * a.frame_bytes;
+    uint8_t *curU = cur + (size_t)W16 * H16;
+    unsigned *perr = a.err + p;
+    const uint32_t tag = a.epoch;
+    const bool has_up = r > 0, has_down = r + 1 < H;
+    const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
+    unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
+    const bool last_row = r == H - 1;
+    typedef const __attribute__((address_space(4))) uint32_t *cu32p;
+    const cu32p recw = (cu32p)(const void *)(a.rec + rec_base + r * W);   // 24 dwords per record
+    PPRegion &G = L.G[w];
+    const PPRegion &Gp = L.G[w ^ 1];
+    uint8_t *const junk = L.junk[w];
+    uint8_t *const Lb = (uint8_t *)&G;
+
+    const int orow = lane >> 2, oq = lane & 3;                                   // luma 16x16 dwords
+    const int li = lane & 31;
+    const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;          // chroma dwords (32..63 mirror)
+    const int le = li < 24 ? li : li - 8;                                        // mailbox entry dword
+    uint8_t *const ybase = cur + (size_t)r * 16 * W16;
+    uint8_t *const cbase = curU + (size_t)r * 8 * CW;
+    const uint32_t yoff = (uint32_t)(orow * W16 + oq * 4);
+    const uint32_t coff = (uint32_t)(ccomp * CW * CH + crow * CW + cq * 4);
+    // common-case frame store maps (as row_unit): offsets in the region /
+    // relative to (row r*16-4 | r*8-2, col -4) of MB c
+    uint32_t sa_lds, sa_glb, sb_lds, sb_glb;
+    bool sa_left, sa_top, sb_left, sb_top;
+    {
+        const int Lry = (int)(G.ry - Lb), Lru = (int)(G.ru - Lb), Lrv = (int)(G.rv - Lb);
+        int row, col;
+        if (lane < 36) { row = lane / 3; col = (lane % 3) * 4; }
+        else if (lane < 48) { row = lane - 36; col = -4; }
+        else { row = -4 + ((lane - 48) >> 2); col = ((lane - 48) & 3) * 4; }
+        sa_lds = (uint32_t)(Lry + (row + 4) * RY_S + 4 + col);
+        sa_glb = (uint32_t)((row + 4) * W16 + col + 4);
+        sa_left = lane >= 36 && lane < 48;
+        sa_top = lane >= 48;
+        int comp;
+        const int k = lane & 31;
+        if (k < 12) { comp = k / 6; row = k % 6; col = 0; }
+        else if (k < 24) { comp = (k - 12) / 6; row = (k - 12) % 6; col = -4; }
+        else { comp = (k - 24) >> 2; row = -2 + (((k - 24) >> 1) & 1); col = ((k - 24) & 1) * 4; }
+        sb_lds = (uint32_t)((comp ? Lrv : Lru) + (row + 2) * RC_S + 4 + col);
+        sb_glb = (uint32_t)(comp * CW * CH + (row + 2) * CW + col + 4);
+        sb_left = k >= 12 && k < 24;
+        sb_top = k >= 24;
+    }
+    // left-halo copy from the partner's region: lanes 0..15 luma rows, 16..31
+    // chroma rows (cols 12..15 / 4..7 -> -4..-1); lanes 32..63 into junk
+    uint32_t cp_src, cp_dst;
+    {
+        int off, step;
+        const uint8_t *D;
+        if (lane < 16) { D = Gp.ry; off = (lane + 4) * RY_S; step = 16; }
+        else { const int k = (lane - 16) & 15; D = (k >> 3) ? Gp.rv : Gp.ru; off = ((k & 7) + 2) * RC_S; step = 8; }
+        cp_src = (uint32_t)((int)(D - (const uint8_t *)&Gp) + off + step);
+        cp_dst = lane < 32 ? (uint32_t)((int)(D - (const uint8_t *)&Gp) + off) : (uint32_t)((int)(junk - Lb) + lane * 4);
+    }
+    // provisional entry dword of this lane (rows 12..15 of an MB's region, cols 0..15)
+    uint32_t prov_off;
+    {
+        const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
+        prov_off = le < 16 ? (uint32_t)((int)(G.ry - Lb) + (16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4)
+                           : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 4 + qq * 4);
+    }
+    // patch dword (cols -4..-1 of rows 12..15 / 6..7 of the current region)
+    uint32_t patch_off;
+    bool is_patch;
+    {
+        const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
+        patch_off = le < 16 ? (uint32_t)((int)(G.ry - Lb) + (16 + (le >> 2)) * RY_S)
+                            : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S);
+        is_patch = le < 16 ? (le & 3) == 3 : qq;
+    }
+    // own samples from the ring slot: luma all lanes, chroma lanes 0..31
+    const uint32_t own_y_lds = (uint32_t)((int)(G.ry - Lb) + (orow + 4) * RY_S + 4 + oq * 4);
+    const uint32_t own_c_lds = lane < 32 ? (uint32_t)((int)((ccomp ? G.rv : G.ru) - Lb) + (crow + 2) * RC_S + 4 + cq * 4)
+                                         : (uint32_t)((int)(junk - Lb) + lane * 4);
+    const uint32_t db_lds = lane < 16 ? (uint32_t)(lane * 4) : (uint32_t)((int)(junk - Lb) + lane * 4);
+    // top halo lanes 0..23: entry dword lane -> region rows 0..3 / chroma rows 0..1
+    uint32_t top_lds;
+    {
+        const int k = lane - 16, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
+        top_lds = lane < 16 ? (uint32_t)((int)(G.ry - Lb) + orow * RY_S + 4 + oq * 4)
+                : lane < 24 ? (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + row * RC_S + 4 + qq * 4)
+                            : (uint32_t)((int)(junk - Lb) + lane * 4);
+    }
+    unsigned long long *const sink = a.gjunk + ((p * H + r) & 127) * 64 + lane;
+
+    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool prof = PROF && a.prof != nullptr;
+    unsigned long long tc0 = 0, tc1;
+#define PPT(i) do { if (prof) { tc1 = clock64(); pt[i] += tc1 - tc0; tc0 = tc1; } } while (0)
+    if (prof && w == 0 && lane == 0) a.prof[((size_t)r * a.npics + p) * 16] = wall_clock64();
+
+    for (int c = w; c < W; c += 2) {
+        if (prof) tc0 = clock64();
+        // per-MB stamps: [0] row-above entry c in hand (H(c) may start), [2] entry c-1 published
+        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
+        const cu32p rw = recw + c * 24;
+        const uint32_t h0 = rw[0];
+        const int avail = (h0 >> 24) & 255;
+        const bool dbf = avail & DB_INNER;
+        // speculative read of the row above's entry c (lanes 0..23 used)
+        const unsigned long long *tga = mbx_up + c * 32 + (lane < 24 ? lane : (lane & 15));
+        unsigned long long gr = ld_gran(tga);
+        // ---- off the chain: my region is free once MB c-1's wave read MB c-2's
+        {
+            unsigned spins = 0;
+            while (c >= 2 && __builtin_amdgcn_readfirstlane(lds_ld(&L.copied)) < c - 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
+            }
+        }
+        PPT(6);
+        const int slot = c & (RING_K - 1);
+        {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
+            }
+        }
+        wave_sync();
+        PPT(7);
+        {
+            const uint32_t oy = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
+            const uint32_t oc = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
+            const uint32_t od = ((const uint32_t *)R->db[slot])[lane & 15];
+            *(uint32_t *)(Lb + own_y_lds) = oy;
+            *(uint32_t *)(Lb + own_c_lds) = oc;
+            *(uint32_t *)(Lb + db_lds) = od;
+        }
+        PPT(0);
+        // ---- the chain: MB c-1's H pass done -> its columns 12..15 and rows 12..15
+        uint32_t prov = 0;
+        if (c > 0) {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&L.hdone)) < c) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
+            }
+            wave_sync();
+            PPT(3);
+            const uint32_t hv = *(const uint32_t *)((const uint8_t *)&Gp + cp_src);
+            prov = *(const uint32_t *)((const uint8_t *)&Gp + prov_off);
+            *(uint32_t *)(Lb + cp_dst) = hv;
+            wave_sync();
+            if (lane == 0) { lds_st(&L.copied, c); lds_st(&R->consumed, c); }
+        } else {
+            wave_sync();
+            if (lane == 0) lds_st(&R->consumed, 0);
+        }
+        // ---- vertical edges; MB c-1's final rows go to the row below right
+        //      after this MB's left edge
+        auto publish = [&]() {
+            const uint32_t patch = *(const uint32_t *)(Lb + patch_off);
+            const uint32_t ent = is_patch ? patch : prov;
+            st_gran(has_down && c > 0 ? mbx_me + (size_t)(c - 1) * 32 + le : sink, ent, tag);
+            if (prof && lane == 0) pmb[2] = wall_clock64();
+        };
+        if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT, publish);
+        else publish();
+        wave_sync();
+        PPT(1);
+        // ---- top halo (row above's entry c final), horizontal edges
+        if (has_up) {
+            unsigned spins = 0;
+            const bool mine = lane < 24;
+            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }
+                if (mine) gr = ld_gran(tga);
+            }
+            *(uint32_t *)(Lb + top_lds) = (uint32_t)gr;
+            wave_sync();
+        }
+        if (prof && lane == 0) pmb[0] = wall_clock64();
+        PPT(5);
+        if (dbf) {
+            deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_TOP);
+            wave_sync();
+        }
+        if (lane == 0) lds_st(&L.hdone, c + 1);
+        PPT(2);
+        // ---- off the chain again: frame stores, once per sample
+        if (!last_row && c != W - 1) {
+            const uint32_t va = *(const uint32_t *)(Lb + sa_lds);
+            const uint32_t vb = *(const uint32_t *)(Lb + sb_lds);
+            uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
+            uint8_t *const cb = cbase + c * 8 - 2 * CW - 4;
+            const bool oka = (!sa_left || c > 0) && (!sa_top || has_up);
+            const bool okb = (!sb_left || c > 0) && (!sb_top || has_up);
+            st32<false>(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
+            st32<false>(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
+        } else {
+            const int yrows = last_row ? 16 : 12;
+            const int crows = last_row ? 8 : 6;
+            const bool last_col = c == W - 1;
+            if (orow < yrows && (oq < 3 || last_col))
+                st32<false>(ybase + c * 16 + yoff, *(const uint32_t *)&G.ry[(orow + 4) * RY_S + 4 + oq * 4]);
+            if (lane < 32 && crow < crows && (cq == 0 || last_col))
+                st32<false>(cbase + c * 8 + coff, *(const uint32_t *)&(ccomp ? G.rv : G.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
+            if (c > 0) {
+                if (lane < 16) {
+                    if (lane < yrows)
+                        st32<false>(ybase + c * 16 - 4 + lane * W16, *(const uint32_t *)&G.ry[(lane + 4) * RY_S]);
+                } else if (lane < 32) {
+                    const int k = lane - 16, comp = k >> 3, row = k & 7;
+                    if (row < crows)
+                        st32<false>(cbase + c * 8 - 4 + comp * CW * CH + row * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[(row + 2) * RC_S]);
+                }
+            }
+            if (has_up) {
+                if (lane >= 32 && lane < 48) {
+                    const int k = lane - 32;
+                    st32<false>(ybase + c * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&G.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
+                } else if (lane >= 48 && lane < 56) {
+                    const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
+                    st32<false>(cbase + c * 8 + qq * 4 + comp * CW * CH + (row - 2) * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[row * RC_S + 4 + qq * 4]);
+                }
+            }
+            // the row's last entry is final as it stands (no right neighbour)
+            if (last_col && has_down && lane < 24)
+                st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, *(const uint32_t *)(Lb + prov_off), tag);
+        }
+        wave_sync();
+        PPT(4);
+    }
+    if (prof) {
+        unsigned long long *o = a.prof + ((size_t)r * a.npics + p) * 16;
+        if (lane == 0 && ((W - 1) & 1) == w) o[1] = wall_clock64();
+        if (w == 1) {
+            if (lane == 0) {
+                for (int i = 0; i < 8; i++) L.ptw1[i] = pt[i];
+                wave_sync();
+                lds_st(&L.pdone, 1);
+            }
+        } else {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&L.pdone)) == 0 && ++spins < (1u << 22)) __builtin_amdgcn_s_sleep(1);
+            wave_sync();
+            if (lane == 0)
+                for (int i = 0; i < 8; i++) o[2 + i] = pt[i] + L.ptw1[i];
+        }
+    }
+#undef PPT
+}
+
+template <int NMC, bool PROF, bool PREP>
+__global__ __launch_bounds__(64 * (NMC + 2)) void k_wgpp(ReconArgs a)
+{
+    __shared__ PPLds L;
+    __shared__ McScratch M[NMC];
+    __shared__ MbRing R;
+    const int S = a.S;
+    const int pair = blockIdx.x / S, s = blockIdx.x - pair * S;
+    const uint32_t kr = a.order[pair];
+    const int k = (int)(kr >> 16), r = (int)(kr & 0xFFFF);
+    const int p = k * S + s;
+    if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
+    if (threadIdx.x == 0) { R.consumed = 0; L.hdone = 0; L.copied = 0; L.pdone = 0; }
+    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2)) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
+    __syncthreads();
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wid < 2) {
+        __builtin_amdgcn_s_setprio(3);
+        row_pp<PROF>(a, p, r, L, wid, lane, &R);
+        return;
+    }
+    McScratch &Mw = M[wid - 2];
+    const Tabs T = load_tabs(lane);
+    uint32_t pre[2] = {0, 0};
+    bool has_pre = false;
+    for (int c = wid - 2; c < a.w; c += NMC) {
+        const int slot = c & (RING_K - 1);
+        if (c >= RING_K) {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RING_K + 1) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }
+            }
+            wave_sync();
+        }
+        const unsigned long long t0 = PROF ? clock64() : 0;
+        unsigned long long ph = 0;
+        const int type = mc_core<false, PROF, PREP>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], T, &ph,
+                                              has_pre, pre, c + NMC < a.w ? r * a.w + c + NMC : -1);
+        has_pre = true;
+        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 1] = ph;
+        if (type == MBT_IPCM) {
+            const PicDesc &pd = a.pics[p];
+            const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
+            ((uint32_t *)R.px[slot])[lane] = src[lane];
+            if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
+        } else if (type >= MBT_I4x4) {
+            const PicDesc &pd = a.pics[p];
+            mc_intra(a.rec + pd.rec_base + r * a.w + c, a.mbx + ((size_t)p * a.h + (r > 0 ? r - 1 : 0)) * a.w * 32,
+                     a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, L.i4tab);
+        }
+        wave_sync();
+        {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
+            const int kk = lane & 7;
+            const uint8_t *px = R.px[slot];
+            const uint32_t v = *(const uint32_t *)&px[kk < 4 ? 240 + kk * 4 : kk < 6 ? 312 + (kk - 4) * 4 : 376 + (kk - 6) * 4];
+            if (r + 1 < a.h)
+                st_gran(a.mbx + ((size_t)p * a.h + r) * a.w * 32 + c * 32 + 24 + kk, v, a.epoch);
+        }
+        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
+        if (lane == 0) lds_st(&R.flag[slot], c + 1);
+    }
+}
+template __global__ void k_wgpp<2, false, true>(ReconArgs);
+template __global__ void k_wgpp<3, false, true>(ReconArgs);
+template __global__ void k_wgpp<2, true, true>(ReconArgs);
+template __global__ void k_wgpp<3, true, true>(ReconArgs);

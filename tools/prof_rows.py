@@ -67,3 +67,17 @@ for r in range(0, h, 4):
     d = "" if prev is None else f"{(ts[2] - prev) / 4:.2f}/row"
     print(f"r{r:02d} " + " ".join(f"{x:7.1f}" for x in ts) + "  " + d)
     prev = ts[2]
+
+# k_wgpp hand-off latency: row r's arrival of entry c (stamp 0) minus row r-1's
+# publish of entry c (stamp 2 of its MB c+1), deep rows, picture 0 of the last batch
+if os.environ.get("H264MI_WG_PP", "1") != "0":
+    d = []
+    for r in range(20, h):
+        for c in range(4, w - 2):
+            d.append(m[0, r, c, 0] - m[0, r - 1, c + 1, 2])
+    d = np.array(d)
+    print("hand-off arrival-publish (us): min %.2f p10 %.2f p50 %.2f p90 %.2f" % (d.min(), np.percentile(d, 10), np.percentile(d, 50), np.percentile(d, 90)))
+    per = np.diff(m[0, 40, :, 0])
+    print("row 40 H-start period (us): p10 %.2f p50 %.2f p90 %.2f" % (np.percentile(per, 10), np.percentile(per, 50), np.percentile(per, 90)))
+    pubs = m[0, 40, 1:, 2] - m[0, 40, :-1, 0]
+    print("row 40 H(c) start -> publish(c) (us): p10 %.2f p50 %.2f p90 %.2f" % (np.percentile(pubs, 10), np.percentile(pubs, 50), np.percentile(pubs, 90)))
