@@ -81,3 +81,6 @@ if os.environ.get("H264MI_WG_PP", "1") != "0":
     print("row 40 H-start period (us): p10 %.2f p50 %.2f p90 %.2f" % (np.percentile(per, 10), np.percentile(per, 50), np.percentile(per, 90)))
     pubs = m[0, 40, 1:, 2] - m[0, 40, :-1, 0]
     print("row 40 H(c) start -> publish(c) (us): p10 %.2f p50 %.2f p90 %.2f" % (np.percentile(pubs, 10), np.percentile(pubs, 50), np.percentile(pubs, 90)))
+    a2 = np.frombuffer(buf, dtype=np.uint64)[:S * h * 16].reshape(h, S, 16).astype(np.float64)
+    print("chain H end -> publish (cycles/MB): row0 %.0f row40 %.0f" % (a2[0, :, 10].mean() / w, a2[40, :, 10].mean() / w))
+    print("chain H end -> V start (cycles/MB): row0 %.0f row40 %.0f" % (a2[0, :, 11].mean() / w, a2[40, :, 11].mean() / w))
