@@ -2565,7 +2565,8 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
             for (int k = 0; k < 3; k++) {
                 const int y = clip3(0, H16 - 1, l_y0 + min(lsub + 4 * k, 8));
                 const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + L.l_ax);
-                L.lw[k][0] = src[0]; L.lw[k][1] = src[1]; L.lw[k][2] = src[2];
+                const uint3 t = *(const uint3 *)src;         // one dwordx3 load (4-byte aligned)
+                L.lw[k][0] = t.x; L.lw[k][1] = t.y; L.lw[k][2] = t.z;
             }
         }
         const int cb = (lane & 31) >> 1, ccomp = lane & 1;
@@ -2581,13 +2582,18 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
             for (int wy = 0; wy < 3; wy++) {
                 const int y = clip3(0, CH - 1, c_y0 + wy);
                 const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + L.c_ax);
-                L.cw[wy][0] = src[0]; L.cw[wy][1] = src[1];
+                uint2 t;
+                __builtin_memcpy(&t, src, 8);                 // one dwordx2 load (4-byte aligned)
+                L.cw[wy][0] = t.x; L.cw[wy][1] = t.y;
             }
         }
     }
     L.dbw = ldg32(pdb, (uint32_t)(lane & 15) * 4);
     L.r0 = L.r1 = L.r2 = 0;
-    if (has_res) { L.r0 = ldg32(pres, lane * 4); L.r1 = ldg32(pres, 256 + lane * 4); L.r2 = ldg32(pres, 512 + lane * 4); }
+    if (has_res) {      // residual dwords 3*lane .. 3*lane+2: one dwordx3 load
+        const uint3 t = *(const uint3 *)(a.res + (size_t)gmb * 384 + lane * 6);
+        L.r0 = t.x; L.r1 = t.y; L.r2 = t.z;
+    }
 }
 
 // returns the MB type; inter MBs end with their samples in px
@@ -2601,7 +2607,8 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     if (lane < 16) ((uint32_t *)db)[lane] = L.dbw;
     if (lane == 15 && (L.dbw >> 24)) atomicOr(a.err + p, 1u);        // k_prep's range-error byte
     if (has_res || rtype < MBT_I4x4) {
-        ((uint32_t *)s_res)[lane] = L.r0; ((uint32_t *)s_res)[64 + lane] = L.r1; ((uint32_t *)s_res)[128 + lane] = L.r2;
+        uint32_t *d = (uint32_t *)s_res + 3 * lane;
+        d[0] = L.r0; d[1] = L.r1; d[2] = L.r2;
     }
     if (rtype >= MBT_I4x4) { wave_sync(); return rtype; }
     const int W16 = a.w * 16, CW = W16 / 2;
