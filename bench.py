@@ -10,11 +10,18 @@ libh264mi.so) and the batches are uploaded to HBM before timing, so the timed
 region is the reconstruction hot path only (kernel-only fps).
 
 A *step* = one picture of each of the rank's 8 streams reconstructed on the
-GPU: k_mb (every MB in parallel: residual, 6-tap/bilinear motion compensation
-of inter MBs, deblocking records) followed by k_rows (one wave per MB row:
-intra prediction and in-loop deblocking, rows pipelined through HBM
-mailboxes).  Steps follow decoding order, so the W warmup steps decode the
-first W pictures and the K timed steps the next K.
+GPU by two kernels on two HIP streams:
+  k_prep  every MB in parallel: deblocking record (bS + thresholds) and
+          residual (dequant + inverse transforms); it depends on no
+          reconstructed sample, so step t+1's k_prep runs beside step t's
+          row kernel;
+  k_wgpp  one workgroup per (picture, MB row): two MC waves (6-tap luma /
+          bilinear chroma MC, intra prediction, clip-add) feed an LDS ring,
+          two ping-pong row waves run the in-loop deblocking chain; rows hand
+          off through tagged-granule mailboxes.
+Steps follow decoding order, so the W warmup steps decode the first W
+pictures and the K timed steps the next K.  (H264MI_KERNEL=classic selects
+the earlier k_mb + k_rows pair, H264MI_WG_PP=0 the one-row-wave k_wg.)
 
 Bit-exactness: rank 0 checks the frames still resident in stream 0's slots
 against the reference decoder's per-frame MD5s (tests/golden/golden.json,
@@ -362,8 +369,10 @@ def main():
     # bytes; the G groups' launches run concurrently (aggregate: wall_read_GBs)
     launch_bytes = per_step_bytes / G
     mb_us_avg, rows_us_avg = mb_us / max(nb, 1), rows_us / max(nb, 1)
-    # k_wg: the first timing slot spans only the error-flag reset before the launch
+    # single-launch kernels (k_wgpp / k_wg): the first timing slot spans only
+    # the wait for k_prep and the error-flag reset before the launch
     step_us = mb_us_avg + rows_us_avg if classic else rows_us_avg
+    kname = eng.kernel_name() or ("k_mb+k_rows" if classic else "k_wg")
     achieved = launch_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
     kmb_alg, n_inter = inter_alg_bytes(caps, a.warmup * P, (a.warmup + a.steps) * P)
     kmb_alg /= G
@@ -402,7 +411,7 @@ def main():
                        "parallelism": f"streams sharded {S}/GPU, no collective; "
                                       f"{P} consecutive pictures per stream overlapped per launch; "
                                       f"{G} picture groups on separate HIP streams"},
-            "roofline": {"kernel": ("k_wg (one launch = one step)" if not classic
+            "roofline": {"kernel": (f"{kname} (one launch = one step; k_prep of the next step runs beside it)" if not classic
                                     else f"k_mb+k_rows of one picture group ({S // G} pictures; "
                                          f"{G} groups run concurrently)"), "bound": "hbm",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -412,10 +421,10 @@ def main():
                          "avg_launch_kernel_us": round(step_us, 2),
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
-            "kernels": ({"k_wg": {"avg_launch_us": round(rows_us_avg, 2),
-                                  "pictures_per_launch": S * P, "frame_slot_ring": ring or None,
-                                  "row_lag_max": max(lags) if lags else None,
-                                  "bound": "latency (MB-row dependency chain); MC waves overlap it"}}
+            "kernels": ({kname: {"avg_launch_us": round(rows_us_avg, 2),
+                                 "pictures_per_launch": S * P, "frame_slot_ring": ring or None,
+                                 "row_lag_max": max(lags) if lags else None,
+                                 "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}}
                         if not classic else
                         {"k_mb": {"avg_launch_us": round(mb_us_avg, 2),
                                   "alg_bytes_per_launch": int(kmb_alg / a.steps),

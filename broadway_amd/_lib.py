@@ -146,6 +146,8 @@ def mi() -> C.CDLL:
     L.h264mi_engine_read.restype = i32
     L.h264mi_engine_sync.argtypes = [vp]
     L.h264mi_engine_sync.restype = i32
+    L.h264mi_engine_kernel.argtypes = [vp]
+    L.h264mi_engine_kernel.restype = C.c_char_p
     L.h264mi_engine_errors.argtypes = [vp]
     L.h264mi_engine_errors.restype = u32
     L.h264mi_engine_last_timing.argtypes = [vp, C.POINTER(C.c_float)]

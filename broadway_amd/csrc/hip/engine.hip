@@ -35,6 +35,7 @@ struct h264mi_engine {
     int classic;                  // single-picture launches: k_wg (default) or k_mb + k_rows (H264MI_KERNEL=classic)
     int wg_nmc;                   // MC waves per k_wg workgroup (H264MI_WG_NMC: 2, 3 or 4)
     int wg_ch;                    // single-picture k_wg launches: chain + helper row waves (k_wgch; H264MI_WG_CH=1)
+    const char *last_kernel;      // name of the last batch's reconstruction kernel (diagnostics)
     int wg_pp;                    // single-picture k_wg launches: two ping-pong row units (k_wgpp, default; H264MI_WG_PP=0: one)
     // stream groups (h264mi_engine_set_groups): the pictures of a device-input
     // batch split into G groups, each on its own HIP stream, so one group's
@@ -287,6 +288,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     const bool rec = e->timing || e->tev;
     if (rec) (void)hipEventRecord(t0, e->st);
+    e->last_kernel = !wg ? "k_mb+k_rows" : pipe ? "k_wg" : (e->wg_ch && prep) ? "k_wgch" : (e->wg_pp && prep) ? "k_wgpp" : "k_wg";
     if (!wg) {
         hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
         HIPCHECK(hipGetLastError());
@@ -451,6 +453,11 @@ extern "C" int h264mi_engine_decode_pipelined(h264mi_engine *e, int nstreams, in
     HIPCHECK(hipSetDevice(e->dev));
     return launch_batch(e, nstreams * depth, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, true, depth,
                         base_pic, lag_rows);
+}
+
+extern "C" const char *h264mi_engine_kernel(h264mi_engine *e)
+{
+    return e && e->last_kernel ? e->last_kernel : "";
 }
 
 extern "C" int h264mi_engine_sync(h264mi_engine *e)

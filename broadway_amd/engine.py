@@ -124,6 +124,10 @@ class Engine:
         if self._L.h264mi_engine_sync(self._h) != 0:
             raise RuntimeError("h264mi_engine_sync failed")
 
+    def kernel_name(self) -> str:
+        """Reconstruction kernel of the last batch (diagnostics)."""
+        return self._L.h264mi_engine_kernel(self._h).decode()
+
     def errors(self) -> int:
         return int(self._L.h264mi_engine_errors(self._h))
 

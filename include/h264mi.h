@@ -176,6 +176,9 @@ int  h264mi_engine_decode_pipelined(h264mi_engine *e, int nstreams, int depth, c
  * of its phases, then 4 u64 per MB (hand-off timestamps); enable != 0 allocates, out != NULL copies the last launch */
 int  h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long long *out, size_t n);
 void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);          /* device pointer */
+/* diagnostics: name of the last batch's reconstruction kernel ("k_wgpp",
+ * "k_wg", "k_mb+k_rows", ...; "" before the first batch) */
+const char *h264mi_engine_kernel(h264mi_engine *e);
 size_t h264mi_engine_frame_bytes(h264mi_engine *e);
 
 /* MB-record capture: run the host parser over a whole Annex-B stream and keep
