@@ -62,16 +62,28 @@ def test_decoder_js_api_holds_reordered_pictures():
     assert 0 < len(got) < len(c["frames"]) and got == c["frames"][:len(got)]
 
 
-# single-picture launch kernels: k_wg with 2/3/4 MC waves per row workgroup
-# (default 3), and the two-kernel k_mb + k_rows path
-KERNEL_MODES = [("wg", "3"), ("wg", "2"), ("wg", "4"), ("classic", "3")]
+# single-picture launch kernels (engine environment -> the kernel it must run):
+# the default k_prep + k_wgpp (2 ping-pong row waves, 2 MC waves), k_wgpp with
+# 3 MC waves, the one-row-wave k_wg (with and without k_prep), the chain +
+# helper k_wgch, and the two-kernel k_mb + k_rows path
+KERNEL_MODES = [
+    ({}, "k_wgpp"),
+    ({"H264MI_WG_NMC": "3"}, "k_wgpp"),
+    ({"H264MI_WG_PP": "0"}, "k_wg"),
+    ({"H264MI_WG_PP": "0", "H264MI_WG_NMC": "2"}, "k_wg"),
+    ({"H264MI_WG_PP": "0", "H264MI_PREP": "0"}, "k_wg"),
+    ({"H264MI_WG_CH": "1"}, "k_wgch"),
+    ({"H264MI_KERNEL": "classic"}, "k_mb+k_rows"),
+]
 
 
-@pytest.fixture(params=KERNEL_MODES, ids=lambda m: m[0] + m[1])
+@pytest.fixture(params=KERNEL_MODES, ids=lambda m: m[1] + "".join(f"-{k[6:].lower()}{v}" for k, v in m[0].items()))
 def kernel_mode(request, monkeypatch):
-    monkeypatch.setenv("H264MI_KERNEL", request.param[0])
-    monkeypatch.setenv("H264MI_WG_NMC", request.param[1])
-    return request.param
+    for k in ("H264MI_KERNEL", "H264MI_WG_NMC", "H264MI_WG_PP", "H264MI_PREP", "H264MI_WG_CH"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in request.param[0].items():
+        monkeypatch.setenv(k, v)
+    return request.param[1]
 
 
 def test_engine_multistream_batch_vs_oracle_replay(kernel_mode):
@@ -90,6 +102,7 @@ def test_engine_multistream_batch_vs_oracle_replay(kernel_mode):
             replays[s].picture(p.rec, p.coef, p.cur_slot)
         for s, p in enumerate(pics):
             assert eng.read(s, p.cur_slot).tobytes() == replays[s].frame(p.cur_slot), f"stream {s} picture {k}"
+    assert eng.kernel_name() == kernel_mode
     assert eng.errors() == 0
 
 
@@ -110,6 +123,7 @@ def test_engine_bench_streams_vs_reference(kernel_mode):
         for s, p in enumerate(pics):
             got = hashlib.md5(eng.read(s, p.cur_slot).tobytes()).hexdigest()
             assert got == CASES[names[s]]["frames"][k], f"stream {s} picture {k}"
+    assert eng.kernel_name() == kernel_mode
     assert eng.errors() == 0
 
 
