@@ -50,6 +50,8 @@ struct h264mi_engine {
     // stream): buffer half prep_parity, ordered by events
     int prep;                 // H264MI_PREP (default 1)
     int prep_parity;
+    int prep_serial;
+    double prep_delay_us;     // H264MI_PREP_DELAY_US: k_prep starts this long after it could          // H264MI_PREP_SERIAL: k_prep waits for the previous k_wgpp (diagnostics)
     hipStream_t st2;
     hipEvent_t ev_in, ev_prep, ev_wgdone[2];
     MbRec *d_rec;
@@ -136,6 +138,9 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         e->wg_nmc = nm ? atoi(nm) : (e->wg_pp ? 2 : 3);
         const char *ch = getenv("H264MI_WG_CH");
         e->wg_ch = ch ? atoi(ch) : 0;
+        e->prep_serial = getenv("H264MI_PREP_SERIAL") != NULL;
+        const char *pd = getenv("H264MI_PREP_DELAY_US");
+        e->prep_delay_us = pd ? atof(pd) : 0.0;
         const char *pr = getenv("H264MI_PREP");
         e->prep = pr ? atoi(pr) : 1;
     }
@@ -276,6 +281,9 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
             HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_in, 0));
         }
         HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_wgdone[pbuf], 0));
+        if (e->prep_serial) HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_wgdone[pbuf ^ 1], 0));   // experiment: no overlap
+        if (e->prep_delay_us > 0)      // start k_prep past the row kernel's start-up burst
+            hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, e->st2, (unsigned long long)(e->prep_delay_us * 100.0));
         hipLaunchKernelGGL(k_prep, dim3((npics * e->nmbs + 3) / 4), dim3(256), 0, e->st2, a);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipEventRecord(e->ev_prep, e->st2));
