@@ -2032,15 +2032,28 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         prov_off = le < 16 ? (uint32_t)((int)(G.ry - Lb) + (16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4)
                            : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 4 + qq * 4);
     }
-    // patch dword (cols -4..-1 of rows 12..15 / 6..7 of the current region)
-    uint32_t patch_off;
-    bool is_patch;
+    // ---- the hand-off to the row below, made by the wave that ran H(c):
+    //      MB c's rows 12..15 are final except columns 13..15, which MB c+1's
+    //      left edge (V(c+1) edge 0) still changes.  That edge reads MB c's
+    //      columns 12..15 (this region, now final w.r.t. H(c)) and MB c+1's
+    //      unfiltered columns 0..3 (its ring slot), with MB c+1's bS and
+    //      left-edge thresholds (its deblocking record, also in the slot) --
+    //      so this wave applies it to those 8 lines (lanes 0..7: luma rows
+    //      12..15, Cb rows 6/7, Cr rows 6/7) and publishes the final rows
+    //      without waiting for the partner's V(c+1).
+    const int pj = lane & 7;
+    const bool pchroma = pj >= 4;
+    uint32_t pp_off;        // p side: cols 12..15 / 4..7 of this region's rows 12..15 / 6..7
+    int pq_off;             // q side: cols 0..3 of the ring slot's MB
     {
-        const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-        patch_off = le < 16 ? (uint32_t)((int)(G.ry - Lb) + (16 + (le >> 2)) * RY_S)
-                            : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S);
-        is_patch = le < 16 ? (le & 3) == 3 : qq;
+        const int comp = (pj >> 1) & 1, row = pj & 1;
+        pp_off = !pchroma ? (uint32_t)((int)(G.ry - Lb) + (16 + pj) * RY_S + 16)
+                          : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 8);
+        pq_off = !pchroma ? (12 + pj) * 16 : 256 + comp * 64 + (6 + row) * 8;
     }
+    // publishing lanes (le): the patched dwords come from patch lane pl_src
+    const bool is_patch = le < 16 ? (le & 3) == 3 : (le & 1);
+    const int pl_src = le < 16 ? (le >> 2) : 4 + ((le - 16) >> 2) * 2 + ((le >> 1) & 1);
     // own samples from the ring slot: luma all lanes, chroma lanes 0..31
     const uint32_t own_y_lds = (uint32_t)((int)(G.ry - Lb) + (orow + 4) * RY_S + 4 + oq * 4);
     const uint32_t own_c_lds = lane < 32 ? (uint32_t)((int)((ccomp ? G.rv : G.ru) - Lb) + (crow + 2) * RC_S + 4 + cq * 4)
@@ -2068,6 +2081,9 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
         const cu32p rw = recw + c * 24;
         const uint32_t h0 = rw[0];
+        // MB c+1's record dword 0 (avail), for the hand-off patch (a VMEM load:
+        // an SMEM one would couple to every LDS wait through lgkmcnt)
+        const uint32_t avn = ldg32(uni(a.rec + rec_base + r * W + min(c + 1, W - 1)), 0);
         const int avail = (h0 >> 24) & 255;
         const bool dbf = avail & DB_INNER;
         // speculative read of the row above's entry c (lanes 0..23 used)
@@ -2101,8 +2117,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             *(uint32_t *)(Lb + db_lds) = od;
         }
         PPT(0);
-        // ---- the chain: MB c-1's H pass done -> its columns 12..15 and rows 12..15
-        uint32_t prov = 0;
+        // ---- the chain: MB c-1's H pass done -> its columns 12..15
         if (c > 0) {
             unsigned spins = 0;
             while (__builtin_amdgcn_readfirstlane(lds_ld(&L.hdone)) < c) {
@@ -2112,7 +2127,6 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             wave_sync();
             PPT(3);
             const uint32_t hv = *(const uint32_t *)((const uint8_t *)&Gp + cp_src);
-            prov = *(const uint32_t *)((const uint8_t *)&Gp + prov_off);
             *(uint32_t *)(Lb + cp_dst) = hv;
             wave_sync();
             if (lane == 0) { lds_st(&L.copied, c); lds_st(&R->consumed, c); }
@@ -2120,16 +2134,8 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             wave_sync();
             if (lane == 0) lds_st(&R->consumed, 0);
         }
-        // ---- vertical edges; MB c-1's final rows go to the row below right
-        //      after this MB's left edge
-        auto publish = [&]() {
-            const uint32_t patch = *(const uint32_t *)(Lb + patch_off);
-            const uint32_t ent = is_patch ? patch : prov;
-            st_gran(has_down && c > 0 ? mbx_me + (size_t)(c - 1) * 32 + le : sink, ent, tag);
-            if (prof && lane == 0) pmb[2] = wall_clock64();
-        };
-        if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT, publish);
-        else publish();
+        // ---- vertical edges
+        if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT);
         wave_sync();
         PPT(1);
         // ---- top halo (row above's entry c final), horizontal edges
@@ -2152,6 +2158,40 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         }
         if (lane == 0) lds_st(&L.hdone, c + 1);
         PPT(2);
+        if (has_down) {
+            const bool more = c + 1 < W;
+            uint32_t ent = *(const uint32_t *)(Lb + prov_off);
+            if (more) {
+                const int s1 = (c + 1) & (RING_K - 1);
+                {   // MB c+1's MC output (normally long done; its wave waits for it too)
+                    unsigned spins = 0;
+                    while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[s1])) != c + 2) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
+                    }
+                    wave_sync();
+                }
+                const uint32_t pdw = *(const uint32_t *)(Lb + pp_off);
+                const uint32_t qdw = *(const uint32_t *)&R->px[s1][pq_off];
+                const uint32_t *dbn = (const uint32_t *)R->db[s1];
+                const uint32_t bsw = dbn[1], t0 = dbn[pchroma ? 12 : 6], t1 = dbn[pchroma ? 13 : 7];
+                int v[20];
+#pragma unroll
+                for (int x = 0; x < 4; x++) { v[x] = (pdw >> (8 * x)) & 255; v[4 + x] = (qdw >> (8 * x)) & 255; }
+#pragma unroll
+                for (int x = 8; x < 20; x++) v[x] = 0;
+                const uint32_t avb = avn >> 24;
+                const bool on = (avb & DB_INNER) && (avb & DB_LEFT);
+                const int bS = on ? (int)((bsw >> 16) & 15) : 0;      // byte 6 low nibble: dir 0, seg 3, edge 0
+                const uint32_t tcs = (((t0 >> 8) & 0xFFFF00u) | (t1 << 24)) + (pchroma ? 0x01010100u : 0u);
+                filt_line<true>(v, 0, bS, t0 & 255, (t0 >> 8) & 255, pchroma ? 0 : ((t0 >> 8) & 255), tcs);
+                const uint32_t newp = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
+                const uint32_t pv = (uint32_t)__builtin_amdgcn_ds_bpermute(pl_src << 2, (int)newp);
+                if (is_patch) ent = pv;
+            }
+            st_gran(mbx_me + (size_t)c * 32 + le, ent, tag);
+            if (prof && lane == 0) pmb[2] = wall_clock64();
+        }
         // ---- off the chain again: frame stores, once per sample
         if (!last_row && c != W - 1) {
             const uint32_t va = *(const uint32_t *)(Lb + sa_lds);
@@ -2189,9 +2229,6 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                     st32<false>(cbase + c * 8 + qq * 4 + comp * CW * CH + (row - 2) * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[row * RC_S + 4 + qq * 4]);
                 }
             }
-            // the row's last entry is final as it stands (no right neighbour)
-            if (last_col && has_down && lane < 24)
-                st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, *(const uint32_t *)(Lb + prov_off), tag);
         }
         wave_sync();
         PPT(4);
