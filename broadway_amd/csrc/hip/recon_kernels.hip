@@ -2121,7 +2121,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         if (c > 0) {
             unsigned spins = 0;
             while (__builtin_amdgcn_readfirstlane(lds_ld(&L.hdone)) < c) {
-                __builtin_amdgcn_s_sleep(1);
+                // (no sleep: the partner's hdone store is the chain's next step)
                 if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
             }
             wave_sync();

@@ -6,7 +6,7 @@ import bench
 from broadway_amd import _lib
 from broadway_amd.engine import Engine
 L = _lib.mi()
-S = 8
+S = int(os.environ.get("PROF_S", "8"))
 streams, caps = bench.prepare(3, [100 + i for i in range(S)], 6)
 w, h = caps[0].w_mbs, caps[0].h_mbs
 d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6, 1, 0)
@@ -74,13 +74,10 @@ if os.environ.get("H264MI_WG_PP", "1") != "0":
     d = []
     for r in range(20, h):
         for c in range(4, w - 2):
-            d.append(m[0, r, c, 0] - m[0, r - 1, c + 1, 2])
+            d.append(m[0, r, c, 0] - m[0, r - 1, c, 2])     # k_wgpp: stamp 2 of MB c = entry c published
     d = np.array(d)
     print("hand-off arrival-publish (us): min %.2f p10 %.2f p50 %.2f p90 %.2f" % (d.min(), np.percentile(d, 10), np.percentile(d, 50), np.percentile(d, 90)))
     per = np.diff(m[0, 40, :, 0])
     print("row 40 H-start period (us): p10 %.2f p50 %.2f p90 %.2f" % (np.percentile(per, 10), np.percentile(per, 50), np.percentile(per, 90)))
-    pubs = m[0, 40, 1:, 2] - m[0, 40, :-1, 0]
+    pubs = m[0, 40, :, 2] - m[0, 40, :, 0]
     print("row 40 H(c) start -> publish(c) (us): p10 %.2f p50 %.2f p90 %.2f" % (np.percentile(pubs, 10), np.percentile(pubs, 50), np.percentile(pubs, 90)))
-    a2 = np.frombuffer(buf, dtype=np.uint64)[:S * h * 16].reshape(h, S, 16).astype(np.float64)
-    print("chain H end -> publish (cycles/MB): row0 %.0f row40 %.0f" % (a2[0, :, 10].mean() / w, a2[40, :, 10].mean() / w))
-    print("chain H end -> V start (cycles/MB): row0 %.0f row40 %.0f" % (a2[0, :, 11].mean() / w, a2[40, :, 11].mean() / w))
