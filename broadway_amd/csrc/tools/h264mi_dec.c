@@ -1,0 +1,110 @@
+/* h264mi_dec -- DecTestBench-style command line decoder over the product
+ * C-ABI (libh264mi.so: host parser + HIP reconstruction), the end-to-end
+ * path of SURVEY.md §8d: host CAVLC parse + H2D of the MB records + kernels +
+ * D2H of every output picture.  Call protocol of the reference testbench
+ * (Decoder/src/DecTestBench.c:230-410): decode, drain NextPicture after each
+ * PIC_RDY, flush at end of stream.
+ *   h264mi_dec [-R] [-Oout.yuv|-Onone] [-rN] [-T] in.h264
+ * -rN decodes the stream N times (one instance each; HIP start-up is paid
+ * once, before the timed loop); -T prints the wall time of the decode loops. */
+#include "../../../include/h264mi.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int decode_once(const uint8_t *stream, uint32_t len, uint8_t *work, int no_reorder, FILE *fo, int *errs)
+{
+    H264SwDecInst inst;
+    if (H264SwDecInit(&inst, (u32)no_reorder) != H264SWDEC_OK) return -1;
+    memcpy(work, stream, len);          /* the decoder edits its input in place */
+    H264SwDecInput in;
+    H264SwDecOutput out;
+    H264SwDecPicture pic;
+    H264SwDecInfo info;
+    memset(&in, 0, sizeof(in));
+    in.pStream = work;
+    in.dataLen = len;
+    size_t size = 0;
+    int pics = 0;
+    u32 pic_id = 0;
+    while (in.dataLen > 0) {
+        in.picId = pic_id;
+        H264SwDecRet r = H264SwDecDecode(inst, &in, &out);
+        if (r == H264SWDEC_HDRS_RDY_BUFF_NOT_EMPTY) {
+            if (H264SwDecGetInfo(inst, &info) != H264SWDEC_OK) break;
+            size = (size_t)info.picWidth * info.picHeight * 3 / 2;
+        } else if (r == H264SWDEC_PIC_RDY || r == H264SWDEC_PIC_RDY_BUFF_NOT_EMPTY) {
+            pic_id++;
+            while (H264SwDecNextPicture(inst, &pic, 0) == H264SWDEC_PIC_RDY) {
+                pics++;
+                *errs += (int)pic.nbrOfErrMBs;
+                if (fo) fwrite(pic.pOutputPicture, 1, size, fo);
+            }
+        } else if (r < 0) {
+            (*errs)++;
+        }
+        u32 used = (u32)(out.pStrmCurrPos - in.pStream);
+        if (used == 0 && r < 0) break;
+        in.dataLen -= used;
+        in.pStream = out.pStrmCurrPos;
+    }
+    while (H264SwDecNextPicture(inst, &pic, 1) == H264SWDEC_PIC_RDY) {
+        pics++;
+        *errs += (int)pic.nbrOfErrMBs;
+        if (fo) fwrite(pic.pOutputPicture, 1, size, fo);
+    }
+    H264SwDecRelease(inst);
+    return pics;
+}
+
+int main(int argc, char **argv)
+{
+    const char *out = NULL, *in = NULL;
+    int no_reorder = 0, timing = 0, reps = 1;
+    for (int i = 1; i < argc; i++) {
+        if (!strncmp(argv[i], "-O", 2)) out = argv[i] + 2;
+        else if (!strcmp(argv[i], "-R")) no_reorder = 1;
+        else if (!strcmp(argv[i], "-T")) timing = 1;
+        else if (!strncmp(argv[i], "-r", 2)) reps = atoi(argv[i] + 2);
+        else in = argv[i];
+    }
+    if (!in || reps < 1) { fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] in.h264\n"); return 2; }
+    FILE *f = fopen(in, "rb");
+    if (!f) { perror(in); return 2; }
+    fseek(f, 0, SEEK_END);
+    long len = ftell(f);
+    rewind(f);
+    uint8_t *buf = (uint8_t *)malloc((size_t)len), *work = (uint8_t *)malloc((size_t)len);
+    if (!buf || !work || fread(buf, 1, (size_t)len, f) != (size_t)len) { fclose(f); return 2; }
+    fclose(f);
+    FILE *fo = (out && strcmp(out, "none")) ? fopen(out, "wb") : NULL;
+    /* HIP start-up (device, code objects) outside the timed loop */
+    {
+        H264SwDecInst warm;
+        if (H264SwDecInit(&warm, 0) != H264SWDEC_OK) { fprintf(stderr, "DECODER INITIALIZATION FAILED\n"); return 1; }
+        H264SwDecRelease(warm);
+    }
+    int pics = 0, errs = 0;
+    const double t0 = now_s();
+    for (int k = 0; k < reps; k++) {
+        const int n = decode_once(buf, (uint32_t)len, work, no_reorder, k == 0 ? fo : NULL, &errs);
+        if (n < 0) { fprintf(stderr, "DECODER INITIALIZATION FAILED\n"); return 1; }
+        pics += n;
+    }
+    const double t1 = now_s();
+    if (fo) fclose(fo);
+    printf("pictures %d errors %d\n", pics, errs);
+    if (timing) printf("decode_seconds %.6f fps %.2f\n", t1 - t0, pics / (t1 - t0));
+    free(buf);
+    free(work);
+    return errs ? 1 : 0;
+}
