@@ -34,7 +34,6 @@ struct h264mi_engine {
     unsigned long long *d_gjunk;  // 64 KiB store sink (ReconArgs::gjunk)
     int classic;                  // single-picture launches: k_wg (default) or k_mb + k_rows (H264MI_KERNEL=classic)
     int wg_nmc;                   // MC waves per k_wg workgroup (H264MI_WG_NMC: 2, 3 or 4)
-    int wg_ch;                    // single-picture k_wg launches: chain + helper row waves (k_wgch; H264MI_WG_CH=1)
     const char *last_kernel;      // name of the last batch's reconstruction kernel (diagnostics)
     int wg_pp;                    // single-picture k_wg launches: two ping-pong row units (k_wgpp, default; H264MI_WG_PP=0: one)
     // stream groups (h264mi_engine_set_groups): the pictures of a device-input
@@ -136,8 +135,6 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         // three workgroups per CU keep every row of 8 1080p pictures
         // resident), 3 with one row unit
         e->wg_nmc = nm ? atoi(nm) : (e->wg_pp ? 2 : 3);
-        const char *ch = getenv("H264MI_WG_CH");
-        e->wg_ch = ch ? atoi(ch) : 0;
         e->prep_serial = getenv("H264MI_PREP_SERIAL") != NULL;
         const char *pd = getenv("H264MI_PREP_DELAY_US");
         e->prep_delay_us = pd ? atof(pd) : -1.0;
@@ -300,7 +297,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     const bool rec = e->timing || e->tev;
     if (rec) (void)hipEventRecord(t0, e->st);
-    e->last_kernel = !wg ? "k_mb+k_rows" : pipe ? "k_wg" : (e->wg_ch && prep) ? "k_wgch" : (e->wg_pp && prep) ? "k_wgpp" : "k_wg";
+    e->last_kernel = !wg ? "k_mb+k_rows" : pipe ? "k_wg" : (e->wg_pp && prep) ? "k_wgpp" : "k_wg";
     if (!wg) {
         hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
         HIPCHECK(hipGetLastError());
@@ -318,9 +315,6 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
             if (nmc == 2) hipLaunchKernelGGL((k_wg<true, 2, false>), grid, dim3(192), 0, e->st, a);
             else if (nmc == 4) hipLaunchKernelGGL((k_wg<true, 4, false>), grid, dim3(320), 0, e->st, a);
             else hipLaunchKernelGGL((k_wg<true, 3, false>), grid, dim3(256), 0, e->st, a);
-        } else if (e->wg_ch && prep) {
-            if (a.prof) hipLaunchKernelGGL((k_wgch<2, true, true>), grid, dim3(256), 0, e->st, a);
-            else hipLaunchKernelGGL((k_wgch<2, false, true>), grid, dim3(256), 0, e->st, a);
         } else if (e->wg_pp && prep) {
             if (a.prof) {
                 if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, true, true>), grid, dim3(256), 0, e->st, a);

@@ -1949,7 +1949,6 @@ struct __attribute__((aligned(16))) PPRegion {
     uint8_t ry[20 * RY_S];      // rows -4..15, cols -4..15
     uint8_t ru[10 * RC_S];      // rows -2..7, cols -4..7
     uint8_t rv[10 * RC_S];
-    uint32_t hdr;               // k_wgch: the MB record's first dword (type, qp, qpc, avail)
 };
 struct __attribute__((aligned(16))) PPLds {
     PPRegion G[2];
@@ -2254,315 +2253,6 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 }
 
 // ---------------------------------------------------------------------------
-// k_wgch: the row's deblocking split into a CHAIN wave and a HELPER wave.
-// The chain wave runs only what the row's dependency chain needs, MB after
-// MB: left-halo copy, vertical edges (publishing MB c-1's final rows to the
-// row below right after the MB edge), row-above wait, horizontal edges.
-// The helper wave does everything else one MB ahead / behind: taking MB c's
-// samples and deblocking record out of the MC ring into region G[c & 1]
-// (filled = c + 1), and storing MB c-2's final samples from that region
-// before it refills it.  No wave-to-wave hand-off sits between consecutive
-// MBs of the chain (k_wgpp has one per MB).  Flags (LDS, monotonic):
-//   filled = c + 1  G[c & 1] holds MB c (helper -> chain)
-//   copied = c + 1  the chain has read MB c-1's region for MB c (chain -> helper)
-//   hdone  = c + 1  H(c) done (chain -> helper: MB c's samples final in G[c & 1])
-// Reference: h264bsdFilterPicture (deblocking.c:574-639), per MB vertical
-// then horizontal edges (:603-637).
-// ---------------------------------------------------------------------------
-struct __attribute__((aligned(16))) ChLds {
-    PPRegion G[2];
-    uint8_t junk[2][256];
-    int filled, copied, hdone, pdone;
-    uint32_t i4tab[9 * 16];
-    unsigned long long ptw1[8];
-};
-
-__device__ __forceinline__ void lds_wait_ge(const int *flag, int v, unsigned *perr, int lane)
-{
-    unsigned spins = 0;
-    while (__builtin_amdgcn_readfirstlane(lds_ld(flag)) < v) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
-    }
-    wave_sync();
-}
-
-template <bool PROF>
-__device__ void row_ch(const ReconArgs &a, int p, int r, ChLds &L, const int role, const int lane, MbRing *R)
-{
-    const int W = a.w, H = a.h;
-    const PicDesc *pdp = a.pics + p;
-    const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
-    const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
-    const int W16 = W * 16, H16 = H * 16, CW = W16 / 2, CH = H16 / 2;
-    uint8_t *cur = a.frames + (unsigned long long)fslot * a.frame_bytes;
-    uint8_t *curU = cur + (size_t)W16 * H16;
-    unsigned *perr = a.err + p;
-    const uint32_t tag = a.epoch;
-    const bool has_up = r > 0, has_down = r + 1 < H;
-    const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
-    unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
-    const bool last_row = r == H - 1;
-    typedef const __attribute__((address_space(4))) uint32_t *cu32p;
-    const cu32p recw = (cu32p)(const void *)(a.rec + rec_base + r * W);   // 24 dwords per record
-    uint8_t *const junk = L.junk[role];
-    // offsets inside a PPRegion (both regions share the layout)
-    const PPRegion &G0 = L.G[0];
-    const uint8_t *const B0 = (const uint8_t *)&G0;
-    const int Lry = (int)(G0.ry - B0), Lru = (int)(G0.ru - B0), Lrv = (int)(G0.rv - B0);
-    auto region = [&](int c) -> uint8_t * { return (uint8_t *)&L.G[c & 1]; };
-
-    const int orow = lane >> 2, oq = lane & 3;
-    const int li = lane & 31;
-    const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;
-    const int le = li < 24 ? li : li - 8;
-    uint8_t *const ybase = cur + (size_t)r * 16 * W16;
-    uint8_t *const cbase = curU + (size_t)r * 8 * CW;
-    unsigned long long *const sink = a.gjunk + ((p * H + r) & 127) * 64 + lane;
-    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bool prof = PROF && a.prof != nullptr;
-    unsigned long long tc0 = 0, tc1;
-#define CHT(i) do { if (prof) { tc1 = clock64(); pt[i] += tc1 - tc0; tc0 = tc1; } } while (0)
-
-    if (role == 0) {
-        // ======================= chain =======================
-        if (prof && lane == 0) a.prof[((size_t)r * a.npics + p) * 16] = wall_clock64();
-        uint32_t cp_src, cp_dst;       // left-halo copy: cols 12..15 / 4..7 -> -4..-1 (lanes 32..63: junk)
-        {
-            int off, step, base;
-            if (lane < 16) { base = Lry; off = (lane + 4) * RY_S; step = 16; }
-            else { const int k = (lane - 16) & 15; base = (k >> 3) ? Lrv : Lru; off = ((k & 7) + 2) * RC_S; step = 8; }
-            cp_src = (uint32_t)(base + off + step);
-            cp_dst = (uint32_t)(base + off);
-        }
-        uint32_t prov_off, patch_off;
-        bool is_patch;
-        {
-            const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-            prov_off = le < 16 ? (uint32_t)(Lry + (16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4)
-                               : (uint32_t)((comp ? Lrv : Lru) + (8 + row) * RC_S + 4 + qq * 4);
-            patch_off = le < 16 ? (uint32_t)(Lry + (16 + (le >> 2)) * RY_S) : (uint32_t)((comp ? Lrv : Lru) + (8 + row) * RC_S);
-            is_patch = le < 16 ? (le & 3) == 3 : qq;
-        }
-        uint32_t top_lds;
-        {
-            const int k = lane - 16, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-            top_lds = lane < 16 ? (uint32_t)(Lry + orow * RY_S + 4 + oq * 4)
-                    : (uint32_t)((comp ? Lrv : Lru) + row * RC_S + 4 + qq * 4);
-        }
-        const bool top_mine = lane < 24;
-        unsigned long long tpub = 0, th_end = 0, tpre = 0;     // PROF: H(c-1) end -> publish(c-1) / -> V start, summed
-        // (the record's first dword comes from the region, put there by the
-        // helper: a scalar load here would make every LDS wait of the chain
-        // wait for it too -- SMEM and LDS share lgkmcnt, and SMEM returns out
-        // of order, so the counter can only be drained to zero)
-        int fseen = 0;                               // last value of `filled` seen
-        for (int c = 0; c < W; c++) {
-            if (prof) { tc0 = clock64(); th_end = c > 0 ? th_end : tc0; }
-            unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
-            const unsigned long long *tga = mbx_up + c * 32 + (lane < 24 ? lane : (lane & 15));
-            unsigned long long gr = ld_gran(tga);           // speculative row-above read
-            uint8_t *const Gc = region(c);
-            const uint8_t *const Gq = region(c + 1);        // MB c-1's region
-            if (fseen < c + 1) {
-                unsigned spins = 0;
-                for (;;) {
-                    fseen = __builtin_amdgcn_readfirstlane(lds_ld(&L.filled));
-                    if (fseen >= c + 1) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
-                }
-                wave_sync();
-            }
-            CHT(7);
-            const uint32_t h0 = __builtin_amdgcn_readfirstlane(((const PPRegion *)Gc)->hdr);
-            const int avail = (h0 >> 24) & 255;
-            const bool dbf = avail & DB_INNER;
-            // MB c-1's rows 12..15 (provisional entry); its cols 12..15 are
-            // read by the vertical pass itself (pdelta) -- copied here only
-            // when this MB is not filtered
-            uint32_t prov = 0;
-            if (c > 0) {
-                prov = *(const uint32_t *)(Gq + prov_off);
-                if (!dbf) {
-                    const uint32_t hv = *(const uint32_t *)(Gq + cp_src);
-                    if (lane < 32) *(uint32_t *)(Gc + cp_dst) = hv;
-                    wave_sync();
-                }
-            }
-
-            auto publish = [&]() {
-                const uint32_t patch = *(const uint32_t *)(Gc + patch_off);
-                st_gran(has_down && c > 0 ? mbx_me + (size_t)(c - 1) * 32 + le : sink, is_patch ? patch : prov, tag);
-                if (prof && lane == 0) pmb[2] = wall_clock64();
-                if (prof) tpub += clock64() - th_end;
-            };
-            if (prof) { const unsigned long long tq = clock64(); tpre += tq - th_end; }
-            PPRegion &G = *(PPRegion *)Gc;
-            if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT, publish, c > 0 ? (int)(Gq - Gc) : 0);
-            else publish();
-            wave_sync();
-            // MB c-1's region has been read (prov, its cols 12..15): the
-            // helper may store it out and refill it with MB c+1
-            if (lane == 0) lds_st(&L.copied, c + 1);
-            CHT(1);
-            if (has_up) {
-                unsigned spins = 0;
-                while (__builtin_amdgcn_ballot_w64(top_mine && (uint32_t)(gr >> 32) != tag) != 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }
-                    if (top_mine) gr = ld_gran(tga);
-                }
-                if (top_mine) *(uint32_t *)(Gc + top_lds) = (uint32_t)gr;
-                wave_sync();
-            }
-            if (prof && lane == 0) pmb[0] = wall_clock64();
-            CHT(5);
-            if (dbf) {
-                deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_TOP);
-                wave_sync();
-            }
-            if (lane == 0) lds_st(&L.hdone, c + 1);
-            CHT(2);
-            if (prof) th_end = tc0;
-        }
-        if (prof && lane == 0) { a.prof[((size_t)r * a.npics + p) * 16 + 10] = tpub; a.prof[((size_t)r * a.npics + p) * 16 + 11] = tpre; }
-    } else {
-        // ======================= helper =======================
-        uint32_t sa_lds, sa_glb, sb_lds, sb_glb;
-        bool sa_left, sa_top, sb_left, sb_top;
-        {
-            int row, col;
-            if (lane < 36) { row = lane / 3; col = (lane % 3) * 4; }
-            else if (lane < 48) { row = lane - 36; col = -4; }
-            else { row = -4 + ((lane - 48) >> 2); col = ((lane - 48) & 3) * 4; }
-            sa_lds = (uint32_t)(Lry + (row + 4) * RY_S + 4 + col);
-            sa_glb = (uint32_t)((row + 4) * W16 + col + 4);
-            sa_left = lane >= 36 && lane < 48;
-            sa_top = lane >= 48;
-            int comp;
-            const int k = lane & 31;
-            if (k < 12) { comp = k / 6; row = k % 6; col = 0; }
-            else if (k < 24) { comp = (k - 12) / 6; row = (k - 12) % 6; col = -4; }
-            else { comp = (k - 24) >> 2; row = -2 + (((k - 24) >> 1) & 1); col = ((k - 24) & 1) * 4; }
-            sb_lds = (uint32_t)((comp ? Lrv : Lru) + (row + 2) * RC_S + 4 + col);
-            sb_glb = (uint32_t)(comp * CW * CH + (row + 2) * CW + col + 4);
-            sb_left = k >= 12 && k < 24;
-            sb_top = k >= 24;
-        }
-        const uint32_t yoff = (uint32_t)(orow * W16 + oq * 4);
-        const uint32_t coff = (uint32_t)(ccomp * CW * CH + crow * CW + cq * 4);
-        const uint32_t own_y_lds = (uint32_t)(Lry + (orow + 4) * RY_S + 4 + oq * 4);
-        const uint32_t own_c_lds = (uint32_t)((ccomp ? Lrv : Lru) + (crow + 2) * RC_S + 4 + cq * 4);
-        uint32_t prov_w;
-        {
-            const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-            prov_w = le < 16 ? (uint32_t)(Lry + (16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4)
-                             : (uint32_t)((comp ? Lrv : Lru) + (8 + row) * RC_S + 4 + qq * 4);
-        }
-        // final samples of MB m from its region (once hdone > m)
-        auto store_mb = [&](int m) {
-            const uint8_t *Gm = region(m);
-            const PPRegion &G = *(const PPRegion *)Gm;
-            if (!last_row && m != W - 1) {
-                const uint32_t va = *(const uint32_t *)(Gm + sa_lds);
-                const uint32_t vb = *(const uint32_t *)(Gm + sb_lds);
-                uint8_t *const yb = ybase + m * 16 - 4 * W16 - 4;
-                uint8_t *const cb = cbase + m * 8 - 2 * CW - 4;
-                const bool oka = (!sa_left || m > 0) && (!sa_top || has_up);
-                const bool okb = (!sb_left || m > 0) && (!sb_top || has_up);
-                st32<false>(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
-                st32<false>(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
-            } else {
-                const int yrows = last_row ? 16 : 12;
-                const int crows = last_row ? 8 : 6;
-                const bool last_col = m == W - 1;
-                if (orow < yrows && (oq < 3 || last_col))
-                    st32<false>(ybase + m * 16 + yoff, *(const uint32_t *)&G.ry[(orow + 4) * RY_S + 4 + oq * 4]);
-                if (lane < 32 && crow < crows && (cq == 0 || last_col))
-                    st32<false>(cbase + m * 8 + coff, *(const uint32_t *)&(ccomp ? G.rv : G.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
-                if (m > 0) {
-                    if (lane < 16) {
-                        if (lane < yrows)
-                            st32<false>(ybase + m * 16 - 4 + lane * W16, *(const uint32_t *)&G.ry[(lane + 4) * RY_S]);
-                    } else if (lane < 32) {
-                        const int k = lane - 16, comp = k >> 3, row = k & 7;
-                        if (row < crows)
-                            st32<false>(cbase + m * 8 - 4 + comp * CW * CH + row * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[(row + 2) * RC_S]);
-                    }
-                }
-                if (has_up) {
-                    if (lane >= 32 && lane < 48) {
-                        const int k = lane - 32;
-                        st32<false>(ybase + m * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&G.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
-                    } else if (lane >= 48 && lane < 56) {
-                        const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-                        st32<false>(cbase + m * 8 + qq * 4 + comp * CW * CH + (row - 2) * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[row * RC_S + 4 + qq * 4]);
-                    }
-                }
-                if (last_col && has_down && lane < 24)      // the row's last entry: final as it stands
-                    st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, *(const uint32_t *)(Gm + prov_w), tag);
-            }
-        };
-        for (int c = 0; c < W; c++) {
-            if (prof) tc0 = clock64();
-            uint8_t *const Gc = region(c);
-            if (c >= 2) {
-                lds_wait_ge(&L.copied, c, perr, lane);       // chain read MB c-2's region (for MB c-1)
-                lds_wait_ge(&L.hdone, c - 1, perr, lane);    // MB c-2 final
-                CHT(3);
-                store_mb(c - 2);
-                CHT(4);
-            }
-            const int slot = c & (RING_K - 1);
-            {
-                unsigned spins = 0;
-                while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
-                }
-                wave_sync();
-            }
-            CHT(6);
-            {
-                const uint32_t oy = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
-                const uint32_t oc = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
-                const uint32_t od = ((const uint32_t *)R->db[slot])[lane & 15];
-                *(uint32_t *)(Gc + own_y_lds) = oy;
-                if (lane < 32) *(uint32_t *)(Gc + own_c_lds) = oc;
-                if (lane < 16) ((uint32_t *)Gc)[lane] = od;       // db at offset 0
-                if (lane == 0) ((PPRegion *)Gc)->hdr = recw[c * 24];
-                wave_sync();
-                if (lane == 0) { lds_st(&R->consumed, c); lds_st(&L.filled, c + 1); }
-            }
-            CHT(0);
-        }
-        for (int m = (W >= 2 ? W - 2 : 0); m < W; m++) {
-            lds_wait_ge(&L.hdone, m + 1, perr, lane);
-            store_mb(m);
-        }
-        if (prof && lane == 0) a.prof[((size_t)r * a.npics + p) * 16 + 1] = wall_clock64();
-    }
-    if (prof) {
-        unsigned long long *o = a.prof + ((size_t)r * a.npics + p) * 16;
-        if (role == 1) {
-            if (lane == 0) {
-                for (int i = 0; i < 8; i++) L.ptw1[i] = pt[i];
-                wave_sync();
-                lds_st(&L.pdone, 1);
-            }
-        } else {
-            unsigned spins = 0;
-            while (__builtin_amdgcn_readfirstlane(lds_ld(&L.pdone)) == 0 && ++spins < (1u << 22)) __builtin_amdgcn_s_sleep(1);
-            wave_sync();
-            if (lane == 0)
-                for (int i = 0; i < 8; i++) o[2 + i] = pt[i] + L.ptw1[i];
-        }
-    }
-#undef CHT
-}
-
-// ---------------------------------------------------------------------------
 // Software-pipelined MC for k_wgpp (k_prep outputs, single-picture launches):
 // mc_issue issues every HBM load of one MB -- its k_prep outputs (deblocking
 // record, residual) and its reference windows -- from the MB's record held
@@ -2794,73 +2484,4 @@ template __global__ void k_wgpp<3, false, true>(ReconArgs);
 template __global__ void k_wgpp<2, true, true>(ReconArgs);
 template __global__ void k_wgpp<3, true, true>(ReconArgs);
 
-template <int NMC, bool PROF, bool PREP>
-__global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(NMC == 3 ? 4 : 3))) void k_wgch(ReconArgs a)
-{
-    __shared__ ChLds L;
-    __shared__ McScratch M[NMC];
-    __shared__ MbRing R;
-    const int S = a.S;
-    const int pair = blockIdx.x / S, s = blockIdx.x - pair * S;
-    const uint32_t kr = a.order[pair];
-    const int k = (int)(kr >> 16), r = (int)(kr & 0xFFFF);
-    const int p = k * S + s;
-    if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
-    if (threadIdx.x == 0) { R.consumed = 0; L.hdone = 0; L.copied = 0; L.filled = 0; L.pdone = 0; }
-    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2)) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
-    __syncthreads();
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wid < 2) {
-        __builtin_amdgcn_s_setprio(3);
-        row_ch<PROF>(a, p, r, L, wid, lane, &R);
-        return;
-    }
-    static_assert(PREP, "k_wgch's MC waves take k_prep outputs");
-    McScratch &Mw = M[wid - 2];
-    const PicDesc pd = a.pics[p];
-    const uint32_t *recrow = (const uint32_t *)(a.rec + pd.rec_base + r * a.w);
-    const int c0 = wid - 2;
-    // MB c0's record (lane i < 24: dword i) and loads; then one MB ahead
-    uint32_t v0 = c0 < a.w ? recrow[(size_t)c0 * 24 + (lane < 24 ? lane : 0)] : 0;
-    McLoad ld;
-    if (c0 < a.w) mc_issue(a, pd, r * a.w + c0, v0, lane, ld);
-    for (int c = c0; c < a.w; c += NMC) {
-        const int slot = c & (RING_K - 1);
-        const bool more = c + NMC < a.w;
-        const uint32_t nv0 = more ? recrow[(size_t)(c + NMC) * 24 + (lane < 24 ? lane : 0)] : 0;
-        if (c >= RING_K) {
-            unsigned spins = 0;
-            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RING_K + 1) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }
-            }
-            wave_sync();
-        }
-        const unsigned long long t0 = PROF ? clock64() : 0;
-        const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], R.res[slot], R.db[slot]);
-        if (type == MBT_IPCM) {
-            const PicDesc &pd = a.pics[p];
-            const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
-            ((uint32_t *)R.px[slot])[lane] = src[lane];
-            if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
-        } else if (type >= MBT_I4x4) {
-            const PicDesc &pd = a.pics[p];
-            mc_intra(a.rec + pd.rec_base + r * a.w + c, a.mbx + ((size_t)p * a.h + (r > 0 ? r - 1 : 0)) * a.w * 32,
-                     a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, L.i4tab);
-        }
-        wave_sync();
-        {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
-            const int kk = lane & 7;
-            const uint8_t *px = R.px[slot];
-            const uint32_t v = *(const uint32_t *)&px[kk < 4 ? 240 + kk * 4 : kk < 6 ? 312 + (kk - 4) * 4 : 376 + (kk - 6) * 4];
-            if (r + 1 < a.h)
-                st_gran(a.mbx + ((size_t)p * a.h + r) * a.w * 32 + c * 32 + 24 + kk, v, a.epoch);
-        }
-        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
-        if (lane == 0) lds_st(&R.flag[slot], c + 1);
-        v0 = nv0;
-        if (more) mc_issue(a, pd, r * a.w + c + NMC, v0, lane, ld);
-    }
-}
-template __global__ void k_wgch<2, false, true>(ReconArgs);
-template __global__ void k_wgch<2, true, true>(ReconArgs);
+

@@ -64,22 +64,21 @@ def test_decoder_js_api_holds_reordered_pictures():
 
 # single-picture launch kernels (engine environment -> the kernel it must run):
 # the default k_prep + k_wgpp (2 ping-pong row waves, 2 MC waves), k_wgpp with
-# 3 MC waves, the one-row-wave k_wg (with and without k_prep), the chain +
-# helper k_wgch, and the two-kernel k_mb + k_rows path
+# 3 MC waves, the one-row-wave k_wg (with and without k_prep), and the
+# two-kernel k_mb + k_rows path
 KERNEL_MODES = [
     ({}, "k_wgpp"),
     ({"H264MI_WG_NMC": "3"}, "k_wgpp"),
     ({"H264MI_WG_PP": "0"}, "k_wg"),
     ({"H264MI_WG_PP": "0", "H264MI_WG_NMC": "2"}, "k_wg"),
     ({"H264MI_WG_PP": "0", "H264MI_PREP": "0"}, "k_wg"),
-    ({"H264MI_WG_CH": "1"}, "k_wgch"),
     ({"H264MI_KERNEL": "classic"}, "k_mb+k_rows"),
 ]
 
 
 @pytest.fixture(params=KERNEL_MODES, ids=lambda m: m[1] + "".join(f"-{k[6:].lower()}{v}" for k, v in m[0].items()))
 def kernel_mode(request, monkeypatch):
-    for k in ("H264MI_KERNEL", "H264MI_WG_NMC", "H264MI_WG_PP", "H264MI_PREP", "H264MI_WG_CH"):
+    for k in ("H264MI_KERNEL", "H264MI_WG_NMC", "H264MI_WG_PP", "H264MI_PREP"):
         monkeypatch.delenv(k, raising=False)
     for k, v in request.param[0].items():
         monkeypatch.setenv(k, v)

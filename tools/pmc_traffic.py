@@ -42,7 +42,7 @@ def main(tag):
     write = per_launch(os.path.join(src, "pmc_write", "bench_counter_collection.csv"), "WRITE_SIZE")
     kernels = {}
     step = 0.0
-    main_k = next((k for k in ("k_wgpp", "k_wgch", "k_wg") if k in fetch), None)
+    main_k = next((k for k in ("k_wgpp", "k_wg") if k in fetch), None)
     step_kernels = ((main_k,) if main_k else ("k_mb", "k_rows")) + (("k_prep",) if "k_prep" in fetch else ())
     for k in step_kernels:
         f_kib, n = fetch[k]
