@@ -131,10 +131,10 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         const char *nm = getenv("H264MI_WG_NMC");
         const char *pp = getenv("H264MI_WG_PP");
         e->wg_pp = pp ? atoi(pp) : 1;
-        // MC waves per workgroup: 2 with the ping-pong row units (4 waves,
-        // three workgroups per CU keep every row of 8 1080p pictures
-        // resident), 3 with one row unit
-        e->wg_nmc = nm ? atoi(nm) : (e->wg_pp ? 2 : 3);
+        // MC waves per workgroup (default 3: with the ping-pong row waves a
+        // 5-wave workgroup at <= 128 VGPRs, three per CU keep every row of
+        // 8 1080p pictures resident)
+        e->wg_nmc = nm ? atoi(nm) : 3;
         e->prep_serial = getenv("H264MI_PREP_SERIAL") != NULL;
         const char *pd = getenv("H264MI_PREP_DELAY_US");
         e->prep_delay_us = pd ? atof(pd) : -1.0;

@@ -331,48 +331,55 @@ __device__ __forceinline__ void luma_row4(const uint8_t *win, int yy, int fx, in
 // Replaces per-sample LDS byte reads under lane-divergent position branches.
 __device__ __forceinline__ void luma_row4_reg(const uint32_t (*wr)[3], int xo, int fx, int fy, bool need_j, int out[4])
 {
-    int sm[6][9];
+    // one window row at a time (9 samples live, not 54): the vertical taps
+    // of h (columns 2..6) and of j (over the rows' horizontal taps)
+    // accumulate as the rows stream in
+    const int tw[6] = {1, -5, 20, 20, -5, 1};
+    int hacc[5] = {0, 0, 0, 0, 0}, jacc[4] = {0, 0, 0, 0}, bh[4], bh1[4], G[5], Gy[4];
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         const uint32_t d0 = wr[i][0], d1 = wr[i][1], d2 = wr[i][2];
         const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)xo);
         const uint32_t a1 = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)xo);
+        int sm[9];
 #pragma unroll
-        for (int x = 0; x < 4; x++) { sm[i][x] = (a0 >> (8 * x)) & 255; sm[i][4 + x] = (a1 >> (8 * x)) & 255; }
-        sm[i][8] = (int)__builtin_amdgcn_ubfe(d2, (uint32_t)xo * 8, 8);
-    }
-    // horizontal taps over row i, output column x: window columns x..x+5
-#define HT(i, x) tap6(sm[i][(x)], sm[i][(x) + 1], sm[i][(x) + 2], sm[i][(x) + 3], sm[i][(x) + 4], sm[i][(x) + 5])
-    int bh[4], bh1[4], hv[5], jj[4];
+        for (int x = 0; x < 4; x++) { sm[x] = (a0 >> (8 * x)) & 255; sm[4 + x] = (a1 >> (8 * x)) & 255; }
+        sm[8] = (int)__builtin_amdgcn_ubfe(d2, (uint32_t)xo * 8, 8);
 #pragma unroll
-    for (int x = 0; x < 4; x++) {
-        bh[x] = clip255((HT(2, x) + 16) >> 5);
-        bh1[x] = clip255((HT(3, x) + 16) >> 5);
-    }
+        for (int x = 0; x < 5; x++) hacc[x] += tw[i] * sm[x + 2];
+        if (i == 2) {
 #pragma unroll
-    for (int x = 0; x < 5; x++)
-        hv[x] = clip255((tap6(sm[0][x + 2], sm[1][x + 2], sm[2][x + 2], sm[3][x + 2], sm[4][x + 2], sm[5][x + 2]) + 16) >> 5);
+            for (int x = 0; x < 5; x++) G[x] = sm[x + 2];
+        }
+        if (i == 3) {
 #pragma unroll
-    for (int x = 0; x < 4; x++) jj[x] = 0;
-    if (need_j) {
+            for (int x = 0; x < 4; x++) Gy[x] = sm[x + 2];
+        }
+        if (i == 2 || i == 3 || need_j) {
 #pragma unroll
-        for (int x = 0; x < 4; x++) {
-            const int j1 = tap6(HT(0, x), HT(1, x), HT(2, x), HT(3, x), HT(4, x), HT(5, x));
-            jj[x] = clip255((j1 + 512) >> 10);
+            for (int x = 0; x < 4; x++) {
+                const int ht = tap6(sm[x], sm[x + 1], sm[x + 2], sm[x + 3], sm[x + 4], sm[x + 5]);
+                if (i == 2) bh[x] = clip255((ht + 16) >> 5);
+                if (i == 3) bh1[x] = clip255((ht + 16) >> 5);
+                if (need_j) jacc[x] += tw[i] * ht;
+            }
         }
     }
-#undef HT
+    int hv[5];
+#pragma unroll
+    for (int x = 0; x < 5; x++) hv[x] = clip255((hacc[x] + 16) >> 5);
     const bool fy0 = fy == 0, fx0 = fx == 0, half = fx == 2 || fy == 2;
 #pragma unroll
     for (int x = 0; x < 4; x++) {
-        const int G = sm[2][x + 2], Gx = sm[2][x + 3], Gy = sm[3][x + 2];
+        const int jj = need_j ? clip255((jacc[x] + 512) >> 10) : 0;
+        const int g = G[x], gx = G[x + 1], gy = Gy[x];
         const int bs = fy == 3 ? bh1[x] : bh[x];
         const int hs = fx == 3 ? hv[x + 1] : hv[x];
         int A, B;
-        if (fx0 && fy0) { A = G; B = G; }
-        else if (fy0) { A = bh[x]; B = fx == 1 ? G : fx == 2 ? bh[x] : Gx; }
-        else if (fx0) { A = hv[x]; B = fy == 1 ? G : fy == 2 ? hv[x] : Gy; }
-        else if (half) { A = jj[x]; B = (fx == 2 && fy == 2) ? jj[x] : (fy == 2 ? hs : bs); }
+        if (fx0 && fy0) { A = g; B = g; }
+        else if (fy0) { A = bh[x]; B = fx == 1 ? g : fx == 2 ? bh[x] : gx; }
+        else if (fx0) { A = hv[x]; B = fy == 1 ? g : fy == 2 ? hv[x] : gy; }
+        else if (half) { A = jj; B = (fx == 2 && fy == 2) ? jj : (fy == 2 ? hs : bs); }
         else { A = bs; B = hs; }
         out[x] = (A + B + 1) >> 1;
     }

@@ -63,12 +63,12 @@ def test_decoder_js_api_holds_reordered_pictures():
 
 
 # single-picture launch kernels (engine environment -> the kernel it must run):
-# the default k_prep + k_wgpp (2 ping-pong row waves, 2 MC waves), k_wgpp with
-# 3 MC waves, the one-row-wave k_wg (with and without k_prep), and the
+# the default k_prep + k_wgpp (2 ping-pong row waves, 3 MC waves), k_wgpp with
+# 2 MC waves, the one-row-wave k_wg (with and without k_prep), and the
 # two-kernel k_mb + k_rows path
 KERNEL_MODES = [
     ({}, "k_wgpp"),
-    ({"H264MI_WG_NMC": "3"}, "k_wgpp"),
+    ({"H264MI_WG_NMC": "2"}, "k_wgpp"),
     ({"H264MI_WG_PP": "0"}, "k_wg"),
     ({"H264MI_WG_PP": "0", "H264MI_WG_NMC": "2"}, "k_wg"),
     ({"H264MI_WG_PP": "0", "H264MI_PREP": "0"}, "k_wg"),
