@@ -101,6 +101,7 @@ static int alloc_pic_buffers(h264mi_engine *e, int cap)
     // cleared granules / progress carry epoch 0, which no launch uses
     (void)hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st);
     (void)hipMemsetAsync(e->d_progress, 0, rows * 4, e->st);
+    (void)hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * np, e->st);
     memset(e->h_err, 0, sizeof(unsigned) * np);
     e->pipe_cap = cap;
     return 0;
@@ -256,7 +257,6 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.ring = e->nslots;
     a.base_pic = base_pic % e->nslots;
     if (grouped && !pipe && e->classic && e->ngroups > 1 && npics >= e->ngroups) return launch_groups(e, npics, a);
-    HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * npics, e->st));
     const bool wg = pipe || !e->classic;
     if (wg) {
         if (pipe) a.prof = NULL;
@@ -335,7 +335,6 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         HIPCHECK(hipGetLastError());
     }
     if (rec) (void)hipEventRecord(t2, e->st);
-    HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * npics, hipMemcpyDeviceToHost, e->st));
     if (prep) HIPCHECK(hipEventRecord(e->ev_wgdone[pbuf], e->st));
     return 0;
 }
@@ -361,7 +360,6 @@ static int launch_groups(h264mi_engine *e, int npics, ReconArgs a)
         ag.mbx = e->d_mbx + (size_t)p0 * e->nmbs * 32;
         ag.err = e->d_err + p0;
         ag.prof = NULL;
-        HIPCHECK(hipMemsetAsync(ag.err, 0, sizeof(unsigned) * n, gs));
         const bool rec = g == 0 && e->tev && e->tev_n < e->tev_cap;
         hipEvent_t t0 = rec ? e->tev[3 * e->tev_n] : NULL, t1 = rec ? e->tev[3 * e->tev_n + 1] : NULL,
                    t2 = rec ? e->tev[3 * e->tev_n + 2] : NULL;
@@ -372,7 +370,6 @@ static int launch_groups(h264mi_engine *e, int npics, ReconArgs a)
         hipLaunchKernelGGL(k_rows<false>, dim3(n * e->h), dim3(64), 0, gs, ag);
         HIPCHECK(hipGetLastError());
         if (rec) { (void)hipEventRecord(t2, gs); e->tev_n++; }
-        HIPCHECK(hipMemcpyAsync(e->h_err + p0, ag.err, sizeof(unsigned) * n, hipMemcpyDeviceToHost, gs));
     }
     e->stagger_pending = 0;
     return 0;
@@ -474,8 +471,11 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     HIPCHECK(hipStreamSynchronize(e->st2));
     for (int g = 0; g < H264MI_MAX_GROUPS; g++)
         if (e->gst[g]) HIPCHECK(hipStreamSynchronize(e->gst[g]));
+    // per-picture error flags OR-accumulate over every launch since the last
+    // sync (no per-launch reset): count the flagged picture slots, then clear
+    HIPCHECK(hipMemcpy(e->h_err, e->d_err, sizeof(unsigned) * e->pipe_cap, hipMemcpyDeviceToHost));
     for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
-    memset(e->h_err, 0, sizeof(unsigned) * e->pipe_cap);
+    HIPCHECK(hipMemset(e->d_err, 0, sizeof(unsigned) * e->pipe_cap));
     return 0;
 }
 

@@ -139,7 +139,9 @@ int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs,
 
 int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */
 int  h264mi_engine_sync(h264mi_engine *e);
-/* residual range errors seen since the last call (reference transform.c:181) */
+/* number of (launch, picture) slots flagged since the last call: residual
+ * range errors (reference transform.c:181) or a bounded wait that expired;
+ * flags accumulate over every launch and are collected by h264mi_engine_sync */
 uint32_t h264mi_engine_errors(h264mi_engine *e);
 /* average duration (us) of the last batch's kernels: [0] k_mb, [1] k_rows */
 int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
