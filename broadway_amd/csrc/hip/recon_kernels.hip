@@ -1188,6 +1188,17 @@ __device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn
 // sinking them into exec-masked blocks (each costs more scalar work than it
 // saves)
 #define MATERIALIZE(x) asm volatile("" : "+v"(x))
+// median of three = clamp lo <= x <= hi for lo <= hi, in this form one
+// v_med3_i32 (min(max(x, lo), hi) is two instructions unless both bounds are
+// constants)
+__device__ __forceinline__ int med3i(int x, int lo, int hi) { return min(max(x, lo), max(min(x, lo), hi)); }
+// c - 2 * x in one v_mad_i32_i24 (the compiler emits a shift and a subtract)
+__device__ __forceinline__ int mad_m2(int x, int c)
+{
+    int r;
+    asm("v_mad_i32_i24 %0, %1, -2, %2" : "=v"(r) : "v"(x), "v"(c));
+    return r;
+}
 
 // One edge of one line (8.7.2.3 / 8.7.2.4).  Per-lane constants: alpha,
 // beta; beta_ap = beta for luma, 0 for chroma (so a_p / a_q are false and
@@ -1202,15 +1213,21 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, const int b
     const int p2 = v[o + 1], p1 = v[o + 2], p0 = v[o + 3];
     const int q0 = v[o + 4], q1 = v[o + 5], q2 = v[o + 6];
     const int d0 = absd(p0, q0);
-    const bool f = bS != 0 && d0 < alpha && max(absd(p1, p0), absd(q1, q0)) < beta;
+    // filterSamples as one sign test: v_sad_u8 subtracts each threshold in
+    // its addend, one v_max3 joins the three
+    const int m0 = (int)__builtin_amdgcn_sad_u8((uint32_t)p0, (uint32_t)q0, (uint32_t)-alpha);
+    const int m1 = (int)__builtin_amdgcn_sad_u8((uint32_t)p1, (uint32_t)p0, (uint32_t)-beta);
+    const int m2 = (int)__builtin_amdgcn_sad_u8((uint32_t)q1, (uint32_t)q0, (uint32_t)-beta);
+    const bool f = bS != 0 && max(m0, max(m1, m2)) < 0;
     const bool ap = absd(p2, p0) < beta_ap, aq = absd(q2, q0) < beta_ap;
     // bS < 4
     const int tc0 = (int)__builtin_amdgcn_ubfe(tcs, (uint32_t)bS << 3, 8);    // bS = 4: offset 32 -> byte 0 (unused)
     const int tc = tc0 + (int)ap + (int)aq;
-    const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-    const int avg = (p0 + q0 + 1) >> 1;
-    int n_p1 = p1 + clip3(-tc0, tc0, (p2 + avg - (p1 << 1)) >> 1);
-    int n_q1 = q1 + clip3(-tc0, tc0, (q2 + avg - (q1 << 1)) >> 1);
+    const int d = med3i((((q0 - p0) << 2) + (p1 - q1) + 4) >> 3, -tc, tc);
+    const int avg = (int)__builtin_amdgcn_lerp((uint32_t)p0, (uint32_t)q0, 1u);    // (p0 + q0 + 1) >> 1 (v_lerp_u8)
+    const int ntc0 = -tc0;
+    int n_p1 = p1 + med3i((mad_m2(p1, p2) + avg) >> 1, ntc0, tc0);
+    int n_q1 = q1 + med3i((mad_m2(q1, q2) + avg) >> 1, ntc0, tc0);
     int n_p0 = clip255(p0 + d), n_q0 = clip255(q0 - d);
     MATERIALIZE(n_p1); MATERIALIZE(n_q1); MATERIALIZE(n_p0); MATERIALIZE(n_q0);
     int r_p2 = p2, r_q2 = q2;
