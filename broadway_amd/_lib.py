@@ -13,7 +13,9 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+# H264MI_LIB_DIR: load another build of the same libraries (A/B timing of
+# kernel variants in one process tree; tools/ab.sh)
+LIB_DIR = os.environ.get("H264MI_LIB_DIR") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 
 
 class NativeLibraryMissing(RuntimeError):

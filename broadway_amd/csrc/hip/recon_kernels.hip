@@ -2048,12 +2048,33 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         cp_src = (uint32_t)((int)(D - (const uint8_t *)&Gp) + off + step);
         cp_dst = lane < 32 ? (uint32_t)((int)(D - (const uint8_t *)&Gp) + off) : (uint32_t)((int)(junk - Lb) + lane * 4);
     }
-    // provisional entry dword of this lane (rows 12..15 of an MB's region, cols 0..15)
-    uint32_t prov_off;
+    // publishing: slot ls = le (0..23; lanes 24..63 repeat slots 16..23 /
+    // 0..23 with the same values) stores granule gi(ls).  Slots 0..7 are the
+    // 8 granules MB c+1's left edge patches (luma rows 12..15 / Cb, Cr rows
+    // 6..7, the dword holding columns 12..15 / 4..7) -- patch lane pj = ls
+    // publishes its own result, no cross-lane move; slots 8..23 the others.
+    uint32_t prov_off;      // the granule's provisional dword in the region (rows 12..15, cols 0..15)
+    int gi;
     {
-        const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-        prov_off = le < 16 ? (uint32_t)((int)(G.ry - Lb) + (16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4)
-                           : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 4 + qq * 4);
+        const int ls = le;
+        int yrow, yq, comp, row, qq;
+        bool luma;
+        if (ls < 8) {
+            luma = ls < 4;
+            yrow = ls & 3; yq = 3;
+            comp = (ls >> 1) & 1; row = ls & 1; qq = 1;
+        } else if (ls < 20) {
+            luma = true;
+            yrow = (ls - 8) / 3; yq = (ls - 8) % 3;
+            comp = row = qq = 0;
+        } else {
+            luma = false;
+            yrow = yq = 0;
+            comp = (ls - 20) >> 1; row = (ls - 20) & 1; qq = 0;
+        }
+        gi = luma ? yrow * 4 + yq : 16 + comp * 4 + row * 2 + qq;
+        prov_off = luma ? (uint32_t)((int)(G.ry - Lb) + (16 + yrow) * RY_S + 4 + yq * 4)
+                        : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 4 + qq * 4);
     }
     // ---- the hand-off to the row below, made by the wave that ran H(c):
     //      MB c's rows 12..15 are final except columns 13..15, which MB c+1's
@@ -2066,17 +2087,12 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     //      without waiting for the partner's V(c+1).
     const int pj = lane & 7;
     const bool pchroma = pj >= 4;
-    uint32_t pp_off;        // p side: cols 12..15 / 4..7 of this region's rows 12..15 / 6..7
-    int pq_off;             // q side: cols 0..3 of the ring slot's MB
+    int pq_off;             // q side: cols 0..3 of the ring slot's MB (p side: the lane's own provisional dword)
     {
         const int comp = (pj >> 1) & 1, row = pj & 1;
-        pp_off = !pchroma ? (uint32_t)((int)(G.ry - Lb) + (16 + pj) * RY_S + 16)
-                          : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 8);
         pq_off = !pchroma ? (12 + pj) * 16 : 256 + comp * 64 + (6 + row) * 8;
     }
-    // publishing lanes (le): the patched dwords come from patch lane pl_src
-    const bool is_patch = le < 16 ? (le & 3) == 3 : (le & 1);
-    const int pl_src = le < 16 ? (le >> 2) : 4 + ((le - 16) >> 2) * 2 + ((le >> 1) & 1);
+    const bool is_patch = le < 8;
     // own samples from the ring slot: luma all lanes, chroma lanes 0..31
     const uint32_t own_y_lds = (uint32_t)((int)(G.ry - Lb) + (orow + 4) * RY_S + 4 + oq * 4);
     const uint32_t own_c_lds = lane < 32 ? (uint32_t)((int)((ccomp ? G.rv : G.ru) - Lb) + (crow + 2) * RC_S + 4 + cq * 4)
@@ -2158,6 +2174,9 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             if (lane == 0) lds_st(&R->consumed, 0);
         }
         // ---- vertical edges
+        // (measured: reading the left halo straight from the partner's region
+        // inside V -- deblock_dir's pdelta -- and releasing it after the MB
+        // edge was 3 us per launch slower than this copy)
         if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT);
         wave_sync();
         PPT(1);
@@ -2186,18 +2205,26 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             uint32_t ent = *(const uint32_t *)(Lb + prov_off);
             if (more) {
                 const int s1 = (c + 1) & (RING_K - 1);
-                {   // MB c+1's MC output (normally long done; its wave waits for it too)
+                // MB c+1's MC output (normally long done): its flag and the
+                // slot data in one LDS round trip.  LDS serves one wave's
+                // accesses in order and the MC wave writes the slot before
+                // the flag, so data read after a ready flag is the slot's.
+                const uint32_t *dbn = (const uint32_t *)R->db[s1];
+                const int fl = lds_ld(&R->flag[s1]);
+                wave_sync();
+                uint32_t qdw = *(const uint32_t *)&R->px[s1][pq_off];
+                uint32_t bsw = dbn[1], t0 = dbn[pchroma ? 12 : 6], t1 = dbn[pchroma ? 13 : 7];
+                if (__builtin_amdgcn_readfirstlane(fl) != c + 2) {
                     unsigned spins = 0;
                     while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[s1])) != c + 2) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
                     }
                     wave_sync();
+                    qdw = *(const uint32_t *)&R->px[s1][pq_off];
+                    bsw = dbn[1]; t0 = dbn[pchroma ? 12 : 6]; t1 = dbn[pchroma ? 13 : 7];
                 }
-                const uint32_t pdw = *(const uint32_t *)(Lb + pp_off);
-                const uint32_t qdw = *(const uint32_t *)&R->px[s1][pq_off];
-                const uint32_t *dbn = (const uint32_t *)R->db[s1];
-                const uint32_t bsw = dbn[1], t0 = dbn[pchroma ? 12 : 6], t1 = dbn[pchroma ? 13 : 7];
+                const uint32_t pdw = ent;
                 int v[20];
 #pragma unroll
                 for (int x = 0; x < 4; x++) { v[x] = (pdw >> (8 * x)) & 255; v[4 + x] = (qdw >> (8 * x)) & 255; }
@@ -2209,10 +2236,9 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                 const uint32_t tcs = (((t0 >> 8) & 0xFFFF00u) | (t1 << 24)) + (pchroma ? 0x01010100u : 0u);
                 filt_line<true>(v, 0, bS, t0 & 255, (t0 >> 8) & 255, pchroma ? 0 : ((t0 >> 8) & 255), tcs);
                 const uint32_t newp = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
-                const uint32_t pv = (uint32_t)__builtin_amdgcn_ds_bpermute(pl_src << 2, (int)newp);
-                if (is_patch) ent = pv;
+                if (is_patch) ent = newp;
             }
-            st_gran(mbx_me + (size_t)c * 32 + le, ent, tag);
+            st_gran(mbx_me + (size_t)c * 32 + gi, ent, tag);
             if (prof && lane == 0) pmb[2] = wall_clock64();
         }
         // ---- off the chain again: frame stores, once per sample
