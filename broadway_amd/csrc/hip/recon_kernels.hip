@@ -2110,13 +2110,16 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool prof = PROF && a.prof != nullptr;
-    unsigned long long tc0 = 0, tc1;
+    unsigned long long tc0 = 0, tc1, tva = 0, tvd = 0;
 #define PPT(i) do { if (prof) { tc1 = clock64(); pt[i] += tc1 - tc0; tc0 = tc1; } } while (0)
     if (prof && w == 0 && lane == 0) a.prof[((size_t)r * a.npics + p) * 16] = wall_clock64();
 
     for (int c = w; c < W; c += 2) {
         if (prof) tc0 = clock64();
-        // per-MB stamps: [0] row-above entry c in hand (H(c) may start), [2] entry c-1 published
+        // per-MB stamps (100 MHz wall clock): [0] row-above entry c in hand (H(c)
+        // may start); [1] V(c) start (after the hdone wait and halo copy) in
+        // bits 0..31, V(c) end in bits 32..63; [2] entry c published in bits
+        // 0..31, H(c) end (hdone = c + 1) in bits 32..63
         unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
         const cu32p rw = recw + c * 24;
         const uint32_t h0 = rw[0];
@@ -2165,6 +2168,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             }
             wave_sync();
             PPT(3);
+            if (prof && lane == 0) tva = wall_clock64();
             const uint32_t hv = *(const uint32_t *)((const uint8_t *)&Gp + cp_src);
             *(uint32_t *)(Lb + cp_dst) = hv;
             wave_sync();
@@ -2180,10 +2184,14 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT);
         wave_sync();
         PPT(1);
+        if (prof && lane == 0) { if (c == 0) tva = wall_clock64(); pmb[1] = (tva & 0xFFFFFFFFull) | (wall_clock64() << 32); }
         // ---- top halo (row above's entry c final), horizontal edges
         if (has_up) {
             unsigned spins = 0;
             const bool mine = lane < 24;
+            // (measured: four staggered polls in flight made the hand-off
+            // slower -- median 0.83 vs 0.68 us; the poll's latency is the
+            // consumer CU's memory queue, MI355X_MICROARCH.md handoff-1to1)
             while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }
@@ -2199,6 +2207,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             wave_sync();
         }
         if (lane == 0) lds_st(&L.hdone, c + 1);
+        if (prof && lane == 0) tvd = wall_clock64();
         PPT(2);
         if (has_down) {
             const bool more = c + 1 < W;
@@ -2239,7 +2248,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                 if (is_patch) ent = newp;
             }
             st_gran(mbx_me + (size_t)c * 32 + gi, ent, tag);
-            if (prof && lane == 0) pmb[2] = wall_clock64();
+            if (prof && lane == 0) pmb[2] = (wall_clock64() & 0xFFFFFFFFull) | (tvd << 32);
         }
         // ---- off the chain again: frame stores, once per sample
         if (!last_row && c != W - 1) {
