@@ -57,6 +57,9 @@ def main(tag):
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
                "hbm_bytes_per_step": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    for extra in ("chain_s8.log", "chain_s1.log"):
+        if os.path.exists(os.path.join(src, extra)):
+            shutil.copy(os.path.join(src, extra), os.path.join(dst, f"{tag}_{extra}"))
     if os.path.exists(os.path.join(src, "bench.json")):
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
     print(json.dumps(out, indent=1))

@@ -7,8 +7,8 @@
 //           transposition), full / half exec
 // Variants of the filter body: 0 = filt_line (SGPR masks), 1 = VGPR masks.
 // Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 -o
-// broadway_amd/lib/ubench_filter tools/ubench_filter.hip; run on the GPU box.
-#include "../broadway_amd/csrc/hip/recon_kernels.hip"
+// tools/ubench/ubench_filter tools/ubench/ubench_filter.hip; run on the GPU box.
+#include "../../broadway_amd/csrc/hip/recon_kernels.hip"
 #include <cstdio>
 #include <cstring>
 #include <vector>
