@@ -70,6 +70,7 @@ struct h264mi_engine {
     // per-batch kernel timing (h264mi_engine_set_timing): event triples
     hipEvent_t *tev;
     int tev_cap, tev_n;
+    bool tev_single;        // single-kernel launches: t0 .. t2 only (one marker fewer between launches)
 };
 
 // per-picture buffers of one launch (deblocking records, intra residuals,
@@ -256,7 +257,10 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.S = npics / depth;
     a.ring = e->nslots;
     a.base_pic = base_pic % e->nslots;
-    if (grouped && !pipe && e->classic && e->ngroups > 1 && npics >= e->ngroups) return launch_groups(e, npics, a);
+    if (grouped && !pipe && e->classic && e->ngroups > 1 && npics >= e->ngroups) {
+        e->tev_single = false;
+        return launch_groups(e, npics, a);
+    }
     const bool wg = pipe || !e->classic;
     if (wg) {
         if (pipe) a.prof = NULL;
@@ -279,11 +283,13 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         }
         HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_wgdone[pbuf], 0));
         if (e->prep_serial) HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_wgdone[pbuf ^ 1], 0));   // experiment: no overlap
-        // start k_prep past the row kernel's start-up burst (all row
-        // workgroups' MC waves filling their rings at once): default 50 us
-        // per 8 x 1080p batch (measured: 17.5k vs 17.0k fps at 8 x 1080p),
-        // scaled by the batch's MB count; H264MI_PREP_DELAY_US overrides
-        const double dly = e->prep_delay_us >= 0 ? e->prep_delay_us : 50.0 * (double)(npics * e->nmbs) / (8.0 * 8160.0);
+        // start k_prep in the row kernel's tail, when the top rows have
+        // finished and their CUs are idle: its memory traffic beside live row
+        // chains lengthens their L2 hand-offs (k_wgpp 449 us with k_prep
+        // 120 us in, 404 at 50 us, 385 at 250-300 us; 8 x 1080p).  Default:
+        // 65 % of the picture's chain estimate W * 1.6 + H * 2.8 us (248 us
+        // at 1080p); H264MI_PREP_DELAY_US overrides
+        const double dly = e->prep_delay_us >= 0 ? e->prep_delay_us : 0.65 * (e->w * 1.6 + e->h * 2.8);
         if (dly > 0.5) hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, e->st2, (unsigned long long)(dly * 100.0));
         hipLaunchKernelGGL(k_prep, dim3((npics * e->nmbs + 3) / 4), dim3(256), 0, e->st2, a);
         HIPCHECK(hipGetLastError());
@@ -298,6 +304,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     const bool rec = e->timing || e->tev;
     if (rec) (void)hipEventRecord(t0, e->st);
     e->last_kernel = !wg ? "k_mb+k_rows" : pipe ? "k_wg" : (e->wg_pp && prep) ? "k_wgpp" : "k_wg";
+    e->tev_single = wg;
     if (!wg) {
         hipLaunchKernelGGL(k_mb, dim3(((npics * e->nmbs + 7) / 8) * 8), dim3(64), 0, e->st, a);
         HIPCHECK(hipGetLastError());
@@ -308,7 +315,6 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     } else {
         // one launch: row workgroups with in-workgroup MC (k_wg); the k_mb
         // slot of the timing is empty
-        if (rec) (void)hipEventRecord(t1, e->st);
         const dim3 grid(a.S * e->h * depth);
         const int nmc = e->wg_nmc;
         if (pipe) {
@@ -492,8 +498,12 @@ extern "C" int h264mi_engine_last_timing(h264mi_engine *e, float *us2)
     if (!e || !e->timing) return -1;
     float ms0 = 0, ms1 = 0;
     HIPCHECK(hipEventSynchronize(e->ev2));
-    HIPCHECK(hipEventElapsedTime(&ms0, e->ev0, e->ev1));
-    HIPCHECK(hipEventElapsedTime(&ms1, e->ev1, e->ev2));
+    if (e->tev_single) {
+        HIPCHECK(hipEventElapsedTime(&ms1, e->ev0, e->ev2));
+    } else {
+        HIPCHECK(hipEventElapsedTime(&ms0, e->ev0, e->ev1));
+        HIPCHECK(hipEventElapsedTime(&ms1, e->ev1, e->ev2));
+    }
     us2[0] = ms0 * 1000.f;
     us2[1] = ms1 * 1000.f;
     return 0;
@@ -523,8 +533,12 @@ extern "C" int h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, d
     double a = 0, b = 0;
     for (int i = 0; i < e->tev_n; i++) {
         float m0 = 0, m1 = 0;
-        HIPCHECK(hipEventElapsedTime(&m0, e->tev[3 * i], e->tev[3 * i + 1]));
-        HIPCHECK(hipEventElapsedTime(&m1, e->tev[3 * i + 1], e->tev[3 * i + 2]));
+        if (e->tev_single) {
+            HIPCHECK(hipEventElapsedTime(&m1, e->tev[3 * i], e->tev[3 * i + 2]));
+        } else {
+            HIPCHECK(hipEventElapsedTime(&m0, e->tev[3 * i], e->tev[3 * i + 1]));
+            HIPCHECK(hipEventElapsedTime(&m1, e->tev[3 * i + 1], e->tev[3 * i + 2]));
+        }
         a += m0 * 1000.0;
         b += m1 * 1000.0;
     }
