@@ -262,6 +262,37 @@ def cpu_baseline(streams, nframes, reps=10):
         shutil.rmtree(td, ignore_errors=True)
 
 
+def rgba_leg(torch, L, eng, S, w_mbs, h_mbs, reps=50):
+    """Decoder.js `rgb: true` output: the I420 -> RGBA
+    kernel (k_yuv2rgba, color.hip) over one reconstructed picture of each
+    stream (frame slot 0, resident in HBM), one launch per step, timed with
+    HIP events on the launch stream.  An HBM-bound elementwise kernel: 1.5 B
+    read + 4 B written per pixel are its algorithmic bytes."""
+    width, height = w_mbs * 16, h_mbs * 16
+    out = torch.empty(S * width * height * 4, dtype=torch.uint8, device="cuda")
+    base = eng.frame_ptr(0, 0)
+    stride = eng.frame_ptr(1, 0) - base if S > 1 else 0
+    st = torch.cuda.current_stream()
+    launch = lambda: L.h264mi_yuv2rgba_device(base, out.data_ptr(), width, height, S, stride, width * height * 4,
+                                              st.cuda_stream)
+    for _ in range(5):
+        assert launch() == 0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        launch()
+    e1.record(st)
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    alg = S * width * height * (1.5 + 4)
+    gbs = alg / (us * 1e-6) / 1e9
+    del out
+    return {"kernel": "k_yuv2rgba", "pictures_per_launch": S, "avg_launch_us": round(us, 2),
+            "frames_per_s": round(S / (us * 1e-6), 1), "alg_bytes_per_launch": int(alg),
+            "achieved_GBs": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "semantics": "per pixel DecoderPost.js yuv2rgbcalc (:514-560), RGBA bytes"}
+
+
 def end_to_end(streams, nframes, reps=3):
     """End-to-end decode through the product C-ABI: one
     broadway_amd/lib/h264mi_dec process per stream, all in parallel (one host
@@ -423,6 +454,7 @@ def main():
     n_checked = 0
     if not a.no_verify and rank == 0:
         ok, n_checked = verify(eng, caps, seeds, nframes, ring)
+    rgba = rgba_leg(torch, L, eng, S, w, h) if rank == 0 else None
 
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
@@ -478,6 +510,7 @@ def main():
             "wall_read_GBs": round(frame_read_gbs, 2),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "rgba_output": rgba,
             "bitexact_check": {"ok": ok, "frames_checked": n_checked, "residual_range_errors": errors},
             "prep_seconds": round(t_prep, 1),
             "hbm_resident_input_MB": round(resident / 1e6, 1),

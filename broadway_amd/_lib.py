@@ -146,6 +146,12 @@ def mi() -> C.CDLL:
     L.h264mi_engine_decode_pipelined.restype = i32
     L.h264mi_engine_read.argtypes = [vp, i32, i32, vp]
     L.h264mi_engine_read.restype = i32
+    L.h264mi_engine_read_rgba.argtypes = [vp, i32, i32, vp]
+    L.h264mi_engine_read_rgba.restype = i32
+    L.h264mi_yuv2rgba_device.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp]
+    L.h264mi_yuv2rgba_device.restype = i32
+    L.H264SwDecNextPictureRGBA.argtypes = [vp, C.POINTER(H264SwDecPicture), u32, vp]
+    L.H264SwDecNextPictureRGBA.restype = i32
     L.h264mi_engine_sync.argtypes = [vp]
     L.h264mi_engine_sync.restype = i32
     L.h264mi_engine_kernel.argtypes = [vp]

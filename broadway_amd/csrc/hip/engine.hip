@@ -3,6 +3,7 @@
 // (streams shard across GPUs with no collective; within a GPU
 // one launch reconstructs one picture from each stream of the batch).
 #include "recon_kernels.hip"
+#include "color.hip"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -71,6 +72,7 @@ struct h264mi_engine {
     hipEvent_t *tev;
     int tev_cap, tev_n;
     bool tev_single;        // single-kernel launches: t0 .. t2 only (one marker fewer between launches)
+    uint8_t *d_rgba;          // h264mi_engine_read_rgba staging (w*h*4 B, allocated on first use)
 };
 
 // per-picture buffers of one launch (deblocking records, intra residuals,
@@ -182,6 +184,7 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->st) (void)hipStreamSynchronize(e->st);
     if (e->st2) (void)hipStreamSynchronize(e->st2);
     free_pic_buffers(e);
+    (void)hipFree(e->d_rgba);
     (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
     (void)hipFree(e->d_pics); (void)hipFree(e->d_gjunk);
     (void)hipHostFree(e->h_rec); (void)hipHostFree(e->h_coef); (void)hipHostFree(e->h_pics);
@@ -580,6 +583,33 @@ extern "C" int h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_
     return 0;
 }
 
+// I420 -> RGBA (DecoderPost.js `rgb: true`, color.hip) for `npics` pictures
+// of width x height pixels at in + k * in_stride -> out + k * out_stride,
+// device pointers, on `stream` (NULL: the null stream); asynchronous
+extern "C" int h264mi_yuv2rgba_device(const void *d_i420, void *d_rgba, int width, int height, int npics,
+                                      size_t in_stride, size_t out_stride, void *stream)
+{
+    if (!d_i420 || !d_rgba || width <= 0 || height <= 0 || (width & 15) || (height & 15) || npics < 1) return -1;
+    const int nthr = (width >> 3) * (height >> 1);
+    hipLaunchKernelGGL(k_yuv2rgba, dim3((nthr + 255) / 256, npics), dim3(256), 0, (hipStream_t)stream,
+                       (const uint8_t *)d_i420, (uint8_t *)d_rgba, width, height, in_stride, out_stride);
+    HIPCHECK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int h264mi_engine_read_rgba(h264mi_engine *e, int stream, int slot, uint8_t *dst)
+{
+    if (!e || stream < 0 || stream >= e->nstreams || slot < 0 || slot >= e->nslots) return -1;
+    const size_t bytes = (size_t)e->nmbs * 256 * 4;
+    if (!e->d_rgba) HIPCHECK(hipMalloc(&e->d_rgba, bytes));
+    if (h264mi_yuv2rgba_device(e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot), e->d_rgba,
+                               e->w * 16, e->h * 16, 1, 0, 0, e->st))
+        return -1;
+    HIPCHECK(hipMemcpyAsync(dst, e->d_rgba, bytes, hipMemcpyDeviceToHost, e->st));
+    HIPCHECK(hipStreamSynchronize(e->st));
+    return 0;
+}
+
 extern "C" void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot)
 {
     if (!e) return NULL;
@@ -634,6 +664,12 @@ static int hb_read(void *vctx, int slot, uint8_t *dst)
     return h264mi_engine_read(c->e, 0, slot, dst);
 }
 
+static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    return h264mi_engine_read_rgba(c->e, 0, slot, dst);
+}
+
 static int hb_copy(void *vctx, int dst, int src)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
@@ -665,6 +701,7 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     be.configure = hb_configure;
     be.decode = hb_decode;
     be.read = hb_read;
+    be.read_rgba = hb_read_rgba;
     be.copy = hb_copy;
     be.destroy = hb_destroy;
     return be;

@@ -177,6 +177,24 @@ H264SwDecRet H264SwDecNextPicture(H264SwDecInst decInst, H264SwDecPicture *pOutp
     return H264SWDEC_PIC_RDY;
 }
 
+/* NextPicture with the picture converted to RGBA on the GPU (Decoder.js
+ * `rgb: true`, DecoderPost.js:82-97 + :420-560): rgba receives
+ * picWidth * picHeight * 4 bytes and pOutputPicture points to it. */
+H264SwDecRet H264SwDecNextPictureRGBA(H264SwDecInst decInst, H264SwDecPicture *pOutput, u32 flushBuffer, u8 *rgba)
+{
+    if (decInst == NULL || pOutput == NULL || rgba == NULL) return H264SWDEC_PARAM_ERR;
+    DecContainer *c = (DecContainer *)decInst;
+    if (flushBuffer) h264dec_flush(&c->dec);
+    uint32_t id, idr, em;
+    const uint8_t *pic = h264dec_next_output_rgba(&c->dec, &id, &idr, &em, rgba);
+    if (!pic) return H264SWDEC_OK;
+    pOutput->pOutputPicture = (u32 *)(void *)pic;
+    pOutput->picId = id;
+    pOutput->isIdrPicture = idr;
+    pOutput->nbrOfErrMBs = em;
+    return H264SWDEC_PIC_RDY;
+}
+
 /* ------------------------------------------------------------------------ */
 /* wasm / JS glue (Decoder.c): one global instance per process               */
 /* ------------------------------------------------------------------------ */

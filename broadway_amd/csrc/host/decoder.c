@@ -492,10 +492,19 @@ void h264dec_flush(H264Dec *d)
 
 const uint8_t *h264dec_next_output(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr, uint32_t *err_mbs)
 {
+    return h264dec_next_output_rgba(d, pic_id, is_idr, err_mbs, NULL);
+}
+
+/* rgba != NULL: the picture as RGBA (w*h*4 bytes) into rgba, converted by
+ * the backend (returns rgba) */
+const uint8_t *h264dec_next_output_rgba(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr, uint32_t *err_mbs,
+                                        uint8_t *rgba)
+{
+    if (rgba && !d->be.read_rgba) return NULL;
     const DpbOut *o = dpb_next_output(&d->dpb);
     if (!o) return NULL;
-    uint8_t *dst = d->out_frames + d->frame_bytes * (size_t)o->slot;
-    if (d->be.read(d->be.ctx, o->slot, dst)) return NULL;
+    uint8_t *dst = rgba ? rgba : d->out_frames + d->frame_bytes * (size_t)o->slot;
+    if (rgba ? d->be.read_rgba(d->be.ctx, o->slot, dst) : d->be.read(d->be.ctx, o->slot, dst)) return NULL;
     if (pic_id) *pic_id = (uint32_t)o->pic_id;
     if (is_idr) *is_idr = (uint32_t)o->is_idr;
     if (err_mbs) *err_mbs = (uint32_t)o->err_mbs;

@@ -24,6 +24,9 @@ typedef struct H264Backend {
     int  (*decode)(void *ctx, const PicBuild *pb, int cur_slot);
     /* copy slot as planar I420 (w*16 * h*16 * 3/2 bytes) to host memory */
     int  (*read)(void *ctx, int slot, uint8_t *dst);
+    /* copy slot converted to RGBA (w*16 * h*16 * 4 bytes, DecoderPost.js
+     * rgb output); NULL when the backend has no conversion */
+    int  (*read_rgba)(void *ctx, int slot, uint8_t *dst);
     /* copy one slot into another (error concealment of lost pictures) */
     int  (*copy)(void *ctx, int dst_slot, int src_slot);
     void (*destroy)(void *ctx);
@@ -88,6 +91,8 @@ void h264dec_flush(H264Dec *d);
 /* next output picture; returns host pointer to I420 data or NULL */
 const uint8_t *h264dec_next_output(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr,
                                    uint32_t *err_mbs);
+const uint8_t *h264dec_next_output_rgba(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr, uint32_t *err_mbs,
+                                        uint8_t *rgba);
 int  h264dec_valid_param_sets(const H264Dec *d);
 const Sps *h264dec_active_sps(const H264Dec *d);
 

@@ -14,10 +14,15 @@ of the wasm glue of Decoder/src/Decoder.c:44-162:
   (Decoder.c:122-134) and the DPB is never flushed (Decoder.c:140), so
   pictures held for display reordering are not emitted.
 
+* ``rgb: true`` (DecoderPost.js:82-97): ``onPictureDecoded`` receives a new
+  RGBA array (``width*height*4`` bytes) converted on the GPU with the
+  reference converter's per-pixel arithmetic (yuv2rgbcalc, :514-560) --
+  ``H264SwDecNextPictureRGBA`` instead of ``H264SwDecNextPicture``.
+
 Unlike the reference module (a single global instance) every ``Decoder`` has
 its own H264SwDec instance, so several streams can be decoded side by side.
-Reconstruction always runs on the GPU through libh264mi.so; ``rgb`` and
-``sliceMode`` (YUV->RGB conversion, per-slice workers) are not supported.
+Reconstruction always runs on the GPU through libh264mi.so; ``sliceMode``
+(per-slice web workers) is not supported.
 """
 from __future__ import annotations
 
@@ -39,8 +44,9 @@ def _now() -> float:
 class Decoder:
     def __init__(self, options: Optional[dict] = None):
         self.options = dict(options or {})
-        if self.options.get("rgb") or self.options.get("sliceMode"):
-            raise NotImplementedError("rgb / sliceMode output is not part of the MI355X path")
+        if self.options.get("sliceMode"):
+            raise NotImplementedError("sliceMode (per-slice workers) is not part of the MI355X path")
+        self._rgb = bool(self.options.get("rgb"))
         self._L = _lib.mi()
         inst = C.c_void_p()
         ret = self._L.H264SwDecInit(C.byref(inst), 0)
@@ -92,17 +98,31 @@ class Decoder:
         elif ret in (_lib.H264SWDEC_PIC_RDY_BUFF_NOT_EMPTY, _lib.H264SWDEC_PIC_RDY):
             inp.dataLen = 0
             self.pic_decode_number += 1
-            while L.H264SwDecNextPicture(self._inst, C.byref(self._pic), 0) == _lib.H264SWDEC_PIC_RDY:
-                self.pic_display_number += 1
-                self._emit(self._pic)
+            while True:
+                if self._rgb:
+                    w, h = self._info.picWidth, self._info.picHeight
+                    rgba = np.empty(w * h * 4, dtype=np.uint8)
+                    if L.H264SwDecNextPictureRGBA(self._inst, C.byref(self._pic), 0,
+                                                  rgba.ctypes.data) != _lib.H264SWDEC_PIC_RDY:
+                        break
+                    self.pic_display_number += 1
+                    self._emit(self._pic, rgba)
+                else:
+                    if L.H264SwDecNextPicture(self._inst, C.byref(self._pic), 0) != _lib.H264SWDEC_PIC_RDY:
+                        break
+                    self.pic_display_number += 1
+                    self._emit(self._pic)
         elif ret in (_lib.H264SWDEC_STRM_PROCESSED, _lib.H264SWDEC_STRM_ERR):
             inp.dataLen = 0
         return ret
 
-    def _emit(self, pic) -> None:
+    def _emit(self, pic, rgba=None) -> None:
         w, h = self._info.picWidth, self._info.picHeight
-        n = w * h * 3 // 2
-        buf = np.ctypeslib.as_array(C.cast(pic.pOutputPicture, C.POINTER(C.c_uint8)), shape=(n,))
+        if rgba is not None:
+            buf = rgba
+        else:
+            n = w * h * 3 // 2
+            buf = np.ctypeslib.as_array(C.cast(pic.pOutputPicture, C.POINTER(C.c_uint8)), shape=(n,))
         infos = None
         if self.infoAr:
             infos = self.infoAr

@@ -120,6 +120,17 @@ class Engine:
             raise RuntimeError("h264mi_engine_read failed")
         return out
 
+    def read_rgba(self, stream: int, slot: int) -> np.ndarray:
+        """The slot converted to RGBA on the GPU (Decoder.js `rgb: true`)."""
+        out = np.empty(self.frame_bytes // 3 * 8, dtype=np.uint8)       # w*h*1.5 -> w*h*4
+        if self._L.h264mi_engine_read_rgba(self._h, stream, slot, out.ctypes.data) != 0:
+            raise RuntimeError("h264mi_engine_read_rgba failed")
+        return out
+
+    def frame_ptr(self, stream: int, slot: int) -> int:
+        """Device address of a frame slot (I420, frame_bytes)."""
+        return int(self._L.h264mi_engine_frame_ptr(self._h, stream, slot))
+
     def sync(self) -> None:
         if self._L.h264mi_engine_sync(self._h) != 0:
             raise RuntimeError("h264mi_engine_sync failed")

@@ -101,6 +101,12 @@ H264SwDecRet H264SwDecNextPicture(H264SwDecInst decInst, H264SwDecPicture *pOutp
 H264SwDecRet H264SwDecGetInfo(H264SwDecInst decInst, H264SwDecInfo *pDecInfo);  /* :204 */
 void H264SwDecRelease(H264SwDecInst decInst);                                    /* :259 */
 H264SwDecApiVersion H264SwDecGetAPIVersion(void);                                /* :487 */
+/* NextPicture, the picture converted to RGBA on the GPU: what Decoder.js
+ * delivers with `rgb: true` (templates/DecoderPost.js:82-97, the asm.js
+ * converter :322-560, per pixel yuv2rgbcalc :514-560).  rgba: picWidth *
+ * picHeight * 4 bytes; pOutput->pOutputPicture = rgba.  No reference C
+ * counterpart: the reference converts in JavaScript. */
+H264SwDecRet H264SwDecNextPictureRGBA(H264SwDecInst decInst, H264SwDecPicture *pOutput, u32 flushBuffer, u8 *rgba);
 
 /* ---------------------------------------------------------------------- */
 /* 2. Broadway glue (reference Decoder/src/Decoder.c:44-185, make.py:39)   */
@@ -138,6 +144,14 @@ int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs,
                                 const void *d_pics);
 
 int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */
+/* D2H of a slot as RGBA (w*16 * h*16 * 4 bytes), converted on the GPU
+ * (DecoderPost.js yuv2rgbcalc :514-560 per pixel) */
+int  h264mi_engine_read_rgba(h264mi_engine *e, int stream, int slot, uint8_t *dst);
+/* the conversion kernel on device buffers: npics MB-aligned I420 pictures
+ * of width x height (multiples of 16) at d_i420 + k * in_stride ->
+ * d_rgba + k * out_stride; asynchronous on `hip_stream` (NULL: null stream) */
+int  h264mi_yuv2rgba_device(const void *d_i420, void *d_rgba, int width, int height, int npics,
+                            size_t in_stride, size_t out_stride, void *hip_stream);
 int  h264mi_engine_sync(h264mi_engine *e);
 /* number of (launch, picture) slots flagged since the last call: residual
  * range errors (reference transform.c:181) or a bounded wait that expired;

@@ -42,6 +42,8 @@ def lib() -> C.CDLL:
         L.oracle_replay_frame.argtypes = [C.c_void_p, C.c_int]
         L.oracle_replay_frame.restype = C.c_void_p
         L.oracle_replay_free.argtypes = [C.c_void_p]
+        L.oracle_yuv2rgba.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        L.oracle_yuv2rgba.restype = None
         _L = L
     return _L
 
@@ -107,3 +109,13 @@ def refdec_frames(stream: bytes, no_reorder: bool = False) -> List[bytes]:
         data = open(yuv, "rb").read() if os.path.exists(yuv) else b""
     fb = w * h * 3 // 2 if w else 0
     return [data[i:i + fb] for i in range(0, len(data), fb)] if fb else []
+
+
+def yuv2rgba(i420, width: int, height: int) -> bytes:
+    """Decoder.js `rgb: true` conversion of one MB-aligned I420 picture
+    (oracle_yuv2rgba, restating DecoderPost.js:420-560): width*height*4 bytes RGBA."""
+    src = np.ascontiguousarray(np.frombuffer(bytes(i420), dtype=np.uint8))
+    assert src.size == width * height * 3 // 2
+    out = np.empty(width * height * 4, dtype=np.uint8)
+    lib().oracle_yuv2rgba(src.ctypes.data, width, height, out.ctypes.data)
+    return out.tobytes()

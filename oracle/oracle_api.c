@@ -105,3 +105,30 @@ int oracle_replay_picture(void *ctx, const void *rec, const int16_t *coef, int w
 }
 const uint8_t *oracle_replay_frame(void *ctx, int slot) { return oracle_ctx_frame(ctx, slot); }
 void oracle_replay_free(void *ctx) { oracle_ctx_destroy(ctx); }
+
+/* I420 -> RGBA of Decoder.js's `rgb: true` output, restated from the
+ * reference's asm.js converter: per pixel yuv2rgbcalc
+ * (templates/DecoderPost.js:514-560) -- a0 = 1192 (y-16), R = (a0 + 1634
+ * (v-128)) >> 10, G = (a0 - 832 (v-128) - 400 (u-128)) >> 10, B = (a0 + 2066
+ * (u-128)) >> 10, each clamped to [0,255] (:541-549), stored as the word
+ * 255 << 24 | B << 16 | G << 8 | R (:551-558) -- over the picture in 2x2
+ * blocks sharing one (u, v) (doit, :420-505).  Plain scalar loops; the
+ * (y, u, v) result cache of the reference changes no value. */
+void oracle_yuv2rgba(const uint8_t *i420, int width, int height, uint8_t *rgba)
+{
+    const uint8_t *Y = i420, *U = i420 + (size_t)width * height;
+    const uint8_t *V = U + (size_t)(width / 2) * (height / 2);
+    for (int r = 0; r < height; r++)
+        for (int c = 0; c < width; c++) {
+            const int y = Y[(size_t)r * width + c];
+            const int u = U[(size_t)(r / 2) * (width / 2) + c / 2] - 128;
+            const int v = V[(size_t)(r / 2) * (width / 2) + c / 2] - 128;
+            const int a0 = 1192 * (y - 16);
+            int R = (a0 + 1634 * v) >> 10, G = (a0 - 832 * v - 400 * u) >> 10, B = (a0 + 2066 * u) >> 10;
+            R = R < 0 ? 0 : R > 255 ? 255 : R;
+            G = G < 0 ? 0 : G > 255 ? 255 : G;
+            B = B < 0 ? 0 : B > 255 ? 255 : B;
+            uint8_t *o = rgba + ((size_t)r * width + c) * 4;
+            o[0] = (uint8_t)R; o[1] = (uint8_t)G; o[2] = (uint8_t)B; o[3] = 255;
+        }
+}
