@@ -12,11 +12,11 @@
 // result cache never changes a value (every word has A = 255), so it has no
 // counterpart here.
 //
-// HBM-bound elementwise kernel: 1.5 B read + 4 B written per pixel.  One
-// thread = 2 rows x 8 columns (one chroma row pair x 4 chroma samples):
-// Y as two 8-byte loads, U / V one dword each, output four 16-byte stores;
-// lanes of a wave cover 512 consecutive columns, so every access is
-// contiguous across the wave.
+// HBM-bound elementwise kernel: 1.5 B read + 4 B written per pixel.  A
+// thread converts two 4-column groups f and f + 64 of a 128-group chunk in
+// two rows: each wave-wide load / store instruction then covers one
+// contiguous span (64 x 4 B of Y, 64 x 2 B of U or V, 64 x 16 B of RGBA),
+// two at a row end.
 
 __device__ __forceinline__ uint32_t rgba_px(int y, int cr, int cg, int cb)
 {
@@ -27,39 +27,47 @@ __device__ __forceinline__ uint32_t rgba_px(int y, int cr, int cg, int cb)
     return 0xFF000000u | ((uint32_t)b << 16) | ((uint32_t)g << 8) | (uint32_t)r;
 }
 
-// grid: (ceil(width/8 * height/2 / 256), npics); in[p] at in + p * in_stride
-__global__ __launch_bounds__(256) void k_yuv2rgba(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int width,
-                                                  int height, size_t in_stride, size_t out_stride)
+// one 4-column group (2 chroma samples) of two rows
+__device__ __forceinline__ void rgba_group(const uint8_t *Y, const uint8_t *U, const uint8_t *V, uint8_t *O,
+                                           int width, size_t yo, size_t co)
 {
-    const int qw = width >> 3;                      // 8-column groups per row
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= qw * (height >> 1)) return;
-    const int y2 = t / qw, xq = t - y2 * qw;
+    const uint32_t y0 = *(const uint32_t *)(Y + yo), y1 = *(const uint32_t *)(Y + yo + width);
+    const uint32_t u2 = *(const uint16_t *)(U + co), v2 = *(const uint16_t *)(V + co);
+    uint32_t o0[4], o1[4];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const int u = (int)((u2 >> (8 * k)) & 255) - 128, v = (int)((v2 >> (8 * k)) & 255) - 128;
+        const int cr = 1634 * v, cg = -832 * v - 400 * u, cb = 2066 * u;
+        o0[2 * k] = rgba_px((int)((y0 >> (16 * k)) & 255), cr, cg, cb);
+        o0[2 * k + 1] = rgba_px((int)((y0 >> (16 * k + 8)) & 255), cr, cg, cb);
+        o1[2 * k] = rgba_px((int)((y1 >> (16 * k)) & 255), cr, cg, cb);
+        o1[2 * k + 1] = rgba_px((int)((y1 >> (16 * k + 8)) & 255), cr, cg, cb);
+    }
+    // streaming output (nothing here reads it back): non-temporal stores
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w0 = {o0[0], o0[1], o0[2], o0[3]}, w1 = {o1[0], o1[1], o1[2], o1[3]};
+    __builtin_nontemporal_store(w0, (u32x4 *)(O + yo * 4));
+    __builtin_nontemporal_store(w1, (u32x4 *)(O + (yo + width) * 4));
+}
+
+// grid: (ceil(groups / 128) blocks of 64 threads, npics), groups = the
+// picture's (row pair, 4-column group) pairs in raster order, so no lane
+// idles at row ends; picture k at in + k * in_stride -> out + k * out_stride
+__global__ __launch_bounds__(64) void k_yuv2rgba(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int width,
+                                                 int height, size_t in_stride, size_t out_stride)
+{
+    const int ng = width >> 2;                      // 4-column groups per row
+    const int nf = ng * (height >> 1);
     const uint8_t *Y = in + blockIdx.y * in_stride;
     const uint8_t *U = Y + (size_t)width * height;
     const uint8_t *V = U + (size_t)(width >> 1) * (height >> 1);
-    const size_t yo = (size_t)(2 * y2) * width + 8 * xq;
-    const size_t co = (size_t)y2 * (width >> 1) + 4 * xq;
-    const uint2 y0 = *(const uint2 *)(Y + yo);
-    const uint2 y1 = *(const uint2 *)(Y + yo + width);
-    const uint32_t u4 = *(const uint32_t *)(U + co);
-    const uint32_t v4 = *(const uint32_t *)(V + co);
-    uint32_t o0[8], o1[8];
+    uint8_t *O = out + blockIdx.y * out_stride;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int u = (int)((u4 >> (8 * k)) & 255) - 128, v = (int)((v4 >> (8 * k)) & 255) - 128;
-        const int cr = 1634 * v, cg = -832 * v - 400 * u, cb = 2066 * u;
-        const uint32_t a = k < 2 ? y0.x : y0.y, b = k < 2 ? y1.x : y1.y;
-        const int s = 16 * (k & 1);
-        o0[2 * k] = rgba_px((int)((a >> s) & 255), cr, cg, cb);
-        o0[2 * k + 1] = rgba_px((int)((a >> (s + 8)) & 255), cr, cg, cb);
-        o1[2 * k] = rgba_px((int)((b >> s) & 255), cr, cg, cb);
-        o1[2 * k + 1] = rgba_px((int)((b >> (s + 8)) & 255), cr, cg, cb);
+    for (int h = 0; h < 2; h++) {
+        const int f = blockIdx.x * 128 + h * 64 + (int)threadIdx.x;
+        if (f < nf) {
+            const int y2 = f / ng, g = f - y2 * ng;
+            rgba_group(Y, U, V, O, width, (size_t)(2 * y2) * width + 4 * g, (size_t)y2 * (width >> 1) + 2 * g);
+        }
     }
-    uint8_t *O = out + blockIdx.y * out_stride + yo * 4;
-    uint4 *r0 = (uint4 *)O, *r1 = (uint4 *)(O + (size_t)width * 4);
-    r0[0] = make_uint4(o0[0], o0[1], o0[2], o0[3]);
-    r0[1] = make_uint4(o0[4], o0[5], o0[6], o0[7]);
-    r1[0] = make_uint4(o1[0], o1[1], o1[2], o1[3]);
-    r1[1] = make_uint4(o1[4], o1[5], o1[6], o1[7]);
 }

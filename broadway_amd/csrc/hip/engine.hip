@@ -590,8 +590,8 @@ extern "C" int h264mi_yuv2rgba_device(const void *d_i420, void *d_rgba, int widt
                                       size_t in_stride, size_t out_stride, void *stream)
 {
     if (!d_i420 || !d_rgba || width <= 0 || height <= 0 || (width & 15) || (height & 15) || npics < 1) return -1;
-    const int nthr = (width >> 3) * (height >> 1);
-    hipLaunchKernelGGL(k_yuv2rgba, dim3((nthr + 255) / 256, npics), dim3(256), 0, (hipStream_t)stream,
+    const int nblk = ((height >> 1) * (width >> 2) + 127) >> 7;
+    hipLaunchKernelGGL(k_yuv2rgba, dim3(nblk, npics), dim3(64), 0, (hipStream_t)stream,
                        (const uint8_t *)d_i420, (uint8_t *)d_rgba, width, height, in_stride, out_stride);
     HIPCHECK(hipGetLastError());
     return 0;
