@@ -7,10 +7,12 @@
 //   d.onPictureDecoded = function (buffer, width, height, infos) { ... };
 //   d.decode(nalU8Array, parInfo);          // synchronous, one NAL per call
 //
-// buffer: MB-aligned planar I420 (width*height*3/2 bytes, no cropping).
+// buffer: MB-aligned planar I420 (width*height*3/2 bytes, no cropping), or
+//         with {rgb: true} RGBA (width*height*4 bytes) converted on the GPU
+//         with the per-pixel arithmetic of DecoderPost.js's yuv2rgbcalc.
 // infos:  parInfo objects passed since the last picture, stamped with
 //         startDecoding / finishDecoding (DecoderPost.js:77-103, :277-281).
-// Not supported (outside the reconstruction path): options.rgb, sliceMode.
+// Not supported (outside the reconstruction path): sliceMode.
 "use strict";
 var path = require("path");
 var native = require(process.env.BROADWAY_NATIVE ||
@@ -23,12 +25,12 @@ function nowValue() {
 
 function Decoder(parOptions) {
   this.options = parOptions || {};
-  if (this.options.rgb || this.options.sliceMode) {
-    throw new Error("rgb / sliceMode output is not part of the MI355X path");
+  if (this.options.sliceMode) {
+    throw new Error("sliceMode output is not part of the MI355X path");
   }
   this.infoAr = [];
   this.onPictureDecoded = function (buffer, width, height, infos) {};
-  this._h = native.create(0);
+  this._h = native.create(0, this.options.rgb ? 1 : 0);
   var self = this;
   this._onPic = function (buffer, width, height) {
     var infos;

@@ -5,7 +5,9 @@
  *
  * Native surface (one H264SwDec instance per JS Decoder, unlike the single
  * global instance of the wasm module, Decoder.c:21-25):
- *   create(noOutputReordering)            -> handle (external)
+ *   create(noOutputReordering, rgb)       -> handle (external); rgb != 0:
+ *       pictures arrive as RGBA (width*height*4 bytes), converted on the GPU
+ *       (H264SwDecNextPictureRGBA; DecoderPost.js rgb option :82-97)
  *   decode(handle, Uint8Array, onPicture) -> undefined
  *       runs the broadwayDecode loop of Decoder.c:44-162 over the bytes:
  *       HDRS_RDY -> GetInfo; PIC_RDY -> drain NextPicture and call
@@ -26,6 +28,7 @@ typedef struct {
     H264SwDecInst inst;
     H264SwDecInfo info;
     u32 pic_decode;
+    u32 rgb;
 } JsDec;
 
 #define CHECK(env, call)                                                  \
@@ -45,11 +48,12 @@ static void finalize_dec(napi_env env, void *data, void *hint)
 
 static napi_value js_create(napi_env env, napi_callback_info cbi)
 {
-    size_t argc = 1;
-    napi_value argv[1], out;
+    size_t argc = 2;
+    napi_value argv[2], out;
     CHECK(env, napi_get_cb_info(env, cbi, &argc, argv, NULL, NULL));
-    uint32_t no_reorder = 0;
+    uint32_t no_reorder = 0, rgb = 0;
     if (argc >= 1) napi_get_value_uint32(env, argv[0], &no_reorder);
+    if (argc >= 2) napi_get_value_uint32(env, argv[1], &rgb);
     JsDec *d = (JsDec *)calloc(1, sizeof(JsDec));
     if (!d) { napi_throw_error(env, NULL, "out of memory"); return NULL; }
     if (H264SwDecInit(&d->inst, no_reorder) != H264SWDEC_OK) {
@@ -58,6 +62,7 @@ static napi_value js_create(napi_env env, napi_callback_info cbi)
         return NULL;
     }
     d->pic_decode = 1;
+    d->rgb = rgb != 0;
     CHECK(env, napi_create_external(env, d, finalize_dec, NULL, &out));
     return out;
 }
@@ -112,15 +117,28 @@ static napi_value js_decode(napi_env env, napi_callback_info cbi)
         case H264SWDEC_PIC_RDY:
             in.dataLen = 0;                      /* Decoder.c:130 */
             d->pic_decode++;
-            while (H264SwDecNextPicture(d->inst, &pic, 0) == H264SWDEC_PIC_RDY) {
-                size_t n = (size_t)d->info.picWidth * d->info.picHeight * 3 / 2;
+            for (;;) {
+                const size_t px = (size_t)d->info.picWidth * d->info.picHeight;
                 napi_value view, args[3], res;
-                /* the picture is borrowed DPB memory (dpb.c:1443): hand JS a
-                 * copy, as SoftAVC.cpp:461-462 does */
-                if (napi_create_buffer_copy(env, n, pic.pOutputPicture, NULL, &view) != napi_ok) {
-                    free(buf);
-                    napi_throw_error(env, NULL, "cannot allocate picture buffer");
-                    return NULL;
+                if (d->rgb) {
+                    /* RGBA straight into a new JS Buffer (DecoderPost.js hands
+                     * onPictureDecoded a fresh copy, :89-95) */
+                    void *dst = NULL;
+                    if (napi_create_buffer(env, px * 4, &dst, &view) != napi_ok) {
+                        free(buf);
+                        napi_throw_error(env, NULL, "cannot allocate picture buffer");
+                        return NULL;
+                    }
+                    if (H264SwDecNextPictureRGBA(d->inst, &pic, 0, (u8 *)dst) != H264SWDEC_PIC_RDY) break;
+                } else {
+                    if (H264SwDecNextPicture(d->inst, &pic, 0) != H264SWDEC_PIC_RDY) break;
+                    /* the picture is borrowed DPB memory (dpb.c:1443): hand JS a
+                     * copy, as SoftAVC.cpp:461-462 does */
+                    if (napi_create_buffer_copy(env, px * 3 / 2, pic.pOutputPicture, NULL, &view) != napi_ok) {
+                        free(buf);
+                        napi_throw_error(env, NULL, "cannot allocate picture buffer");
+                        return NULL;
+                    }
                 }
                 args[0] = view;
                 napi_create_uint32(env, d->info.picWidth, &args[1]);

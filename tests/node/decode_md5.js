@@ -1,6 +1,7 @@
 // Decode an Annex-B file through bindings/node/Decoder.js (one NAL per
 // decode() call, as Player/mp4.js feeds the wasm decoder) and print one JSON
-// line: {"width", "height", "frames": [md5...]}.
+// line: {"width", "height", "frames": [md5...]}.  A third argument "rgb"
+// decodes with {rgb: true} (RGBA pictures).
 "use strict";
 var fs = require("fs");
 var crypto = require("crypto");
@@ -15,7 +16,7 @@ for (var i = 0; i + 3 <= data.length; i++) {
   }
 }
 var out = {width: 0, height: 0, frames: [], infos: 0};
-var d = new Decoder({});
+var d = new Decoder({rgb: process.argv[3] === "rgb"});
 d.onPictureDecoded = function (buffer, width, height, infos) {
   out.width = width;
   out.height = height;

@@ -49,3 +49,26 @@ def test_node_decoder_vs_reference(name):
     assert (out["width"], out["height"]) == (c["width"], c["height"])
     assert out["frames"] == c["frames"]
     assert out["infos"] == len(c["frames"]) or out["infos"] > 0
+
+
+@need_node
+@pytest.mark.gpu
+def test_node_decoder_rgb_option():
+    """new Decoder({rgb: true}): RGBA pictures, each the conversion of the
+    reference's I420 picture (DecoderPost.js yuv2rgbcalc, oracle restatement)."""
+    import hashlib
+    import oracle as O
+    c = cases()["small_ip_8x6_2sl"]
+    s = stream(c)
+    frames, _, w, h, _ = O.decode(s)
+    assert [hashlib.md5(f).hexdigest() for f in frames] == c["frames"]
+    want = [hashlib.md5(O.yuv2rgba(f, w, h)).hexdigest() for f in frames]
+    with tempfile.TemporaryDirectory() as td:
+        p = os.path.join(td, "s.h264")
+        open(p, "wb").write(s)
+        r = subprocess.run([NODE, os.path.join(ROOT, "tests", "node", "decode_md5.js"), p, "rgb"],
+                           capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert (out["width"], out["height"]) == (w, h)
+    assert out["frames"] == want
