@@ -291,8 +291,12 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         // chains lengthens their L2 hand-offs (k_wgpp 449 us with k_prep
         // 120 us in, 404 at 50 us, 385 at 250-300 us; 8 x 1080p).  Default:
         // 65 % of the picture's chain estimate W * 1.6 + H * 2.8 us (248 us
-        // at 1080p); H264MI_PREP_DELAY_US overrides
-        const double dly = e->prep_delay_us >= 0 ? e->prep_delay_us : 0.65 * (e->w * 1.6 + e->h * 2.8);
+        // at 1080p); H264MI_PREP_DELAY_US overrides.  Only for device-
+        // resident batches queued back to back (decode_device): a host-staged
+        // batch (the H264SwDec path, one picture per host parse) finds the
+        // GPU idle, and its k_prep must not wait at all.
+        const double dly = e->prep_delay_us >= 0 ? e->prep_delay_us
+                           : grouped ? 0.65 * (e->w * 1.6 + e->h * 2.8) : 0.0;
         if (dly > 0.5) hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, e->st2, (unsigned long long)(dly * 100.0));
         hipLaunchKernelGGL(k_prep, dim3((npics * e->nmbs + 3) / 4), dim3(256), 0, e->st2, a);
         HIPCHECK(hipGetLastError());
