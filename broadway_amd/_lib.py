@@ -162,6 +162,8 @@ def mi() -> C.CDLL:
     L.h264mi_engine_last_timing.restype = i32
     L.h264mi_engine_set_timing.argtypes = [vp, i32]
     L.h264mi_engine_set_timing.restype = i32
+    L.h264mi_engine_set_timing_stride.argtypes = [vp, i32]
+    L.h264mi_engine_set_timing_stride.restype = i32
     L.h264mi_engine_timing_report.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i32)]
     L.h264mi_engine_timing_report.restype = i32
     L.h264mi_engine_profile.argtypes = [vp, i32, C.POINTER(C.c_uint64), sz]

@@ -71,6 +71,7 @@ struct h264mi_engine {
     // per-batch kernel timing (h264mi_engine_set_timing): event triples
     hipEvent_t *tev;
     int tev_cap, tev_n;
+    int tev_stride, tev_seq;  // record every tev_stride-th launch (h264mi_engine_set_timing_stride)
     bool tev_single;        // single-kernel launches: t0 .. t2 only (one marker fewer between launches)
     uint8_t *d_rgba;          // h264mi_engine_read_rgba staging (w*h*4 B, allocated on first use)
 };
@@ -304,11 +305,13 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         HIPCHECK(hipStreamWaitEvent(e->st, e->ev_prep, 0));
     }
     hipEvent_t t0 = e->ev0, t1 = e->ev1, t2 = e->ev2;
-    if (e->tev && e->tev_n < e->tev_cap) {
+    bool rec_tev = false;
+    if (e->tev && e->tev_n < e->tev_cap && e->tev_seq++ % (e->tev_stride > 0 ? e->tev_stride : 1) == 0) {
         t0 = e->tev[3 * e->tev_n]; t1 = e->tev[3 * e->tev_n + 1]; t2 = e->tev[3 * e->tev_n + 2];
         e->tev_n++;
+        rec_tev = true;
     }
-    const bool rec = e->timing || e->tev;
+    const bool rec = e->timing || rec_tev;
     if (rec) (void)hipEventRecord(t0, e->st);
     e->last_kernel = !wg ? "k_mb+k_rows" : pipe ? "k_wg" : (e->wg_pp && prep) ? "k_wgpp" : "k_wg";
     e->tev_single = wg;
@@ -525,11 +528,20 @@ extern "C" int h264mi_engine_set_timing(h264mi_engine *e, int max_batches)
         e->tev = NULL;
     }
     e->tev_cap = e->tev_n = 0;
+    e->tev_seq = 0;
     if (max_batches <= 0) return 0;
     e->tev = (hipEvent_t *)calloc((size_t)max_batches * 3, sizeof(hipEvent_t));
     if (!e->tev) return -1;
     for (int i = 0; i < 3 * max_batches; i++) HIPCHECK(hipEventCreate(&e->tev[i]));
     e->tev_cap = max_batches;
+    return 0;
+}
+
+extern "C" int h264mi_engine_set_timing_stride(h264mi_engine *e, int stride)
+{
+    if (!e || stride < 1) return -1;
+    e->tev_stride = stride;
+    e->tev_seq = 0;
     return 0;
 }
 

@@ -148,9 +148,12 @@ class Engine:
             return None
         return float(v[0]), float(v[1])
 
-    def set_timing(self, max_batches: int) -> None:
+    def set_timing(self, max_batches: int, stride: int = 1) -> None:
+        """HIP-event timing of up to max_batches launches, every stride-th one."""
         if self._L.h264mi_engine_set_timing(self._h, int(max_batches)) != 0:
             raise RuntimeError("h264mi_engine_set_timing failed")
+        if self._L.h264mi_engine_set_timing_stride(self._h, int(stride)) != 0:
+            raise RuntimeError("h264mi_engine_set_timing_stride failed")
 
     def timing_report(self):
         a, b, n = C.c_double(), C.c_double(), C.c_int()

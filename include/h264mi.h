@@ -163,6 +163,9 @@ int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
  * record up to max_batches batches (0 disables); the report syncs and returns
  * the summed durations of k_mb and of k_rows, in microseconds */
 int  h264mi_engine_set_timing(h264mi_engine *e, int max_batches);
+/* time only every stride-th launch (the event markers between launches cost
+ * the stream a few us each; default 1) */
+int  h264mi_engine_set_timing_stride(h264mi_engine *e, int stride);
 int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches);
 /* frame-pipelined batches: one launch reconstructs `depth` consecutive
  * pictures of each of `nstreams` streams, and a picture's motion
