@@ -69,6 +69,13 @@ static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_
         zeros = 0;
         int invalid = 0;
         for (;;) {
+            if (zeros == 0) {
+                /* runs of non-zero bytes change nothing but the position */
+                const uint8_t *z = (const uint8_t *)memchr(p, 0, len - cnt);
+                if (!z) { p += len - cnt; cnt = len; size = cnt - init; break; }
+                cnt += (uint32_t)(z - p);
+                p = z;
+            }
             uint8_t b = *p++;
             cnt++;
             if (!b) zeros++;
@@ -102,6 +109,15 @@ static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_
     if (emul) {
         int zc = 0;
         for (uint32_t i = 0; i < size; i++) {
+            if (zc == 0) {
+                /* copy up to the next zero byte in one go */
+                const uint8_t *z = (const uint8_t *)memchr(src + i, 0, size - i);
+                const uint32_t n = z ? (uint32_t)(z - (src + i)) : size - i;
+                memcpy(d->rbsp + w, src + i, n);
+                w += n;
+                i += n;
+                if (i == size) break;
+            }
             uint8_t b = src[i];
             if (zc == 2 && b == 3) {
                 if (i == size - 1 || src[i + 1] > 3) return -1;
