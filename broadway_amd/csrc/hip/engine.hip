@@ -686,6 +686,14 @@ static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
     return h264mi_engine_read_rgba(c->e, 0, slot, dst);
 }
 
+static void *hb_host_alloc(void *vctx, size_t bytes)
+{
+    void *p = NULL;
+    return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : NULL;
+}
+
+static void hb_host_free(void *vctx, void *p) { (void)hipHostFree(p); }
+
 static int hb_copy(void *vctx, int dst, int src)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
@@ -718,6 +726,8 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     be.decode = hb_decode;
     be.read = hb_read;
     be.read_rgba = hb_read_rgba;
+    be.host_alloc = hb_host_alloc;
+    be.host_free = hb_host_free;
     be.copy = hb_copy;
     be.destroy = hb_destroy;
     return be;

@@ -25,11 +25,18 @@ int h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be)
     return 0;
 }
 
+static void out_frames_free(H264Dec *d)
+{
+    if (d->out_frames && d->be.host_free) d->be.host_free(d->be.ctx, d->out_frames);
+    else free(d->out_frames);
+    d->out_frames = NULL;
+}
+
 void h264dec_release(H264Dec *d)
 {
     if (d->pb_ready) picbuild_free(&d->pb);
     free(d->rbsp);
-    free(d->out_frames);
+    out_frames_free(d);
     if (d->be.destroy) d->be.destroy(d->be.ctx);
     memset(d, 0, sizeof(*d));
 }
@@ -272,8 +279,9 @@ static int activate(H264Dec *d, int pps_id, int is_idr)
         dpb_init(&d->dpb, sps->max_dpb, sps->num_ref_frames, 1 << sps->log2_max_frame_num, no_reorder);
         d->nslots = d->dpb.npic;
         d->frame_bytes = (size_t)sps->w_mbs * sps->h_mbs * 384;
-        free(d->out_frames);
-        d->out_frames = (uint8_t *)malloc(d->frame_bytes * (size_t)d->nslots);
+        out_frames_free(d);
+        d->out_frames = (uint8_t *)(d->be.host_alloc ? d->be.host_alloc(d->be.ctx, d->frame_bytes * (size_t)d->nslots)
+                                                     : malloc(d->frame_bytes * (size_t)d->nslots));
         if (!d->out_frames) return DEC_MEMALLOC_ERROR;
         if (d->be.configure(d->be.ctx, sps->w_mbs, sps->h_mbs, d->nslots)) return DEC_MEMALLOC_ERROR;
     } else if (pps_id != d->active_pps) {

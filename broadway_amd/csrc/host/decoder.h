@@ -27,6 +27,10 @@ typedef struct H264Backend {
     /* copy slot converted to RGBA (w*16 * h*16 * 4 bytes, DecoderPost.js
      * rgb output); NULL when the backend has no conversion */
     int  (*read_rgba)(void *ctx, int slot, uint8_t *dst);
+    /* optional: host memory for the output frames (pinned by the HIP
+     * backend, so each picture's D2H copy runs at DMA speed); NULL: malloc */
+    void *(*host_alloc)(void *ctx, size_t bytes);
+    void (*host_free)(void *ctx, void *p);
     /* copy one slot into another (error concealment of lost pictures) */
     int  (*copy)(void *ctx, int dst_slot, int src_slot);
     void (*destroy)(void *ctx);
