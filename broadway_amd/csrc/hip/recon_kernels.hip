@@ -1272,14 +1272,9 @@ struct NoMid { __device__ __forceinline__ void operator()() const {} };
 // (region cols -4..-1, the left MB's cols 12..15, now final) are written back
 // -- the row hand-off publishes from there without waiting for the internal
 // edges (edges 1..3 touch only this MB's columns 1..14)
-// pdelta (dir 0, != 0): the left halo (cols -4..-1) is read from the previous
-// MB's region at byte distance pdelta (its cols 12..15 / 4..7) instead of
-// from this region -- no separate copy; the write-back after the MB edge
-// then puts it in place.
 template <class Mid = NoMid>
 __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, uint8_t *ry, uint8_t *ru, uint8_t *rv,
-                                            uint8_t *junk, int lane, bool mb_edge_on, const Mid &mid = Mid(),
-                                            int pdelta = 0)
+                                            uint8_t *junk, int lane, bool mb_edge_on, const Mid &mid = Mid())
 {
     const int li = lane & 31;
     const bool chroma = li >= 16;
@@ -1307,7 +1302,7 @@ __device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, ui
         const uint32_t *row = (const uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
 #pragma unroll
         for (int j = 0; j < 5; j++) {
-            const uint32_t w = (j == 0 && pdelta) ? *(const uint32_t *)((const uint8_t *)row + pdelta + (chroma ? 8 : 16)) : row[j];
+            const uint32_t w = row[j];
             v[4 * j] = w & 255; v[4 * j + 1] = (w >> 8) & 255; v[4 * j + 2] = (w >> 16) & 255; v[4 * j + 3] = w >> 24;
         }
     } else {
@@ -2179,7 +2174,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         }
         // ---- vertical edges
         // (measured: reading the left halo straight from the partner's region
-        // inside V -- deblock_dir's pdelta -- and releasing it after the MB
+        // inside V and releasing it after the MB
         // edge was 3 us per launch slower than this copy)
         if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT);
         wave_sync();
