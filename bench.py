@@ -409,10 +409,11 @@ def main():
         step(k)
     eng.sync()
     torch.cuda.synchronize()
-    # HIP events around every 4th launch: each event marker costs the stream
-    # a few us between launches (tools/gap_probe.py), so timing every launch
-    # would slow the measured run itself
-    eng.set_timing(a.steps, stride=4)
+    # HIP events around every 4th launch.  k_wgpp's ride on its own dispatch
+    # packet (hipExtLaunchKernelGGL: no marker packets between launches,
+    # 382 vs 392 us measured per launch); a profiled dispatch still costs the
+    # stream a little (every launch timed: -0.9 % frames/s), hence the stride
+    eng.set_timing(a.steps, stride=int(os.environ.get("BENCH_TIMING_STRIDE", "4")))
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

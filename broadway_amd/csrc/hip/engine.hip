@@ -4,6 +4,7 @@
 // one launch reconstructs one picture from each stream of the batch).
 #include "recon_kernels.hip"
 #include "color.hip"
+#include <hip/hip_ext.h>
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -312,7 +313,10 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         rec_tev = true;
     }
     const bool rec = e->timing || rec_tev;
-    if (rec) (void)hipEventRecord(t0, e->st);
+    // k_wgpp (the default path): the timing events ride on the kernel's own
+    // dispatch packet (hipExtLaunchKernelGGL), no marker packets around it
+    const bool pp_fast = wg && !pipe && e->wg_pp && prep && !a.prof;
+    if (rec && !pp_fast) (void)hipEventRecord(t0, e->st);
     e->last_kernel = !wg ? "k_mb+k_rows" : pipe ? "k_wg" : (e->wg_pp && prep) ? "k_wgpp" : "k_wg";
     e->tev_single = wg;
     if (!wg) {
@@ -335,8 +339,13 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
             if (a.prof) {
                 if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, true, true>), grid, dim3(256), 0, e->st, a);
                 else hipLaunchKernelGGL((k_wgpp<3, true, true>), grid, dim3(320), 0, e->st, a);
-            } else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, false, true>), grid, dim3(256), 0, e->st, a);
-            else hipLaunchKernelGGL((k_wgpp<3, false, true>), grid, dim3(320), 0, e->st, a);
+            } else if (nmc == 2) {
+                hipExtLaunchKernelGGL((k_wgpp<2, false, true>), grid, dim3(256), 0, e->st, rec ? t0 : nullptr,
+                                      rec ? t2 : nullptr, 0, a);
+            } else {
+                hipExtLaunchKernelGGL((k_wgpp<3, false, true>), grid, dim3(320), 0, e->st, rec ? t0 : nullptr,
+                                      rec ? t2 : nullptr, 0, a);
+            }
         } else if (prep) {
             if (a.prof) hipLaunchKernelGGL((k_wg<false, 3, true, true>), grid, dim3(256), 0, e->st, a);
             else if (nmc == 2) hipLaunchKernelGGL((k_wg<false, 2, false, true>), grid, dim3(192), 0, e->st, a);
@@ -350,7 +359,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         }
         HIPCHECK(hipGetLastError());
     }
-    if (rec) (void)hipEventRecord(t2, e->st);
+    if (rec && !pp_fast) (void)hipEventRecord(t2, e->st);
     if (prep) HIPCHECK(hipEventRecord(e->ev_wgdone[pbuf], e->st));
     return 0;
 }
