@@ -15,21 +15,25 @@ GPU by two kernels on two HIP streams:
           residual (dequant + inverse transforms); it depends on no
           reconstructed sample, so step t+1's k_prep runs beside step t's
           row kernel;
-  k_wgpp  one workgroup per (picture, MB row): two MC waves (6-tap luma /
+  k_wgpp  one workgroup per (picture, MB row): three MC waves (6-tap luma /
           bilinear chroma MC, intra prediction, clip-add) feed an LDS ring,
           two ping-pong row waves run the in-loop deblocking chain; rows hand
           off through tagged-granule mailboxes.
 Steps follow decoding order, so the W warmup steps decode the first W
-pictures and the K timed steps the next K.  (H264MI_KERNEL=classic selects
-the earlier k_mb + k_rows pair, H264MI_WG_PP=0 the one-row-wave k_wg.)
+pictures and the K timed steps the next K.
 
-Bit-exactness: rank 0 checks the frames still resident in stream 0's slots
-against the reference decoder's per-frame MD5s (tests/golden/golden.json,
-made by running the reference C on the same generated streams).
+Bit-exactness: after the timed loop an untimed pass decodes the same W + K
+steps again and compares EVERY picture of every stream of every rank with the
+reference decoder's per-frame MD5s (tests/golden/golden.json, made by running
+the reference C on the same generated streams, seeds 100..163).
 
-Multi-GPU: one process per GPU (torch.distributed.run), streams partitioned
-across ranks with no data-path collective (SURVEY.md §8e) -> "scaling": "weak";
-the only communication is the barrier and the max-over-ranks of the timing.
+Multi-GPU: one process per GPU, streams partitioned across ranks with no
+data-path collective -> "scaling": "weak"; the only
+communication is the barrier, the max-over-ranks of the timing and the sum of
+the verification counts (gloo, host scalars).  `--gpus N` without a
+torch.distributed environment starts the N ranks itself (torch.distributed.run,
+before this process touches the GPU).  `--dry-run` runs the sharding, host
+parse, step loop and reductions without any device call (CPU tests).
 
 Prints ONE JSON line on rank 0.
 """
@@ -42,6 +46,7 @@ import hashlib
 import json
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -54,25 +59,24 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MBREC = 96
+MAX_E2E_PROCS = 8          # end-to-end leg: decoder processes (the box allows 16 GPU processes)
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=56)
     ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="pictures per stream per launch (>1: frame-pipelined k_wg; 1: k_mb + k_rows)")
     ap.add_argument("--streams", type=int, default=8, help="streams per GPU (configs[3]: 8)")
-    ap.add_argument("--groups", type=int, default=4,
-                    help="picture groups per launch on separate HIP streams (--pipeline 1 only)")
     ap.add_argument("--config", type=int, default=3, help="generator preset (3 = 1080p I+P)")
-    ap.add_argument("--pipe-kernel", action="store_true", help="use the pipelined k_wg launch even for --pipeline 1")
     ap.add_argument("--gen", default="", help="generator overrides k=v,... (experiments; default: preset)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host parse + GPU + D2H) leg")
-    return ap.parse_args()
+    ap.add_argument("--no-rgba", action="store_true", help="skip the RGBA output leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no device calls: sharding, host parse, step loop and reductions only (CPU tests)")
+    return ap.parse_args(argv)
 
 
 def shard_seeds(rank: int, streams_per_gpu: int):
@@ -80,18 +84,43 @@ def shard_seeds(rank: int, streams_per_gpu: int):
     return [100 + rank * streams_per_gpu + i for i in range(streams_per_gpu)]
 
 
-def max_over_ranks(dist, torch, value: float) -> float:
+def reduce_over_ranks(dist, torch, value: float, op: str = "max") -> float:
     if dist is None:
         return value
     t = torch.tensor([value], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
     return float(t.item())
 
 
-def dist_setup(gpus):
+def max_over_ranks(dist, torch, value: float) -> float:
+    return reduce_over_ranks(dist, torch, value, "max")
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    """--gpus N outside torch.distributed: start N ranks (one per GPU) with
+    torch.distributed.run as a child process (this process has not touched
+    the GPU) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dist_setup(gpus: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
     import torch
     import torch.distributed as dist
     if world > 1:
@@ -114,46 +143,36 @@ def prepare(config, seeds, nframes, overrides=None):
     return [r[0] for r in res], [r[1] for r in res]
 
 
-def upload(L, caps, npics, depth, ring):
-    """Lay out all record batches / coefficients / picture descriptors in HBM.
-    Launch k covers pictures [k*depth, (k+1)*depth) of every stream, records
-    picture-major (picture t of the launch, stream s at (t*S + s)), so a
-    launch's records are contiguous; PicDesc.rec_base is relative to them.
-    ring > 0 (pipelined launches): picture j writes frame slot j % ring and
-    the records' reference slots are rewritten from DPB slots to ring slots."""
+def pack(caps, npics):
+    """Host image of every record batch / coefficient block / picture
+    descriptor of pictures [0, npics) of every stream.  Step k's records are
+    contiguous, picture-major (stream s at k*S + s); PicDesc.rec_base is
+    relative to the step's records, coef_base to the whole coefficient pool."""
     S = len(caps)
-    w, h = caps[0].w_mbs, caps[0].h_mbs
-    nmbs = w * h
-    nslots = ring if ring else max(c.nslots for c in caps)
+    nmbs = caps[0].w_mbs * caps[0].h_mbs
+    nslots = max(c.nslots for c in caps)
     rec_bytes = nmbs * MBREC
     recs = bytearray(npics * S * rec_bytes)
     coef_parts = []
     pics = np.zeros((npics * S, 8), dtype=np.uint32)
     cbase = 0
-    dpb_pic = [dict() for _ in caps]        # DPB slot -> picture index now in it
     for j in range(npics):
         for s, c in enumerate(caps):
             p = c.pictures[j]
             off = (j * S + s) * rec_bytes
             recs[off:off + rec_bytes] = C.string_at(p.rec, rec_bytes)
-            slot = p.cur_slot
-            if ring:
-                r = np.frombuffer(recs, dtype=REC_DT, count=nmbs, offset=off)
-                inter = r["type"] <= 1
-                if inter.any():
-                    lut = np.zeros(64, dtype=np.uint8)
-                    for d, pj in dpb_pic[s].items():
-                        lut[d] = pj % ring
-                    refs = r["ref"].copy()
-                    refs[inter] = lut[refs[inter]]
-                    r["ref"][:] = refs
-                dpb_pic[s][p.cur_slot] = j
-                slot = j % ring
             if p.ncoef:
                 coef_parts.append(C.string_at(p.coef, p.ncoef * 32))
-            pics[j * S + s] = (((j % depth) * S + s) * nmbs, s * nslots, slot, 0, cbase, 0, 0, 0)
+            pics[j * S + s] = (s * nmbs, s * nslots, p.cur_slot, 0, cbase, 0, 0, 0)
             cbase += p.ncoef
     coefs = b"".join(coef_parts) + b"\0" * 64
+    return recs, coefs, pics, rec_bytes * S, nslots
+
+
+def upload(L, caps, npics):
+    """pack() into HBM; returns (d_recs, d_coef, d_pics, step_rec_bytes,
+    nslots, resident bytes)."""
+    recs, coefs, pics, step_rec_bytes, nslots = pack(caps, npics)
     d_recs = L.h264mi_device_alloc(len(recs))
     d_coef = L.h264mi_device_alloc(len(coefs))
     d_pics = L.h264mi_device_alloc(pics.nbytes)
@@ -163,55 +182,22 @@ def upload(L, caps, npics, depth, ring):
     assert L.h264mi_copy_h2d(d_recs, rb, len(recs)) == 0
     assert L.h264mi_copy_h2d(d_coef, coefs, len(coefs)) == 0
     assert L.h264mi_copy_h2d(d_pics, pics.ctypes.data, pics.nbytes) == 0
-    return d_recs, d_coef, d_pics, rec_bytes * S, nslots, len(recs) + len(coefs)
+    return d_recs, d_coef, d_pics, step_rec_bytes, nslots, len(recs) + len(coefs)
 
 
-REC_DT = np.dtype([("type", "u1"), ("qp", "u1"), ("qpc", "u1"), ("avail", "u1"), ("pred", "u1"),
-                   ("dbf", "u1"), ("offA", "i1"), ("offB", "i1"), ("cbits", "<u4"), ("coef", "<u4"),
-                   ("i4", "u1", 8), ("ref", "u1", 4), ("mv", "<i2", 32), ("slice", "<u2"), ("rsv", "<u2")])
-
-
-def row_reach(caps, lo, hi):
-    """How many MB rows beyond its own an inter MB of pictures [lo, hi) reads
-    from a reference (6-tap footprint included, clamped to the picture)."""
-    dy = 0
-    for c in caps:
-        nmbs, H16 = c.w_mbs * c.h_mbs, c.h_mbs * 16
-        rows = np.repeat(np.arange(c.h_mbs), c.w_mbs)
-        for j in range(lo, hi):
-            r = np.frombuffer(C.string_at(c.pictures[j].rec, nmbs * MBREC), dtype=REC_DT)
-            inter = r["type"] <= 1
-            if not inter.any():
-                continue
-            mvy = r["mv"][inter].reshape(-1, 16, 2)[:, :, 1].astype(np.int64) >> 2
-            y0 = (rows[inter] * 16)[:, None] + mvy
-            lo_r = np.clip(y0 - 2, 0, H16 - 1) // 16
-            hi_r = np.clip(y0 + 15 + 3, 0, H16 - 1) // 16
-            dy = max(dy, int((rows[inter][:, None] - lo_r).max()), int((hi_r - rows[inter][:, None]).max()))
-    return dy
-
-
-def inter_alg_bytes(caps, lo, hi):
-    """Algorithmic bytes of k_mb for pictures [lo, hi) of every stream:
-    MC reference footprint (SURVEY §8d R_alg luma+chroma term), the
-    coefficient blocks and records of inter MBs, and the 384-B write of every
-    inter MB."""
-    dt = REC_DT
-    assert dt.itemsize == MBREC
-    total = 0
-    n_inter = 0
-    for c in caps:
-        nmbs = c.w_mbs * c.h_mbs
-        for k in range(lo, hi):
-            p = c.pictures[k]
-            r = np.frombuffer(C.string_at(p.rec, nmbs * MBREC), dtype=dt)
-            inter = r["type"] <= 1
-            cb = r["cbits"][inter]
-            nblk = int(np.unpackbits(cb.view(np.uint8)).sum())
-            ni = int(inter.sum())
-            total += p.alg_ref_bytes + 32 * nblk + (MBREC + 384) * ni
-            n_inter += ni
-    return total, n_inter
+def golden_frames(config, seed, overrides):
+    """The reference decoder's per-frame MD5s of generator stream (config,
+    seed) when a fixture covers it (overrides other than nframes: none)."""
+    if overrides:
+        return None
+    gold = os.path.join(ROOT, "tests", "golden", "golden.json")
+    if not os.path.exists(gold):
+        return None
+    for c in json.load(open(gold))["cases"].values():
+        if c["config"] == config and c["seed"] == seed and set(c["overrides"]) <= {"nframes"} \
+                and not c["no_reorder"]:
+            return c["frames"]
+    return None
 
 
 def cpu_baseline(streams, nframes, reps=10):
@@ -291,20 +277,22 @@ def rgba_leg(torch, L, eng, S, w_mbs, h_mbs, reps=50):
             "frames_per_s": round(S / (us * 1e-6), 1), "alg_bytes_per_launch": int(alg),
             "achieved_GBs": round(gbs, 1), "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 4),
             "semantics": "per pixel DecoderPost.js yuv2rgbcalc (:514-560), RGBA bytes",
-            "note": "repeated launches over the same 8 pictures: the 25 MB I420 input stays in the 256 MB "
-                    "MALL, the 67 MB RGBA output is written with non-temporal stores"}
+            "note": "repeated launches over the same pictures: the I420 input stays in the 256 MB "
+                    "MALL, the RGBA output is written with non-temporal stores"}
 
 
 def end_to_end(streams, nframes, reps=3):
     """End-to-end decode through the product C-ABI: one
-    broadway_amd/lib/h264mi_dec process per stream, all in parallel (one host
-    thread each), each decoding its stream `reps` times -- host CAVLC parse,
-    H2D of the MB records, k_prep + k_wgpp, D2H of every output picture.
-    Rate = all pictures / the slowest process's decode time (HIP start-up of
-    each process excluded; it is paid before its timed loop)."""
+    broadway_amd/lib/h264mi_dec process per stream (at most MAX_E2E_PROCS),
+    all in parallel (one host thread each), each decoding its stream `reps`
+    times -- host CAVLC parse, H2D of the MB records, k_prep + k_wgpp, D2H of
+    every output picture.  Rate = all pictures / the slowest process's decode
+    time (HIP start-up of each process excluded; it is paid before its timed
+    loop)."""
     exe = os.path.join(ROOT, "broadway_amd", "lib", "h264mi_dec")
     if not os.path.exists(exe):
         return None
+    streams = streams[:MAX_E2E_PROCS]
     td = tempfile.mkdtemp(prefix="h264e2e")
     try:
         procs = []
@@ -314,47 +302,54 @@ def end_to_end(streams, nframes, reps=3):
                 f.write(s)
             procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T", pth], stdout=subprocess.PIPE,
                                           stderr=subprocess.PIPE, text=True))
-        secs, pics = [], 0
+        secs, pics, parts = [], 0, {}
         for pr in procs:
             o, e = pr.communicate(timeout=600)
             if pr.returncode != 0:
                 raise RuntimeError(f"h264mi_dec failed: {e.strip()[-300:]}")
             for line in o.splitlines():
-                if line.startswith("pictures"):
-                    pics += int(line.split()[1])
-                if line.startswith("decode_seconds"):
-                    secs.append(float(line.split()[1]))
+                f = line.split()
+                if not f:
+                    continue
+                if f[0] == "pictures":
+                    pics += int(f[1])
+                elif f[0] == "decode_seconds":
+                    secs.append(float(f[1]))
+                elif f[0].startswith("t_") and len(f) > 1:
+                    parts[f[0]] = parts.get(f[0], 0.0) + float(f[1])
         t = max(secs)
-        return {"value": round(pics / t, 2), "unit": "frames/s", "host_threads": len(streams),
-                "sample": f"{len(streams)} x {nframes}-frame 1080p streams x {reps} passes, one h264mi_dec process "
-                          f"(H264SwDec* C-ABI) per stream: host parse + H2D + kernels + D2H of every picture; "
-                          f"{pics} frames in {t:.2f} s"}
+        res = {"value": round(pics / t, 2), "unit": "frames/s", "host_threads": len(streams),
+               "sample": f"{len(streams)} x {nframes}-frame 1080p streams x {reps} passes, one h264mi_dec process "
+                         f"(H264SwDec* C-ABI) per stream: host parse + H2D + kernels + D2H of every picture; "
+                         f"{pics} frames in {t:.2f} s"}
+        if parts and pics:
+            res["per_picture_ms"] = {k[2:]: round(v * 1e3 / pics * len(streams) / len(streams), 3)
+                                     for k, v in sorted(parts.items())}
+        return res
     finally:
         shutil.rmtree(td, ignore_errors=True)
 
 
-def verify(eng, caps, seeds, n_decoded, ring=0):
-    """Bit-exactness: every slot of stream 0 still holding one of the decoded
-    pictures vs the reference decoder's MD5 of that picture (POC type 2:
-    output order == decode order)."""
-    gold = os.path.join(ROOT, "tests", "golden", "golden.json")
-    cases = json.load(open(gold))["cases"] if os.path.exists(gold) else {}
-    ref = cases.get(f"bench_1080p_s{seeds[0]}")
-    if ref is None:
-        return None, 0
-    c = caps[0]
-    last = {}
-    for k in range(n_decoded):
-        last[k % ring if ring else c.pictures[k].cur_slot] = k    # the picture each slot holds now
-    ok = True
-    n = 0
-    for slot, k in last.items():
-        if k >= len(ref["frames"]):
-            continue                              # beyond the fixture
-        n += 1
-        if hashlib.md5(eng.read(0, slot).tobytes()).hexdigest() != ref["frames"][k]:
-            ok = False
-    return ok, n
+def verify_all(eng, step, caps, seeds, config, overrides, nsteps):
+    """Untimed verification pass: decode steps [0, nsteps) again and compare
+    every picture of every stream with the reference decoder's MD5s (POC
+    type 2: output order == decode order, frame k = picture k).  Returns
+    (ok, frames checked, frames without a fixture)."""
+    refs = [golden_frames(config, sd, overrides) for sd in seeds]
+    ok, n, missing = True, 0, 0
+    for k in range(nsteps):
+        step(k)
+        eng.sync()
+        for s, c in enumerate(caps):
+            ref = refs[s]
+            if ref is None or k >= len(ref):
+                missing += 1
+                continue
+            got = hashlib.md5(eng.read(s, c.pictures[k].cur_slot).tobytes()).hexdigest()
+            n += 1
+            if got != ref[k]:
+                ok = False
+    return ok, n, missing
 
 
 def load_traffic():
@@ -369,105 +364,121 @@ def load_traffic():
         return None
 
 
-def main():
-    a = parse_args()
+class _DryEngine:
+    """--dry-run stand-in for broadway_amd.engine.Engine: no device calls."""
+
+    def __init__(self, *a, **k):
+        self.launches = 0
+
+    def decode_device(self, *a):
+        self.launches += 1
+
+    def sync(self):
+        pass
+
+    def set_timing(self, *a, **k):
+        pass
+
+    def timing_report(self):
+        return 0.0, 0.0, 0
+
+    def errors(self):
+        return 0
+
+    def kernel_name(self):
+        return "dry-run"
+
+    def close(self):
+        pass
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse_args(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, argv))
     torch, dist, rank, local, world = dist_setup(a.gpus)
     from broadway_amd import _lib
-    from broadway_amd.engine import Engine
     L = _lib.mi()
 
     S = a.streams
-    P = max(1, a.pipeline)
     seeds = shard_seeds(rank, S)
-    nframes = (a.warmup + a.steps) * P
+    nframes = a.warmup + a.steps
     t_prep = time.perf_counter()
     overrides = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.gen.split(",") if kv)
     streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= nframes for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    use_pipe = P > 1 or a.pipe_kernel
-    ring = P + 17 if use_pipe else 0        # frame-slot ring: launch + any short-term reference span
-    d_recs, d_coef, d_pics, pic_rec_bytes, nslots, resident = upload(L, caps, nframes, P, ring)
-    lags = [row_reach(caps, k * P, (k + 1) * P) + 2 for k in range(a.warmup + a.steps)] if use_pipe else []
+    if a.dry_run:
+        d_recs = d_coef = d_pics = 0
+        _, _, _, step_rec_bytes, nslots = pack(caps, nframes)
+        resident = 0
+        eng = _DryEngine()
+    else:
+        from broadway_amd.engine import Engine
+        d_recs, d_coef, d_pics, step_rec_bytes, nslots, resident = upload(L, caps, nframes)
+        eng = Engine(w, h, S, nslots, device=local)
+        torch.cuda.set_device(local)
     t_prep = time.perf_counter() - t_prep
-
-    eng = Engine(w, h, S, nslots, device=local)
-    eng.set_pipeline(P)
-    classic = os.environ.get("H264MI_KERNEL") == "classic"     # default: k_wg
-    G = max(1, min(a.groups, S)) if classic and not use_pipe else 1
-    eng.set_groups(G)
-    torch.cuda.set_device(local)
+    sync = (lambda: None) if a.dry_run else torch.cuda.synchronize
 
     def step(k):
-        if not use_pipe:
-            eng.decode_device(S, d_recs + k * pic_rec_bytes, d_coef, d_pics + k * S * 32)
-        else:
-            eng.decode_pipelined(S, P, d_recs + k * P * pic_rec_bytes, d_coef, d_pics + k * P * S * 32, k * P,
-                                 lags[k])
+        eng.decode_device(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32)
 
     for k in range(a.warmup):
         step(k)
     eng.sync()
-    torch.cuda.synchronize()
-    # HIP events around every 4th launch.  k_wgpp's ride on its own dispatch
-    # packet (hipExtLaunchKernelGGL: no marker packets between launches,
-    # 382 vs 392 us measured per launch); a profiled dispatch still costs the
-    # stream a little (every launch timed: -0.9 % frames/s), hence the stride
+    sync()
+    # HIP events around every 4th launch, carried by k_wgpp's own dispatch
+    # packet (hipExtLaunchKernelGGL: no marker packets between launches); a
+    # profiled dispatch still costs the stream a little, hence the stride
     eng.set_timing(a.steps, stride=int(os.environ.get("BENCH_TIMING_STRIDE", "4")))
     if dist:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for k in range(a.warmup, a.warmup + a.steps):
         step(k)
     eng.sync()
-    torch.cuda.synchronize()
+    sync()
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
     dt = max_over_ranks(dist, torch, t1 - t0)
-    mb_us, rows_us, nb = eng.timing_report()
+    _, rows_us, nb = eng.timing_report()
     errors = eng.errors()
 
-    frames_total = S * a.steps * P * world
+    frames_total = S * a.steps * world
     fps = frames_total / dt
     # roofline (SURVEY §8d): R_alg per frame = MC reference footprint + coded
-    # 4x4 blocks x 32 B + 96-B MB records; one step = P frames of each of the
-    # S streams, reconstructed by one k_wg launch (P > 1) or k_mb + k_rows
+    # 4x4 blocks x 32 B + 96-B MB records; one step = one picture of each of
+    # the S streams, reconstructed by one k_prep + k_wgpp launch pair
     r_alg = 0
     for c in caps:
-        for k in range(a.warmup * P, (a.warmup + a.steps) * P):
+        for k in range(a.warmup, a.warmup + a.steps):
             p = c.pictures[k]
             r_alg += p.alg_ref_bytes + 32 * p.n_coded + MBREC * c.w_mbs * c.h_mbs
-    per_step_bytes = r_alg / a.steps
-    # HIP-event durations are per launch: with G picture groups a launch
-    # (k_mb + k_rows of group 0) covers S/G pictures, i.e. 1/G of the step's
-    # bytes; the G groups' launches run concurrently (aggregate: wall_read_GBs)
-    launch_bytes = per_step_bytes / G
-    mb_us_avg, rows_us_avg = mb_us / max(nb, 1), rows_us / max(nb, 1)
-    # single-launch kernels (k_wgpp / k_wg): the first timing slot spans only
-    # the wait for k_prep and the error-flag reset before the launch
-    step_us = mb_us_avg + rows_us_avg if classic else rows_us_avg
-    kname = eng.kernel_name() or ("k_mb+k_rows" if classic else "k_wg")
+    launch_bytes = r_alg / a.steps
+    step_us = rows_us / max(nb, 1)
     achieved = launch_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
-    kmb_alg, n_inter = inter_alg_bytes(caps, a.warmup * P, (a.warmup + a.steps) * P)
-    kmb_alg /= G
-    kmb_achieved = (kmb_alg / a.steps) / (mb_us_avg * 1e-6) / 1e9 if mb_us_avg > 0 else 0.0
     traffic = load_traffic()
     frame_read_gbs = r_alg * world / dt / 1e9
 
-    ok = None
-    n_checked = 0
-    if not a.no_verify and rank == 0:
-        ok, n_checked = verify(eng, caps, seeds, nframes, ring)
-    rgba = rgba_leg(torch, L, eng, S, w, h) if rank == 0 else None
+    ok, n_checked, n_missing = None, 0, 0
+    if not a.no_verify and not a.dry_run:
+        ok, n_checked, n_missing = verify_all(eng, step, caps, seeds, a.config, overrides, nframes)
+    n_checked_all = int(reduce_over_ranks(dist, torch, n_checked, "sum"))
+    n_missing_all = int(reduce_over_ranks(dist, torch, n_missing, "sum"))
+    ok_all = None if ok is None else reduce_over_ranks(dist, torch, 0.0 if ok else 1.0, "max") == 0.0
+    errors_all = int(reduce_over_ranks(dist, torch, errors, "sum"))
+    rgba = rgba_leg(torch, L, eng, S, w, h) if rank == 0 and not a.dry_run and not a.no_rgba else None
 
     cpu = None
-    if rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline and not a.dry_run:
         cpu = cpu_baseline(streams, nframes)
     eng.close()
     e2e = None
-    if rank == 0 and world == 1 and not a.no_e2e:
+    if rank == 0 and world == 1 and not a.no_e2e and not a.dry_run:
         e2e = end_to_end(streams, nframes)
 
     if rank == 0:
@@ -485,16 +496,16 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded H.264 Baseline generator; records pre-parsed on host, resident in HBM)",
             "config": {"workload": "configs[3]: 1080p (1920x1088, crop 1080) Baseline I+P, 1 I per 60, "
-                                   "4 slices/picture, deblock idc 0/2",
+                                   "4 slices/picture, deblock idc 0/2" if a.config == 3 and not overrides
+                                   else f"generator preset {a.config} {overrides or ''}".strip(),
                        "streams_per_gpu": S, "total_streams": S * world,
-                       "frames_per_stream_timed": a.steps * P, "pictures_per_stream_per_step": P,
+                       "frames_per_stream_timed": a.steps,
                        "seeds": f"100..{100 + S * world - 1}",
-                       "parallelism": f"streams sharded {S}/GPU, no collective; "
-                                      f"{P} consecutive pictures per stream overlapped per launch; "
-                                      f"{G} picture groups on separate HIP streams"},
-            "roofline": {"kernel": (f"{kname} (one launch = one step; k_prep of the next step runs beside it)" if not classic
-                                    else f"k_mb+k_rows of one picture group ({S // G} pictures; "
-                                         f"{G} groups run concurrently)"), "bound": "hbm",
+                       "parallelism": f"streams sharded {S}/GPU over {world} rank(s), no collective; "
+                                      f"one picture of each stream per launch"},
+            "roofline": {"kernel": "k_wgpp (one launch = one step; k_prep of the next step runs beside it)",
+                         "bound": "hbm",
+                         "limiter": "latency: the MB-row deblocking dependency chain (DESIGN.md §3), not HBM",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
@@ -502,28 +513,27 @@ def main():
                          "avg_launch_kernel_us": round(step_us, 2),
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
-            "kernels": ({kname: {"avg_launch_us": round(rows_us_avg, 2),
-                                 "pictures_per_launch": S * P, "frame_slot_ring": ring or None,
-                                 "row_lag_max": max(lags) if lags else None,
-                                 "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}}
-                        if not classic else
-                        {"k_mb": {"avg_launch_us": round(mb_us_avg, 2),
-                                  "alg_bytes_per_launch": int(kmb_alg / a.steps),
-                                  "achieved_GBs": round(kmb_achieved, 1),
-                                  "frac": round(kmb_achieved / HBM_PEAK_GBS, 5)},
-                         "k_rows": {"avg_launch_us": round(rows_us_avg, 2),
-                                    "bound": "latency (MB-row dependency chain)"}}),
+            "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S,
+                                   "timed_launches": nb,
+                                   "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}},
             "wall_read_GBs": round(frame_read_gbs, 2),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "rgba_output": rgba,
-            "bitexact_check": {"ok": ok, "frames_checked": n_checked, "residual_range_errors": errors},
+            "bitexact_check": {"ok": ok_all, "frames_checked": n_checked_all,
+                               "frames_expected": S * world * nframes, "frames_without_fixture": n_missing_all,
+                               "method": "untimed re-decode of all warmup+timed steps, every picture of every "
+                                         "stream of every rank vs reference-decoder MD5s",
+                               "residual_range_errors": errors_all},
             "prep_seconds": round(t_prep, 1),
             "hbm_resident_input_MB": round(resident / 1e6, 1),
         }
-        print(json.dumps(line))
-    for p in (d_recs, d_coef, d_pics):
-        L.h264mi_device_free(p)
+        if a.dry_run:
+            line["dry_run"] = {"launches": eng.launches, "seeds": seeds}
+        print(json.dumps(line), flush=True)
+    if not a.dry_run:
+        for p in (d_recs, d_coef, d_pics):
+            L.h264mi_device_free(p)
     if dist:
         dist.destroy_process_group()
 

@@ -138,12 +138,6 @@ def mi() -> C.CDLL:
     L.h264mi_engine_decode.restype = i32
     L.h264mi_engine_decode_device.argtypes = [vp, i32, vp, vp, vp]
     L.h264mi_engine_decode_device.restype = i32
-    L.h264mi_engine_set_pipeline.argtypes = [vp, i32]
-    L.h264mi_engine_set_pipeline.restype = i32
-    L.h264mi_engine_set_groups.argtypes = [vp, i32]
-    L.h264mi_engine_set_groups.restype = i32
-    L.h264mi_engine_decode_pipelined.argtypes = [vp, i32, i32, vp, vp, vp, i32, i32]
-    L.h264mi_engine_decode_pipelined.restype = i32
     L.h264mi_engine_read.argtypes = [vp, i32, i32, vp]
     L.h264mi_engine_read.restype = i32
     L.h264mi_engine_read_rgba.argtypes = [vp, i32, i32, vp]

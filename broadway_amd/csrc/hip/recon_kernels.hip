@@ -1,25 +1,22 @@
 // H.264 Baseline macroblock reconstruction + in-loop deblocking for gfx950.
 //
 // Two kernels per picture batch (one picture from each of S streams):
-//   k_mb    -- every MB of every picture in the batch, fully parallel, one
-//              64-lane wave per MB: deblocking record (bS of the 32 4x4 edge
-//              segments + alpha/beta/indexA per edge class), residual
-//              (dequant + 4x4 IDCT + luma/chroma DC transforms) and, for inter
-//              MBs, 6-tap luma / bilinear chroma motion compensation from the
-//              HBM-resident reference slots staged through LDS, clip-add and
-//              write-out.  Reference: h264bsdProcessBlock/LumaDc/ChromaDc
-//              (transform.c:94-398), h264bsdInterPrediction
-//              (inter_prediction.c:364-487), h264bsdPredictSamples
-//              (reconstruct.c:1819-1941), h264bsdWriteOutputBlocks
-//              (image.c:171-343), GetBoundaryStrengths / thresholds
-//              (deblocking.c:1134-1532).
-//   k_rows  -- one 16-wave workgroup per picture: MB rows pipelined across the
-//              waves with LDS progress counters (MB (r,c) waits for (r-1,c+1)),
-//              intra reconstruction (I4x4 10-step sub-wavefront, I16x16,
-//              chroma, I_PCM) from unfiltered neighbour samples, then the MB's
-//              deblocking in the reference's raster-equivalent order.
-//              Reference: h264bsdIntraPrediction (intra_prediction.c:475-988),
-//              h264bsdFilterPicture (deblocking.c:574-1736).
+//   k_prep  -- every MB of the batch, fully parallel (one wave per MB): the
+//              work that reads no reconstructed sample -- the deblocking
+//              record (bS of the 32 4x4 edge segments + alpha/beta/tc0/indexA
+//              per edge class; GetBoundaryStrengths / thresholds,
+//              deblocking.c:1134-1532) and the residual (dequant + 4x4 IDCT +
+//              luma/chroma DC transforms, transform.c:94-398) with the
+//              reference's [-512,511] range check.
+//   k_wgpp  -- one workgroup per (picture, MB row): three MC waves walk the
+//              row's MBs (6-tap luma / bilinear chroma MC from the
+//              HBM-resident reference slots, reconstruct.c:1819-2314; intra
+//              4x4 / 16x16 / chroma / I_PCM from unfiltered neighbours,
+//              intra_prediction.c:475-988; clip-add) into an LDS ring; two
+//              ping-pong row waves deblock the row in the reference's
+//              raster-equivalent order (h264bsdFilterPicture,
+//              deblocking.c:574-1736) and hand the final bottom rows to the
+//              row below through tagged-granule mailboxes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../../include/h264mi_records.h"
@@ -36,18 +33,11 @@ struct ReconArgs {
     int w, h;                 // picture size in MBs
     uint8_t *dbrec;           // 64 B deblocking record per MB of the batch
     int16_t *res;             // 384 residual samples per MB (intra MBs only)
-    unsigned int *err;        // per picture: bit0 residual range error, bit1 wait timeout
-    unsigned long long *mbx;  // row mailboxes: 32 tagged granules per MB of the batch (k_rows)
+    unsigned int *err;        // per picture: bit0 residual range error, bit1/2/4 bounded-wait timeouts
+    unsigned long long *mbx;  // row mailboxes: 32 tagged granules per MB of the batch
     unsigned int epoch;       // launch counter != 0: granule tag (no reset between launches)
-    unsigned long long *prof; // optional k_rows phase clocks: 16 per (row, picture) workgroup
-    // frame-pipelined launches (k_wg): pictures p = k*S + s, k = 0..P-1.
-    // Frame slots follow a ring: the launch's picture k of a stream writes
-    // slot (base_pic + k) mod ring, so a reference slot x was written in this
-    // launch by picture (x - base_pic) mod ring if that is < k.
-    uint32_t *progress;       // per picture row: (epoch << 12) | iterations whose frame stores drained
-    int S;                    // streams per pipeline stage
-    int ring, base_pic;
-    const uint32_t *order;    // k_wg: dispatch order of the P*H (picture, row) pairs, (k << 16) | r
+    unsigned long long *prof; // optional per-MB chain stamps (profiling k_wgpp)
+    int S;                    // pictures (streams) of the batch
     unsigned long long *gjunk; // 64 KiB sink: 128 x 64 granules for lanes with nothing to store
 };
 
@@ -96,8 +86,7 @@ __device__ __forceinline__ uint32_t tab_at(uint32_t reg, int idx)
     return (uint32_t)__builtin_amdgcn_ds_bpermute(idx << 2, (int)reg);
 }
 
-// ordering of LDS traffic between the lanes of one wave (waves of k_rows
-// work independently; k_mb workgroups are a single wave)
+// ordering of LDS traffic between the lanes of one wave
 // A wave's LDS instructions execute in issue order, so lanes of one wave see
 // each other's LDS writes once the compiler keeps program order: a compiler
 // barrier is enough (no s_waitcnt, which would also drain in-flight global
@@ -275,49 +264,6 @@ __device__ void mb_residual(const MbRec &r, const int16_t *base, int16_t *res,
 __device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f)
 {
     return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
-}
-
-// win: 9x9 window whose (2,2) element is the integer sample G of output x=0.
-// Computes 4 outputs (x = 0..3) of window row offset `yy` (0..3).
-// win: 9 rows x 9 samples of the block's reference window (row stride 12)
-__device__ __forceinline__ void luma_row4(const uint8_t *win, int yy, int fx, int fy, int out[4])
-{
-#define W(x, y) ((int)win[((y) + 2 + yy) * 12 + (x) + 2])
-#define B1(x, y) tap6(W((x)-2, y), W((x)-1, y), W(x, y), W((x)+1, y), W((x)+2, y), W((x)+3, y))
-#define H1(x, y) tap6(W(x, (y)-2), W(x, (y)-1), W(x, y), W(x, (y)+1), W(x, (y)+2), W(x, (y)+3))
-    const int pos = fy * 4 + fx;
-#pragma unroll
-    for (int x = 0; x < 4; x++) {
-        int v;
-        const int G = W(x, 0);
-        if (pos == 0) { v = G; }
-        else if (fy == 0) {
-            const int b = clip255((B1(x, 0) + 16) >> 5);
-            v = fx == 2 ? b : (fx == 1 ? (G + b + 1) >> 1 : (W(x + 1, 0) + b + 1) >> 1);
-        } else if (fx == 0) {
-            const int hh = clip255((H1(x, 0) + 16) >> 5);
-            v = fy == 2 ? hh : (fy == 1 ? (G + hh + 1) >> 1 : (W(x, 1) + hh + 1) >> 1);
-        } else if (fx == 2 || fy == 2) {
-            const int j1 = tap6(B1(x, -2), B1(x, -1), B1(x, 0), B1(x, 1), B1(x, 2), B1(x, 3));
-            const int j = clip255((j1 + 512) >> 10);
-            if (pos == 10) v = j;
-            else if (fy == 2) {           // i (fx=1) or k (fx=3)
-                const int hv = clip255((H1(x + (fx == 3 ? 1 : 0), 0) + 16) >> 5);
-                v = (hv + j + 1) >> 1;
-            } else {                       // f (fy=1) or q (fy=3)
-                const int bv = clip255((B1(x, fy == 3 ? 1 : 0) + 16) >> 5);
-                v = (bv + j + 1) >> 1;
-            }
-        } else {                           // e, g, p, r: diagonal quarter positions
-            const int bv = clip255((B1(x, fy == 3 ? 1 : 0) + 16) >> 5);
-            const int hv = clip255((H1(x + (fx == 3 ? 1 : 0), 0) + 16) >> 5);
-            v = (bv + hv + 1) >> 1;
-        }
-        out[x] = v;
-    }
-#undef W
-#undef B1
-#undef H1
 }
 
 // Register form of luma_row4 (same outputs, h264bsdPredictSamples' 16
@@ -544,12 +490,6 @@ __device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint
     wave_sync();
 }
 
-// ---------------------------------------------------------------------------
-// k_mb: every MB of the batch in parallel (one wave per MB)
-//   all MBs : deblocking record
-//   inter   : residual + 6-tap/bilinear MC + clip-add + write-out
-//   intra   : residual -> scratch (consumed by k_rows)
-// ---------------------------------------------------------------------------
 // per-wave LDS scratch of the MB reconstruction (reference windows)
 struct McScratch {
     int32_t dc[24];
@@ -568,311 +508,6 @@ struct McScratch {
         };
     };
 };
-
-// MB `mb` of picture p (one wave): deblocking record -> db[64]; residual ->
-// res[384] (intra MBs with coded blocks; inter MBs use it as scratch); inter
-// MBs: 6-tap / bilinear MC + residual, clipped, -> px[384] (luma 16x16, Cb
-// 8x8, Cr 8x8).  All outputs in LDS.  PIPE: reference samples written by a
-// picture of this launch are waited for (per-row progress) and read sc1.
-// PROF: *ph receives four 16-bit shader-cycle durations: deblocking record,
-// residual, window landing + LDS staging, interpolation (inter MBs)
-// pre0/pre1: the staged-record words of this MB when has_pre (loaded one MB
-// ahead by the caller); next_mb >= 0: load the next MB's into pre0/pre1 once
-// this MB's are in LDS.
-// PREP: the deblocking record and the residual were computed ahead by k_prep
-// (a.dbrec / a.res); they are loaded (issued after the reference windows)
-// instead of computed.
-template <bool PIPE, bool PROF = false, bool PREP = false>
-__device__ int mc_core(const ReconArgs &a, int p, int mb, int lane, McScratch &M, uint8_t *px, int16_t *res,
-                       uint8_t *db, const Tabs &T, unsigned long long *ph = nullptr, bool has_pre = false,
-                       uint32_t *pre = nullptr, int next_mb = -1)
-{
-    unsigned long long tp0 = PROF ? clock64() : 0, tp1 = 0, tp2 = 0, tp3 = 0;
-    const PicDesc pd = a.pics[p];
-    const int gmb = pd.rec_base + mb;
-    const int mbx = mb % a.w, mby = mb / a.w;
-    {
-        uint32_t v0, v1;
-        if (has_pre) { v0 = pre[0]; v1 = pre[1]; }
-        else stage_recs_load(a, gmb, mbx, mby, lane, v0, v1);
-        M.srec[lane] = v0;
-        if (lane < 8) M.srec[64 + lane] = v1;
-        if (next_mb >= 0) stage_recs_load(a, pd.rec_base + next_mb, next_mb % a.w, next_mb / a.w, lane, pre[0], pre[1]);
-    }
-    wave_sync();
-    const MbRec &r = *(const MbRec *)M.srec;
-    const int rtype = __builtin_amdgcn_readfirstlane(r.type);
-    const uint32_t rcbits = __builtin_amdgcn_readfirstlane(r.cbits);
-    int16_t *s_res = res;
-    uint8_t *s_out = px;
-    // the MB's coded blocks: issued first (before the reference windows), so
-    // that waiting for them (vmcnt retires in order) never waits for a window
-    const int ncw = (PREP || rtype == MBT_IPCM) ? 0 : __popc(rcbits & 0x7FFFFFFu) * 8;
-    const bool has_res = rtype != MBT_IPCM && rcbits != 0;
-    // PREP: this MB's k_prep outputs (loads issued where they are first needed)
-    const gcu8p pdb = uni(a.dbrec + (size_t)gmb * 64);
-    const gcu8p pres = uni(a.res + (size_t)gmb * 384);
-    auto load_prep = [&](uint32_t &dbw, uint32_t &r0, uint32_t &r1, uint32_t &r2) {
-        dbw = ldg32(pdb, (uint32_t)(lane & 15) * 4);
-        r0 = r1 = r2 = 0;
-        if (has_res) { r0 = ldg32(pres, lane * 4); r1 = ldg32(pres, 256 + lane * 4); r2 = ldg32(pres, 512 + lane * 4); }
-    };
-    auto store_prep = [&](uint32_t dbw, uint32_t r0, uint32_t r1, uint32_t r2, bool zero_res) {
-        if (lane < 16) ((uint32_t *)db)[lane] = dbw;
-        if (lane == 15 && (dbw >> 24)) atomicOr(a.err + p, 1u);        // k_prep's range-error byte
-        if (has_res || zero_res) {
-            ((uint32_t *)s_res)[lane] = r0; ((uint32_t *)s_res)[64 + lane] = r1; ((uint32_t *)s_res)[128 + lane] = r2;
-        }
-    };
-    uint32_t cq0 = 0, cq1 = 0, cq2 = 0, cq3 = 0;
-    {
-        const uint32_t *csrc = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + (uint32_t)__builtin_amdgcn_readfirstlane(r.coef)) * 16);
-        if (lane < ncw) cq0 = csrc[lane];
-        if (lane + 64 < ncw) cq1 = csrc[lane + 64];
-        if (lane + 128 < ncw) cq2 = csrc[lane + 128];
-        if (lane + 192 < ncw) cq3 = csrc[lane + 192];
-    }
-    auto stage_coef = [&]() {
-        if (lane < ncw) M.coef[lane] = cq0;
-        if (lane + 64 < ncw) M.coef[lane + 64] = cq1;
-        if (lane + 128 < ncw) M.coef[lane + 128] = cq2;
-        if (lane + 192 < ncw) M.coef[lane + 192] = cq3;
-        wave_sync();
-    };
-
-    if (PREP && rtype >= MBT_I4x4) {
-        uint32_t dbw, r0, r1, r2;
-        load_prep(dbw, r0, r1, r2);
-        store_prep(dbw, r0, r1, r2, false);
-        wave_sync();
-        return rtype;
-    }
-    if (rtype >= MBT_I4x4) {
-        mb_dbrec(a, lane, db, M.srec, T);
-        if (rtype != MBT_IPCM && rcbits) {
-            int e = 0;
-            stage_coef();
-            mb_residual(r, (const int16_t *)M.coef, s_res, M.dc, lane, &e, T.ls);
-            if (e && lane == 0) atomicOr(a.err + p, 1u);
-        }
-        return rtype;
-    }
-
-    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
-    if (PIPE) {
-        // wait for exactly the reference samples this MB reads that a picture
-        // of this launch writes: per 8x8 partition q (one reference slot), the
-        // clamped 6-tap footprint of its four 4x4 blocks; a sample of row R,
-        // column C is final once that row's progress passed C+1 and the row
-        // below's passed C (progress >= C+2 over rows R..R+1)
-        const int kcur = p / a.S, s = p - kcur * a.S;
-        const int b = lane >> 2;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int bx0 = mbx * 16 + blk_x(b) * 4 + (mvx >> 2), by0 = mby * 16 + blk_y(b) * 4 + (mvy >> 2);
-        int xlo = clip3(0, W16 - 1, bx0 - 2), xhi = clip3(0, W16 - 1, bx0 + 6);
-        int ylo = clip3(0, H16 - 1, by0 - 2), yhi = clip3(0, H16 - 1, by0 + 6);
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) {          // reduce over the partition's 16 lanes
-            xlo = min(xlo, __shfl_xor(xlo, m, 64)); xhi = max(xhi, __shfl_xor(xhi, m, 64));
-            ylo = min(ylo, __shfl_xor(ylo, m, 64)); yhi = max(yhi, __shfl_xor(yhi, m, 64));
-        }
-        for (int q = 0; q < 4; q++) {
-            const int x = r.ref[q];
-            const int t = ((x - a.base_pic) % a.ring + a.ring) % a.ring;
-            if (t >= kcur) continue;                 // written before this launch
-            const int pp = t * a.S + s;
-            const int rlo = __builtin_amdgcn_readlane(ylo, 16 * q) >> 4;
-            const int rhi = min(a.h - 1, (__builtin_amdgcn_readlane(yhi, 16 * q) >> 4) + 1);
-            const uint32_t need = (a.epoch << 12) + (uint32_t)min(a.w, (__builtin_amdgcn_readlane(xhi, 16 * q) >> 4) + 2);
-            for (int base = rlo; base <= rhi; base += WAVE) {
-                const int R = base + lane;
-                unsigned spins = 0;
-                for (;;) {
-                    const uint32_t v = R <= rhi ? ld_sc1_u32(a.progress + (size_t)pp * a.h + R) : 0xFFFFFFFFu;
-                    if (__builtin_amdgcn_ballot_w64(v < need) == 0) break;
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > (1u << 20)) { if (lane == 0) atomicOr(a.err + p, 4u); break; }   // bounded wait
-                }
-            }
-        }
-    }
-
-    // Reference windows with aligned dword loads (h264bsdPredictSamples
-    // reads, reconstruct.c:1819-1941; out-of-picture samples clamp like
-    // h264bsdFillBlock, :2222-2314).  Luma: block b = lane>>2 owns window rows
-    // (lane&3)+4k, 3 dwords each from the aligned column ax; chroma: lanes
-    // 0..31 = (block, plane), 3 rows x 2 dwords.  A window crossing the
-    // picture's left/right edge is rebuilt per sample (offset 0).  The loads
-    // are issued first; the deblocking record and the residual are computed
-    // while they are in flight.
-    const uint8_t *frames = a.frames;
-    const int lb = lane >> 2, lsub = lane & 3;
-    const int l_x0 = mbx * 16 + blk_x(lb) * 4 + (r.mv[lb][0] >> 2) - 2;
-    const int l_y0 = mby * 16 + blk_y(lb) * 4 + (r.mv[lb][1] >> 2) - 2;
-    const int l_ax = clip3(0, W16 - 12, l_x0 & ~3);
-    const bool l_in = l_x0 >= 0 && l_x0 + 8 <= W16 - 1;
-    uint32_t lw[3][3];
-    {
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[lb >> 2]) * a.frame_bytes;
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const int wy = lsub + 4 * k;
-            const int y = clip3(0, H16 - 1, l_y0 + min(wy, 8));
-            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + l_ax);
-            lw[k][0] = ld32<PIPE>(src); lw[k][1] = ld32<PIPE>(src + 1); lw[k][2] = ld32<PIPE>(src + 2);
-        }
-    }
-    const int cb = (lane & 31) >> 1, ccomp = lane & 1;
-    const int c_x0 = mbx * 8 + blk_x(cb) * 2 + (r.mv[cb][0] >> 3);
-    const int c_y0 = mby * 8 + blk_y(cb) * 2 + (r.mv[cb][1] >> 3);
-    const int c_ax = clip3(0, CW - 8, c_x0 & ~3);
-    const bool c_in = c_x0 >= 0 && c_x0 + 2 <= CW - 1;
-    uint32_t cw[3][2];
-    {
-        const uint8_t *ref = frames + (unsigned long long)(pd.frame_base + r.ref[cb >> 2]) * a.frame_bytes +
-                             (unsigned long long)W16 * H16 + (unsigned long long)ccomp * CW * CH;
-#pragma unroll
-        for (int wy = 0; wy < 3; wy++) {
-            const int y = clip3(0, CH - 1, c_y0 + wy);
-            const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + c_ax);
-            cw[wy][0] = ld32<PIPE>(src); cw[wy][1] = ld32<PIPE>(src + 1);
-        }
-    }
-
-    int e = 0;
-    if (PREP) {
-        uint32_t dbw, r0, r1, r2;
-        load_prep(dbw, r0, r1, r2);
-        if (PROF) tp1 = clock64();
-        store_prep(dbw, r0, r1, r2, true);
-    } else {
-        mb_dbrec(a, lane, db, M.srec, T);
-        if (PROF) tp1 = clock64();
-        if (rcbits) {
-            stage_coef();
-            mb_residual(r, (const int16_t *)M.coef, s_res, M.dc, lane, &e, T.ls);
-        } else {
-            for (int i = lane; i < 192; i += WAVE) ((uint32_t *)s_res)[i] = 0;
-        }
-    }
-    if (PROF) tp2 = clock64();
-
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int wy = lsub + 4 * k;
-        if (wy >= 9) break;
-        uint32_t d0 = lw[k][0], d1 = lw[k][1], d2 = lw[k][2];
-        if (!l_in) {
-            uint32_t o[3] = {0, 0, 0};
-#pragma unroll
-            for (int i = 0; i < 9; i++) {
-                const int kk = clip3(0, W16 - 1, l_x0 + i) - l_ax;
-                const uint32_t w = kk < 4 ? d0 : (kk < 8 ? d1 : d2);
-                o[i >> 2] |= ((w >> ((kk & 3) * 8)) & 255u) << ((i & 3) * 8);
-            }
-            d0 = o[0]; d1 = o[1]; d2 = o[2];
-        }
-        M.wraw[lb][wy][0] = d0; M.wraw[lb][wy][1] = d1; M.wraw[lb][wy][2] = d2;
-    }
-    if (lsub == 0) M.wxo[lb] = (uint8_t)(l_in ? l_x0 - l_ax : 0);
-    if (lane < 32) {
-#pragma unroll
-        for (int wy = 0; wy < 3; wy++) {
-            uint32_t d0 = cw[wy][0], d1 = cw[wy][1];
-            if (!c_in) {
-                uint32_t o = 0;
-#pragma unroll
-                for (int i = 0; i < 3; i++) {
-                    const int kk = clip3(0, CW - 1, c_x0 + i) - c_ax;
-                    const uint32_t w = kk < 4 ? d0 : d1;
-                    o |= ((w >> ((kk & 3) * 8)) & 255u) << (i * 8);
-                }
-                d0 = o;
-            }
-            M.craw[ccomp][cb][wy][0] = d0; M.craw[ccomp][cb][wy][1] = d1;
-        }
-        M.cxo[ccomp][cb] = (uint8_t)(c_in ? c_x0 - c_ax : 0);
-    }
-    wave_sync();
-    if (PROF) tp3 = clock64();
-
-    {   // luma: lane -> (block, row)
-        const int b = lane >> 2, yy = lane & 3;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        int o[4];
-        const int fx = mvx & 3, fy = mvy & 3;
-        const bool need_j = __builtin_amdgcn_ballot_w64(fx != 0 && fy != 0 && (fx == 2 || fy == 2)) != 0;
-        luma_row4_reg(&M.wraw[b][yy], M.wxo[b], fx, fy, need_j, o);
-        const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
-#pragma unroll
-        for (int x = 0; x < 4; x++) s_out[by * 16 + bx + x] = (uint8_t)clip255(o[x] + s_res[by * 16 + bx + x]);
-    }
-    {   // chroma: lane -> (block, comp, row), 2 samples
-        const int b = lane >> 2, comp = (lane >> 1) & 1, yy = lane & 1;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int fx = mvx & 7, fy = mvy & 7;
-        const uint8_t *w = (const uint8_t *)&M.craw[comp][b][0][0] + M.cxo[comp][b];
-        const int cx = blk_x(b) * 2, cy = blk_y(b) * 2 + yy;
-#pragma unroll
-        for (int x = 0; x < 2; x++) {
-            const int A = w[yy * 8 + x], B = w[yy * 8 + x + 1], C = w[(yy + 1) * 8 + x], D = w[(yy + 1) * 8 + x + 1];
-            const int v = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
-            s_out[256 + comp * 64 + cy * 8 + cx + x] = (uint8_t)clip255(v + s_res[256 + comp * 64 + cy * 8 + cx + x]);
-        }
-    }
-    wave_sync();
-
-    if (lane == 0 && e) atomicOr(a.err + p, 1u);
-    if (PROF && ph) {
-        const unsigned long long tp4 = clock64();
-        auto d16 = [](unsigned long long d) { return d > 65535 ? 65535ull : d; };
-        *ph = d16(tp1 - tp0) | d16(tp2 - tp1) << 16 | d16(tp3 - tp2) << 32 | d16(tp4 - tp3) << 48;
-    }
-    return rtype;
-}
-
-// k_mb: every MB of the batch in parallel, one wave per MB.  XCD-aware MB
-// order: workgroups are dealt round-robin over the 8 XCDs (speed only, not
-// correctness), so XCD x = blockIdx % 8 gets the x-th contiguous eighth of the
-// batch -- neighbouring MBs share its L2 when their reference windows overlap.
-// Outputs to HBM for k_rows: deblocking record, intra residual, inter samples.
-__global__ __launch_bounds__(64) void k_mb(ReconArgs a)
-{
-    __shared__ McScratch M;
-    __shared__ uint8_t s_px[384];
-    __shared__ int16_t s_res[384];
-    __shared__ uint8_t s_db[64];
-    const int nmbs = a.w * a.h;
-    const int total = a.npics * nmbs;
-    const int chunk = (total + 7) >> 3;
-    const int gidx = (blockIdx.x & 7) * chunk + (blockIdx.x >> 3);
-    if (gidx >= total) return;
-    const int p = gidx / nmbs, mb = gidx - p * nmbs, lane = threadIdx.x;
-    const PicDesc &pd = a.pics[p];
-    const int gmb = pd.rec_base + mb;
-    const Tabs T = load_tabs(lane);
-    const int type = mc_core<false>(a, p, mb, lane, M, s_px, s_res, s_db, T);
-    if (lane < 16) ((uint32_t *)(a.dbrec + (size_t)gmb * 64))[lane] = ((const uint32_t *)s_db)[lane];
-    if (type >= MBT_I4x4) {
-        if (type != MBT_IPCM && a.rec[gmb].cbits) {
-            uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
-            for (int i = lane; i < 192; i += WAVE) dst[i] = ((const uint32_t *)s_res)[i];
-        }
-        return;
-    }
-    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
-    const int mbx = mb % a.w, mby = mb / a.w;
-    uint8_t *cur = a.frames + (unsigned long long)(pd.frame_base + pd.cur_slot) * a.frame_bytes;
-    {
-        const int row = lane >> 2, q4 = lane & 3;
-        *(uint32_t *)(cur + (size_t)(mby * 16 + row) * W16 + mbx * 16 + q4 * 4) = *(const uint32_t *)(s_px + row * 16 + q4 * 4);
-    }
-    if (lane < 32) {
-        const int comp = lane >> 4, row = (lane >> 1) & 7, q2 = lane & 1;
-        uint8_t *cp = cur + (size_t)W16 * H16 + (size_t)comp * CW * CH;
-        *(uint32_t *)(cp + (size_t)(mby * 8 + row) * CW + mbx * 8 + q2 * 4) = *(const uint32_t *)(s_px + 256 + comp * 64 + row * 8 + q2 * 4);
-    }
-}
 
 // k_prep: the per-MB work that does not depend on any reconstructed sample --
 // deblocking record (bS + thresholds) and residual (dequant + inverse
@@ -1135,46 +770,8 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
     wave_sync();
 }
 
-// ---------------------------------------------------------------------------
-// k_rows: intra reconstruction + in-loop deblocking.  One single-wave
-// workgroup per MB row (grid = rows x pictures, blockIdx = row * npics + pic
-// so a picture's rows share one XCD under round-robin placement -- speed
-// only).  The wave walks its row left to right; MB (r,c) needs the row above
-// finished through (r-1,c+1) -- the raster-order dependencies of intra
-// prediction and h264bsdFilterPicture (deblocking.c:603-637).
-//
-// Row hand-off (row r -> row r+1) goes through a per-row mailbox in HBM,
-// 32 granules per MB column, each granule = {dword of data, launch epoch}
-// written by ONE 8-byte sc1 store (MI355X_MICROARCH.md, R2 granules: no
-// fence, no drain, no flag); the consumer re-reads with 8-byte sc1 loads
-// until every tag carries this launch's epoch.  Entry layout (dwords):
-//   [0..15]  luma rows 12..15 (final once the next MB's vertical edges ran)
-//   [16..23] Cb/Cr rows 6..7 (dword = comp*4 + row*2 + half)
-//   [24..31] unfiltered bottom row Y16 U8 V8 (intra neighbours of row r+1)
-// Every output sample is written exactly once, by the MB that finalises it,
-// so no other ordering of frame stores is needed.
-// ---------------------------------------------------------------------------
-// One MB row per single-wave workgroup.  (Measured at 1080p x 8 streams:
-// bands of 2/4/8 rows per workgroup handing off through an LDS ring ran
-// 969/977/1025 us per launch vs 950 us -- the row lag is set by the MB
-// dependency chain, not by the hand-off latency.)
 #define RY_S 20       // region luma stride (cols -4..15)
 #define RC_S 20       // region chroma stride (cols -4..7, padded to the luma stride)
-
-struct __attribute__((aligned(16))) RowLds {
-    int16_t res[384];
-    uint8_t db[64];
-    uint8_t ry[20 * RY_S];      // rows -4..15
-    uint8_t ru[10 * RC_S];      // rows -2..7
-    uint8_t rv[10 * RC_S];
-    uint8_t ty[17 * TY_STRIDE];
-    uint8_t tu[9 * TC_STRIDE];
-    uint8_t tv[9 * TC_STRIDE];
-    uint8_t left_unf[32];       // unfiltered right column of the previous MB: Y16 U8 V8
-    uint8_t junk[256];          // per-lane sink of unconditional LDS stores (lanes with nothing to store)
-    uint32_t i4tab[9 * 16];     // intra 4x4 prediction table (i4_entry), mode x position
-    uint8_t sx[32];             // gathered neighbours of the two blocks of an intra 4x4 step
-};
 
 
 __device__ __forceinline__ int absd(int a, int b) { return (int)__builtin_amdgcn_sad_u8((unsigned)a, (unsigned)b, 0u); }
@@ -1381,407 +978,6 @@ struct __attribute__((aligned(16))) MbRing {
 __device__ __forceinline__ int lds_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
-// One MB row of picture p, left to right (one wave).  RING: MB c's MC
-// outputs come from the workgroup's MC waves through the LDS ring (k_wg);
-// otherwise from k_mb's HBM outputs (k_rows).  PIPE (RING only): frame
-// stores are sc1 and per-row progress is published for later pictures' MC.
-template <bool PIPE, bool RING, bool PROF>
-__device__ void row_unit(const ReconArgs &a, int p, int r, RowLds &L, int lane, MbRing *R)
-{
-    static_assert(RING || !PIPE, "pipelined row units take MC outputs from the LDS ring");
-    const int W = a.w, H = a.h;
-    const PicDesc *pdp = a.pics + p;
-    const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
-    const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
-    const int coef_base = __builtin_amdgcn_readfirstlane(pdp->coef_base);
-    const int W16 = W * 16, H16 = H * 16, CW = W16 / 2, CH = H16 / 2;
-    uint8_t *cur = a.frames + (unsigned long long)fslot * a.frame_bytes;
-    uint8_t *curU = cur + (size_t)W16 * H16;
-    uint8_t *curV = curU + (size_t)CW * CH;
-    unsigned *perr = a.err + p;
-    const uint32_t tag = a.epoch;
-    const bool has_up = r > 0, has_down = r + 1 < H;
-    const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
-    unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
-    const bool last_row = r == H - 1;
-    // record words through the constant address space: uniform scalar
-    // (SMEM) loads, counted by lgkmcnt instead of the in-order vmcnt
-    typedef const __attribute__((address_space(4))) uint32_t *cu32p;
-    const cu32p recw = (cu32p)(const void *)(a.rec + rec_base + r * W);   // 24 dwords per record
-
-    // lane roles for dword transfers
-    const int orow = lane >> 2, oq = lane & 3;                                   // luma 16x16
-    const int li = lane & 31;
-    const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;          // chroma (lanes 32..63 mirror)
-    // final-rows entry dword of this lane: 0..23; lanes with li 24..31 repeat
-    // li 16..23, so every lane of the publishing store carries real data
-    const int le = li < 24 ? li : li - 8;
-    // global accesses: uniform (SGPR) base + 32-bit per-lane offset
-    uint8_t *const ybase = cur + (size_t)r * 16 * W16;                   // MB row r, luma
-    uint8_t *const cbase = curU + (size_t)r * 8 * CW;                    // MB row r, Cb (Cr at +CW*CH)
-    const uint32_t yoff = (uint32_t)(orow * W16 + oq * 4);
-    const uint32_t coff = (uint32_t)(ccomp * CW * CH + crow * CW + cq * 4);
-    // common-case frame stores of iteration c (not the last row or column):
-    // set A (luma, 64 lanes): own rows 0..11 x cols 0..11 (lanes 0..35), the
-    // left MB's cols 12..15 rows 0..11 (36..47, c > 0), the row above's rows
-    // 12..15 (48..63, r > 0); set B (chroma, lanes 0..31): own rows 0..5 x
-    // cols 0..3 (0..11), left MB's cols 4..7 (12..23), the row above's rows
-    // 6..7 (24..31).  Offsets are relative to (row r*16-4 | r*8-2, col -4).
-    uint32_t sa_lds, sa_glb, sb_lds, sb_glb;
-    bool sa_left, sa_top, sb_left, sb_top;
-    {
-        const int Lry = (int)(L.ry - (uint8_t *)&L), Lru = (int)(L.ru - (uint8_t *)&L), Lrv = (int)(L.rv - (uint8_t *)&L);
-        int row, col, lo;
-        if (lane < 36) { row = lane / 3; col = (lane % 3) * 4; }
-        else if (lane < 48) { row = lane - 36; col = -4; }
-        else { row = -4 + ((lane - 48) >> 2); col = ((lane - 48) & 3) * 4; }
-        sa_lds = (uint32_t)(Lry + (row + 4) * RY_S + 4 + col);
-        sa_glb = (uint32_t)((row + 4) * W16 + col + 4);
-        sa_left = lane >= 36 && lane < 48;
-        sa_top = lane >= 48;
-        int comp;
-        const int k = lane & 31;
-        if (k < 12) { comp = k / 6; row = k % 6; col = 0; }
-        else if (k < 24) { comp = (k - 12) / 6; row = (k - 12) % 6; col = -4; }
-        else { comp = (k - 24) >> 2; row = -2 + (((k - 24) >> 1) & 1); col = ((k - 24) & 1) * 4; }
-        lo = comp ? Lrv : Lru;
-        sb_lds = (uint32_t)(lo + (row + 2) * RC_S + 4 + col);
-        sb_glb = (uint32_t)(comp * CW * CH + (row + 2) * CW + col + 4);
-        sb_left = k >= 12 && k < 24;
-        sb_top = k >= 24;
-    }
-    // end-of-iteration shift (cols 12..15 / 4..7 -> the next MB's left halo):
-    // lanes 0..15 luma rows, 16..31 chroma rows, 32..63 into their junk slots
-    uint32_t sh_src, sh_dst;
-    {
-        uint8_t *D;
-        int off, step;
-        if (lane < 16) { D = L.ry; off = (lane + 4) * RY_S; step = 16; }
-        else { const int k = (lane - 16) & 15; D = (k >> 3) ? L.rv : L.ru; off = ((k & 7) + 2) * RC_S; step = 8; }
-        sh_src = (uint32_t)((int)(D - (uint8_t *)&L) + off + step);
-        sh_dst = lane < 32 ? (uint32_t)((int)(D - (uint8_t *)&L) + off) : (uint32_t)((int)(L.junk - (uint8_t *)&L) + lane * 4);
-    }
-    // top-entry fetch lane map: lanes 0..31 entry c dword lane; 32: entry c+1
-    // dword 24; 33..35: entry c-1 dwords 27/29/31; others: dummy (entry c dword 0)
-    const int tdsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;   // entry c + tdsel (clamped)
-    const int tdw = lane < 32 ? lane : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 0;
-    // LDS slots of MB c's own samples: luma all lanes, chroma lanes 0..31
-    // (32..63 into their junk slots); deblocking record lanes 0..15
-    const uint32_t own_y_lds = (uint32_t)((int)(L.ry - (uint8_t *)&L) + (orow + 4) * RY_S + 4 + oq * 4);
-    const uint32_t own_c_lds = lane < 32 ? (uint32_t)((int)((ccomp ? L.rv : L.ru) - (uint8_t *)&L) + (crow + 2) * RC_S + 4 + cq * 4)
-                                         : (uint32_t)((int)(L.junk - (uint8_t *)&L) + lane * 4);
-    const uint32_t db_lds = lane < 16 ? (uint32_t)((int)(L.db - (uint8_t *)&L) + lane * 4)
-                                      : (uint32_t)((int)(L.junk - (uint8_t *)&L) + lane * 4);
-
-    uint32_t *progress_me = PIPE ? a.progress + (size_t)p * H + r : nullptr;
-    // global stores are unconditional: lanes with nothing to store write this
-    // row's sink granule instead.  Stores skipped by an exec-mask branch leave
-    // the waitcnt pass unable to count them, and it then waits for every
-    // store of the iteration (vmcnt(0)) before the next MB's prefetched data
-    unsigned long long *const sink = a.gjunk + ((p * H + r) & 127) * 64 + lane;
-
-    // prefetch registers for MB (r, 0)
-    uint32_t n_db = 0, n_y = 0, n_c = 0, n_r0 = 0, n_r1 = 0, n_r2 = 0;
-    uint32_t n_h0, n_h1, n_h2, n_h3, n_h4, n_h5;   // record dwords 0..5 (uniform)
-    {
-        if (!RING) {
-            const int g0 = rec_base + r * W;
-            n_db = ((const uint32_t *)(a.dbrec + (size_t)g0 * 64))[lane & 15];
-            n_y = *(const uint32_t *)(ybase + yoff);
-            n_c = *(const uint32_t *)(cbase + coff);
-            const uint32_t *rs = (const uint32_t *)(a.res + (size_t)g0 * 384);
-            n_r0 = rs[lane]; n_r1 = rs[64 + lane]; n_r2 = rs[128 + lane];
-        }
-        n_h0 = recw[0]; n_h1 = recw[1]; n_h2 = recw[2]; n_h3 = recw[3]; n_h4 = recw[4]; n_h5 = recw[5];
-        // retire these before the loop: otherwise the waitcnt pass merges their
-        // pending state into the loop header and, inside the loop, waits for
-        // each iteration's newest loads before reusing these registers
-        __builtin_amdgcn_s_waitcnt(0x0F70);     // vmcnt(0)
-    }
-    unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bool prof = PROF && a.prof != nullptr;     // PROF = false: no clock code at all
-    if (!RING)       // (k_wg builds it in its prologue, for the MC waves too)
-        for (int e = lane; e < 9 * 16; e += WAVE) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
-    const unsigned long long tstart = prof ? wall_clock64() : 0;
-    uint32_t prov = 0;          // lanes 0..31: this row's mailbox entry of the previous MB (provisional)
-
-    for (int c = 0; c < W; c++) {
-        const uint32_t h0 = __builtin_amdgcn_readfirstlane(n_h0), h1 = __builtin_amdgcn_readfirstlane(n_h1);
-        const uint32_t cbits = __builtin_amdgcn_readfirstlane(n_h2), qcoef = __builtin_amdgcn_readfirstlane(n_h3);
-        const uint64_t i4 = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(n_h5) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(n_h4);
-        const int qtype = h0 & 255, avail = (h0 >> 24) & 255, pred = h1 & 255;
-        const bool intra = qtype >= MBT_I4x4;
-        const bool dbf = avail & DB_INNER;
-        unsigned long long tc0 = prof ? clock64() : 0, tc1;
-        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
-        if (prof && lane == 0) pmb[0] = wall_clock64();
-        // ---- MB c's own samples / residual / deblocking record into LDS, from
-        //      the registers the previous iteration prefetched them into (before
-        //      this iteration's prefetch reuses them).  Unconditional: intra
-        //      MBs overwrite the samples, inter MBs never read the residual.
-        const int slot = c & (RING_K - 1);
-        {
-            uint32_t own_y = n_y, own_c = n_c, own_db = n_db;
-            if (RING) {
-                unsigned spins = 0;
-                const unsigned long long tw = prof ? clock64() : 0;
-                while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
-                }
-                wave_sync();
-                if (prof) pt[7] += clock64() - tw;
-                // MB c reconstructed: MB c-1's slot (its left neighbour) is free
-                if (lane == 0) lds_st(&R->consumed, c);
-                own_y = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
-                own_c = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
-                own_db = ((const uint32_t *)R->db[slot])[lane & 15];
-            }
-            uint8_t *const Lb = (uint8_t *)&L;
-            *(uint32_t *)(Lb + db_lds) = own_db;
-            *(uint32_t *)(Lb + own_y_lds) = own_y;
-            *(uint32_t *)(Lb + own_c_lds) = own_c;
-            if (!RING) {
-                ((uint32_t *)L.res)[lane] = n_r0;
-                ((uint32_t *)L.res)[64 + lane] = n_r1;
-                ((uint32_t *)L.res)[128 + lane] = n_r2;
-            }
-            if (!RING && qtype == MBT_IPCM) {      // (RING: the MC wave put the samples in the slot)
-                const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)coef_base + qcoef) * 16);
-                const uint32_t py = src[lane], pc = src[64 + li];
-                *(uint32_t *)(Lb + own_y_lds) = py;
-                *(uint32_t *)(Lb + own_c_lds) = pc;
-            }
-        }
-        // speculative read of the row above's granules (issued before the
-        // prefetch: vmcnt retires in order, so waiting for it must not wait
-        // for the prefetch); re-read until the needed ones carry this epoch.
-        // Lanes 24..35 (unfiltered samples: intra neighbours) are published
-        // right after the row above reconstructs an MB; lanes 0..23 (final
-        // rows) after its next MB's vertical edges.
-        const int ce = min(max(c + tdsel, 0), W - 1);
-        const unsigned long long *tga = mbx_up + ce * 32 + tdw;
-        unsigned long long gr = ld_gran(tga);     // r == 0: own row's mailbox, value unused
-        // ---- prefetch MB (r, c+1) (clamped: the last iteration re-reads MB W-1)
-        {
-            const int cn = min(c + 1, W - 1);
-            if (!RING) {
-                const int gn = rec_base + r * W + cn;
-                n_db = ldg32(uni(a.dbrec + (size_t)gn * 64), (uint32_t)(lane & 15) * 4);
-                n_y = ldg32(uni(ybase + cn * 16), yoff);
-                n_c = ldg32(uni(cbase + cn * 8), coff);
-                const gcu8p rs = uni(a.res + (size_t)gn * 384);
-                n_r0 = ldg32(rs, lane * 4); n_r1 = ldg32(rs, 256 + lane * 4); n_r2 = ldg32(rs, 512 + lane * 4);
-            }
-            const cu32p rw = recw + cn * 24;
-            n_h0 = rw[0]; n_h1 = rw[1]; n_h2 = rw[2]; n_h3 = rw[3]; n_h4 = rw[4]; n_h5 = rw[5];
-        }
-
-        // ---- row above: wait until entry c is final, then fetch it (+ the
-        //      neighbours' unfiltered samples for intra).  Intra MBs need it
-        //      before prediction; all others only before the horizontal edges.
-        uint32_t top = 0;
-        auto fetch_top = [&](bool unfiltered) {
-            const bool mine = unfiltered ? (lane >= 24 && lane < 36) : lane < 24;
-            unsigned spins = 0;
-            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-                if (mine) gr = ld_gran(tga);          // re-poll only the granules still needed
-            }
-            top = (uint32_t)gr;
-            if (prof && !RING && lane == 0) pmb[1] = wall_clock64();   // (RING: slot 1 holds the MC phases)
-        };
-        const bool early = !RING && has_up && intra && qtype != MBT_IPCM;
-        if (early) fetch_top(true);
-        if (prof) { tc1 = clock64(); pt[0] += tc1 - tc0; tc0 = tc1; }
-
-        if (!RING && intra && qtype != MBT_IPCM) {     // (RING: reconstructed by the MC waves)
-            const bool aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
-            const uint32_t b0 = top & 255, b1 = (top >> 8) & 255, b2 = (top >> 16) & 255, b3 = top >> 24;
-            if (lane >= 24 && lane < 32) {
-                if (aB) {
-                    const int k = lane - 24;
-                    uint8_t *dst = k < 4 ? &L.ty[1 + k * 4] : (k < 6 ? &L.tu[1 + (k - 4) * 4] : &L.tv[1 + (k - 6) * 4]);
-                    dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
-                }
-            } else if (lane == 32) {
-                if (aC) { L.ty[17] = b0; L.ty[18] = b1; L.ty[19] = b2; L.ty[20] = b3; }
-            } else if (lane < 36) {
-                if (aD) (lane == 33 ? L.ty[0] : lane == 34 ? L.tu[0] : L.tv[0]) = b3;
-            } else if (lane >= 40 && lane < 56) L.ty[(lane - 39) * TY_STRIDE] = L.left_unf[lane - 40];
-            else if (lane >= 56) {
-                const int k = lane - 56;
-                L.tu[(k + 1) * TC_STRIDE] = L.left_unf[16 + k];
-                L.tv[(k + 1) * TC_STRIDE] = L.left_unf[24 + k];
-            }
-            wave_sync();
-            intra_tile(qtype, avail, pred, i4, RING ? R->res[slot] : L.res, cbits != 0, L.ty, L.tu, L.tv, L.i4tab, L.sx,
-                       L.junk, lane);
-            {   // tile samples start at column 1: byte reads (LDS dword reads must be aligned)
-                const uint8_t *sy = &L.ty[(orow + 1) * TY_STRIDE + 1 + oq * 4];
-                *(uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4] = sy[0] | (sy[1] << 8) | (sy[2] << 16) | ((uint32_t)sy[3] << 24);
-            }
-            if (lane < 32) {
-                const uint8_t *T = ccomp ? L.tv : L.tu;
-                uint8_t *D = ccomp ? L.rv : L.ru;
-                const uint8_t *sp = &T[(crow + 1) * TC_STRIDE + 1 + cq * 4];
-                *(uint32_t *)&D[(crow + 2) * RC_S + 4 + cq * 4] = sp[0] | (sp[1] << 8) | (sp[2] << 16) | ((uint32_t)sp[3] << 24);
-            }
-        }
-        wave_sync();
-
-        // ---- unfiltered edges: bottom row (mailbox dwords 24..31), right column
-        //      (RING: published by the MC waves)
-        if (!RING) {
-            uint32_t unf;
-            const int k = li & 7;     // lanes 24..31 (mirrored for the rest)
-            const uint8_t *ub = k < 4 ? &L.ry[19 * RY_S + 4 + k * 4] : k < 6 ? &L.ru[9 * RC_S + 4 + (k - 4) * 4] : &L.rv[9 * RC_S + 4 + (k - 6) * 4];
-            unf = *(const uint32_t *)ub;
-            const uint8_t *rcp = li < 16 ? &L.ry[(li + 4) * RY_S + 19] : li < 24 ? &L.ru[(li - 16 + 2) * RC_S + 11] : &L.rv[(li - 24 + 2) * RC_S + 11];
-            const uint8_t rc = *rcp;
-            wave_sync();
-            *(lane < 32 ? &L.left_unf[lane] : &L.junk[lane]) = rc;
-            // publish this MB's unfiltered bottom row (the row below's intra neighbours)
-            // (every lane: lanes with equal li & 7 hold the same dword, so the
-            // duplicates store identical data to the same granule)
-            st_gran(has_down ? mbx_me + (size_t)c * 32 + 24 + (li & 7) : sink, unf, tag);
-        }
-        if (prof) { tc1 = clock64(); pt[6] += tc1 - tc0; tc0 = tc1; }
-        // ---- vertical edges (need only this row's samples), with the
-        //      hand-off in between: the final rows of MB c-1 (entry dwords
-        //      0..23) are final once this MB's left edge is filtered -- the
-        //      internal edges never touch MB c-1 -- so they go to the row
-        //      below before the internal edges run
-        auto publish = [&]() {
-            const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-            const uint32_t patch = le < 16 ? *(const uint32_t *)&L.ry[(16 + (le >> 2)) * RY_S]
-                                           : *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S];
-            const bool is_patch = le < 16 ? (le & 3) == 3 : qq;
-            const uint32_t ent = is_patch ? patch : prov;
-            st_gran(has_down && c > 0 ? mbx_me + (size_t)(c - 1) * 32 + le : sink, ent, tag);
-            if (prof && lane == 0) pmb[2] = wall_clock64();
-        };
-        if (dbf) deblock_dir(0, L.db, L.ry, L.ru, L.rv, L.junk, lane, avail & DB_LEFT, publish);
-        else publish();
-        wave_sync();
-        if (prof) { tc1 = clock64(); pt[1] += tc1 - tc0; tc0 = tc1; }
-
-        // ---- top halo, horizontal edges
-        if (has_up) {
-            fetch_top(false);
-            if (lane < 16) *(uint32_t *)&L.ry[orow * RY_S + 4 + oq * 4] = top;              // rows -4..-1
-            else if (lane < 24) {
-                const int k = lane - 16, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-                *(uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4] = top;          // rows -2..-1
-            }
-            wave_sync();
-        }
-        if (prof) { tc1 = clock64(); pt[5] += tc1 - tc0; tc0 = tc1; }
-        if (dbf) {
-            deblock_dir(1, L.db, L.ry, L.ru, L.rv, L.junk, lane, avail & DB_TOP);
-            wave_sync();
-        }
-        // provisional entry c (rows 12..15 final except columns 13..15)
-        if (has_down) {
-            const int k = le - 16, comp = (k >> 2) & 1, row = (k >> 1) & 1, qq = k & 1;
-            const uint32_t pl = *(const uint32_t *)&L.ry[(16 + ((le >> 2) & 3)) * RY_S + 4 + (le & 3) * 4];
-            const uint32_t pc = *(const uint32_t *)&(comp ? L.rv : L.ru)[(8 + row) * RC_S + 4 + qq * 4];
-            prov = le < 16 ? pl : pc;
-        }
-        if (prof) { tc1 = clock64(); pt[2] += tc1 - tc0; tc0 = tc1; }
-
-        // ---- frame stores, once per sample
-        if (PIPE) {
-            // the stores of iterations < c have had a whole iteration to land:
-            // drain them and tell the next picture's MC (progress = c)
-            drain_vm();
-            st_sc1_u32(progress_me, (tag << 12) | (uint32_t)c);      // every lane: same dword, same value
-        }
-        if (!last_row && c != W - 1) {
-            // common case: two store instructions (see the lane maps above)
-            const uint32_t va = *(const uint32_t *)((const uint8_t *)&L + sa_lds);
-            const uint32_t vb = *(const uint32_t *)((const uint8_t *)&L + sb_lds);
-            uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
-            uint8_t *const cb = cbase + c * 8 - 2 * CW - 4;
-            const bool oka = (!sa_left || c > 0) && (!sa_top || has_up);
-            const bool okb = (!sb_left || c > 0) && (!sb_top || has_up);     // lanes 32..63 repeat 0..31
-            st32<PIPE>(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
-            st32<PIPE>(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
-        } else {
-            const int yrows = last_row ? 16 : 12;
-            const int crows = last_row ? 8 : 6;
-            const bool last_col = c == W - 1;
-            if (orow < yrows && (oq < 3 || last_col))
-                st32<PIPE>(ybase + c * 16 + yoff, *(const uint32_t *)&L.ry[(orow + 4) * RY_S + 4 + oq * 4]);
-            if (lane < 32 && crow < crows && (cq == 0 || last_col))
-                st32<PIPE>(cbase + c * 8 + coff, *(const uint32_t *)&(ccomp ? L.rv : L.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
-            if (c > 0) {    // left halo: MB (r,c-1) luma cols 12..15 / chroma cols 4..7
-                if (lane < 16) {
-                    if (lane < yrows)
-                        st32<PIPE>(ybase + c * 16 - 4 + lane * W16, *(const uint32_t *)&L.ry[(lane + 4) * RY_S]);
-                } else if (lane < 32) {
-                    const int k = lane - 16, comp = k >> 3, row = k & 7;
-                    if (row < crows)
-                        st32<PIPE>(cbase + c * 8 - 4 + comp * CW * CH + row * CW, *(const uint32_t *)&(comp ? L.rv : L.ru)[(row + 2) * RC_S]);
-                }
-            }
-            if (has_up) {   // top halo: MB (r-1,c) luma rows 12..15, chroma rows 6..7 (now final)
-                if (lane >= 32 && lane < 48) {
-                    const int k = lane - 32;
-                    st32<PIPE>(ybase + c * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&L.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
-                } else if (lane >= 48 && lane < 56) {
-                    const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-                    st32<PIPE>(cbase + c * 8 + qq * 4 + comp * CW * CH + (row - 2) * CW, *(const uint32_t *)&(comp ? L.rv : L.ru)[row * RC_S + 4 + qq * 4]);
-                }
-            }
-        }
-        wave_sync();
-        // ---- shift: this MB's cols 12..15 / 4..7 become the next MB's left halo
-        *(uint32_t *)((uint8_t *)&L + sh_dst) = *(const uint32_t *)((const uint8_t *)&L + sh_src);
-        wave_sync();
-        if (prof) { tc1 = clock64(); pt[4] += tc1 - tc0; }
-    }
-    // last entry of the row is final as it stands
-    if (has_down) {
-        if (lane < 24) st_gran(mbx_me + (size_t)(W - 1) * 32 + lane, prov, tag);
-    }
-    if (PIPE) {
-        drain_vm();
-        if (lane == 0) st_sc1_u32(progress_me, (tag << 12) | (uint32_t)W);
-    }
-    if (prof && lane == 0) {
-        unsigned long long *o = a.prof + ((size_t)r * a.npics + p) * 16;
-        o[0] = tstart; o[1] = wall_clock64();
-        for (int i = 0; i < 8; i++) o[2 + i] = pt[i];
-    }
-}
-
-template <bool PROF>
-__global__ __launch_bounds__(64) void k_rows(ReconArgs a)
-{
-    __shared__ RowLds L;
-    const int p = blockIdx.x % a.npics, r = blockIdx.x / a.npics;
-    if (r >= a.h) return;
-    // the row chain wins issue over concurrent k_mb waves (stream groups)
-    __builtin_amdgcn_s_setprio(3);
-    row_unit<false, false, PROF>(a, p, r, L, threadIdx.x, nullptr);
-}
-
-// ---------------------------------------------------------------------------
-// k_wg: one workgroup per (picture, MB row): wave 0 is the row unit, waves
-// 1..NMC compute the row's MBs (deblocking record, residual, MC) round-robin
-// into the LDS ring, at most RING_K MBs ahead of the row unit.  No HBM round
-// trip between MC and reconstruction.
-//
-// The launch covers P pictures of S streams (picture index k*S + s); the host
-// orders the (k, r) pairs in a.order so that a workgroup only ever waits on
-// workgroups dispatched before it (dispatch follows blockIdx; every wait is
-// bounded): the row above (tagged granules) and, PIPE, the rows of earlier
-// pictures of the launch its MVs reach (per-row progress, sc1 stores/loads).
-// blockIdx = pair * S + s, so with round-robin placement stream s stays on
-// XCD s % 8 (speed only).
-// ---------------------------------------------------------------------------
 // k_wg MC wave, intra MB c of row r: unfiltered neighbours -> prediction
 // tile -> the MB's ring slot (reconstruction runs ahead of the deblocking
 // row unit; intra prediction reads unfiltered samples only).  Left: MB c-1's
@@ -1861,84 +1057,6 @@ __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const uns
     }
     wave_sync();
 }
-
-template <bool PIPE, int NMC, bool PROF, bool PREP = false>
-__global__ __launch_bounds__(64 * (NMC + 1)) void k_wg(ReconArgs a)
-{
-    __shared__ RowLds L;
-    __shared__ McScratch M[NMC];
-    __shared__ MbRing R;
-    const int S = a.S;
-    const int pair = blockIdx.x / S, s = blockIdx.x - pair * S;
-    const uint32_t kr = a.order[pair];
-    const int k = (int)(kr >> 16), r = (int)(kr & 0xFFFF);
-    const int p = k * S + s;
-    if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
-    if (threadIdx.x == 0) R.consumed = 0;
-    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 1)) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
-    __syncthreads();
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wid == 0) {
-        // the row unit is the dependency chain: it wins issue over the MC
-        // waves sharing its SIMD
-        __builtin_amdgcn_s_setprio(3);
-        row_unit<PIPE, true, PROF>(a, p, r, L, lane, &R);
-        return;
-    }
-    McScratch &Mw = M[wid - 1];
-    const Tabs T = load_tabs(lane);
-    uint32_t pre[2] = {0, 0};
-    bool has_pre = false;
-    for (int c = wid - 1; c < a.w; c += NMC) {
-        const int slot = c & (RING_K - 1);
-        if (c >= RING_K) {
-            unsigned spins = 0;
-            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RING_K + 1) {
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }   // bounded wait
-            }
-            wave_sync();
-        }
-        const unsigned long long t0 = PROF ? clock64() : 0;
-        unsigned long long ph = 0;
-        const int type = mc_core<PIPE, PROF, PREP>(a, p, r * a.w + c, lane, Mw, R.px[slot], R.res[slot], R.db[slot], T, &ph,
-                                             has_pre, pre, c + NMC < a.w ? r * a.w + c + NMC : -1);
-        has_pre = true;
-        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 1] = ph;
-        if (type == MBT_IPCM) {
-            const PicDesc &pd = a.pics[p];
-            const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
-            ((uint32_t *)R.px[slot])[lane] = src[lane];
-            if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
-        } else if (type >= MBT_I4x4) {
-            const PicDesc &pd = a.pics[p];
-            mc_intra(a.rec + pd.rec_base + r * a.w + c, a.mbx + ((size_t)p * a.h + (r > 0 ? r - 1 : 0)) * a.w * 32,
-                     a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, L.i4tab);
-        }
-        wave_sync();
-        {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
-            const int k = lane & 7;
-            const uint8_t *px = R.px[slot];
-            const uint32_t v = *(const uint32_t *)&px[k < 4 ? 240 + k * 4 : k < 6 ? 312 + (k - 4) * 4 : 376 + (k - 6) * 4];
-            if (r + 1 < a.h)
-                st_gran(a.mbx + ((size_t)p * a.h + r) * a.w * 32 + c * 32 + 24 + k, v, a.epoch);
-        }
-        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
-        if (lane == 0) lds_st(&R.flag[slot], c + 1);
-    }
-}
-template __global__ void k_wg<false, 2, false>(ReconArgs);
-template __global__ void k_wg<false, 3, false>(ReconArgs);
-template __global__ void k_wg<false, 4, false>(ReconArgs);
-template __global__ void k_wg<false, 3, true>(ReconArgs);
-template __global__ void k_wg<true, 2, false>(ReconArgs);
-template __global__ void k_wg<true, 3, false>(ReconArgs);
-template __global__ void k_wg<true, 4, false>(ReconArgs);
-template __global__ void k_wg<false, 2, false, true>(ReconArgs);
-template __global__ void k_wg<false, 3, false, true>(ReconArgs);
-template __global__ void k_wg<false, 3, true, true>(ReconArgs);
-template __global__ void k_rows<false>(ReconArgs);
-template __global__ void k_rows<true>(ReconArgs);
 
 // ---------------------------------------------------------------------------
 // k_wgpp: k_wg with TWO row-unit waves per MB row, ping-pong: wave w
@@ -2472,10 +1590,9 @@ __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(
     __shared__ McScratch M[NMC];
     __shared__ MbRing R;
     const int S = a.S;
-    const int pair = blockIdx.x / S, s = blockIdx.x - pair * S;
-    const uint32_t kr = a.order[pair];
-    const int k = (int)(kr >> 16), r = (int)(kr & 0xFFFF);
-    const int p = k * S + s;
+    // blockIdx = r * S + s: the S pictures' row r are dispatched together,
+    // rows in order, so a row's workgroup only waits on earlier ones
+    const int r = blockIdx.x / S, p = blockIdx.x - r * S;
     if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
     if (threadIdx.x == 0) { R.consumed = 0; L.hdone = 0; L.copied = 0; L.pdone = 0; }
     for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2)) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
@@ -2533,9 +1650,7 @@ __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(
         if (more) mc_issue(a, pd, r * a.w + c + NMC, v0, lane, ld);
     }
 }
-template __global__ void k_wgpp<2, false, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true>(ReconArgs);
-template __global__ void k_wgpp<2, true, true>(ReconArgs);
 template __global__ void k_wgpp<3, true, true>(ReconArgs);
 
 

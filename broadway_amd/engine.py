@@ -3,7 +3,8 @@
 ``Capture`` runs the product host parser over a whole stream and keeps each
 picture's MB-record batch (include/h264mi_records.h).  ``Engine`` owns the
 HBM frame slots of S streams and reconstructs one picture of each stream per
-launch sequence (k_inter + one k_wave per MB anti-diagonal).
+launch pair (k_prep: deblocking records + residuals; k_wgpp: MC, intra and the
+deblocking row chain).
 """
 from __future__ import annotations
 
@@ -97,22 +98,6 @@ class Engine:
     def decode_device(self, npics: int, d_recs: int, d_coef: int, d_pics: int) -> None:
         if self._L.h264mi_engine_decode_device(self._h, npics, d_recs, d_coef, d_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device failed")
-
-    def set_groups(self, ngroups: int) -> None:
-        """Split decode_device batches into `ngroups` picture groups on separate
-        HIP streams (k_mb of one group overlaps the others' k_rows)."""
-        if self._L.h264mi_engine_set_groups(self._h, int(ngroups)) != 0:
-            raise RuntimeError("h264mi_engine_set_groups failed")
-
-    def set_pipeline(self, depth: int) -> None:
-        if self._L.h264mi_engine_set_pipeline(self._h, int(depth)) != 0:
-            raise RuntimeError("h264mi_engine_set_pipeline failed")
-
-    def decode_pipelined(self, nstreams: int, depth: int, d_recs: int, d_coef: int, d_pics: int,
-                         base_pic: int, lag_rows: int) -> None:
-        if self._L.h264mi_engine_decode_pipelined(self._h, nstreams, depth, d_recs, d_coef, d_pics,
-                                                  int(base_pic), int(lag_rows)) != 0:
-            raise RuntimeError("h264mi_engine_decode_pipelined failed")
 
     def read(self, stream: int, slot: int) -> np.ndarray:
         out = np.empty(self.frame_bytes, dtype=np.uint8)

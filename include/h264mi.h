@@ -157,46 +157,25 @@ int  h264mi_engine_sync(h264mi_engine *e);
  * range errors (reference transform.c:181) or a bounded wait that expired;
  * flags accumulate over every launch and are collected by h264mi_engine_sync */
 uint32_t h264mi_engine_errors(h264mi_engine *e);
-/* average duration (us) of the last batch's kernels: [0] k_mb, [1] k_rows */
+/* duration (us) of the last batch's k_wgpp launch: us2[1] (us2[0] = 0);
+ * needs H264MI_TIMING in the environment */
 int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
-/* per-batch kernel timing with HIP events on the engine's stream:
- * record up to max_batches batches (0 disables); the report syncs and returns
- * the summed durations of k_mb and of k_rows, in microseconds */
+/* per-batch kernel timing with HIP events carried by k_wgpp's dispatch
+ * packet: record up to max_batches launches (0 disables); the report syncs
+ * and returns the summed k_wgpp durations in *wave_us (*inter_us = 0), in
+ * microseconds */
 int  h264mi_engine_set_timing(h264mi_engine *e, int max_batches);
-/* time only every stride-th launch (the event markers between launches cost
- * the stream a few us each; default 1) */
+/* time only every stride-th launch (default 1) */
 int  h264mi_engine_set_timing_stride(h264mi_engine *e, int stride);
 int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches);
-/* frame-pipelined batches: one launch reconstructs `depth` consecutive
- * pictures of each of `nstreams` streams, and a picture's motion
- * compensation starts as soon as the reference samples it reads are final
- * (per-MB dependency tracking on the GPU).  set_pipeline sizes the
- * per-picture buffers (nstreams x depth).  d_pics: nstreams*depth PicDesc,
- * picture-major (k*nstreams + s).  Frame slots form a ring: picture k of
- * the launch writes slot (base_pic + k) mod nslots of its stream and record
- * ref[] fields name ring slots, so no picture of a launch overwrites a slot
- * another picture of the launch reads (nslots >= depth + reference span).
- * lag_rows: row k+1 of the launch's picture order trails by this many MB
- * rows; it must exceed every MV's reference reach in MB rows by 2 (the
- * caller computes it from the records; <= 0 = whole pictures in sequence). */
-int  h264mi_engine_set_pipeline(h264mi_engine *e, int depth);
-/* stream groups: decode_device batches are split into `ngroups` groups of
- * pictures, each reconstructed on its own HIP stream (k_mb then k_rows), so
- * one group's motion compensation overlaps the other groups' row kernels.
- * The groups are offset once (a short delay kernel) so that, with equal
- * per-picture cost, their k_mb phases stay apart.  The caller keeps
- * d_recs / d_coef / d_pics unchanged until h264mi_engine_sync.  1 = off. */
-#define H264MI_MAX_GROUPS 8
-int  h264mi_engine_set_groups(h264mi_engine *e, int ngroups);
-int  h264mi_engine_decode_pipelined(h264mi_engine *e, int nstreams, int depth, const void *d_recs,
-                                    const int16_t *d_coef, const void *d_pics, int base_pic, int lag_rows);
-/* diagnostics: per k_rows workgroup (row r of batch picture p at index
+/* diagnostics: per k_wgpp workgroup (row r of batch picture p at index
  * r * npics + p) 16 u64: wall-clock start/end (100 MHz) and shader-clock sums
- * of its phases, then 4 u64 per MB (hand-off timestamps); enable != 0 allocates, out != NULL copies the last launch */
+ * of its phases, then 4 u64 per MB (chain stamps); enable != 0 allocates and
+ * switches to the profiling kernel, out != NULL copies the last launch */
 int  h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long long *out, size_t n);
 void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);          /* device pointer */
-/* diagnostics: name of the last batch's reconstruction kernel ("k_wgpp",
- * "k_wg", "k_mb+k_rows", ...; "" before the first batch) */
+/* diagnostics: name of the last batch's reconstruction kernel ("k_wgpp";
+ * "" before the first batch) */
 const char *h264mi_engine_kernel(h264mi_engine *e);
 size_t h264mi_engine_frame_bytes(h264mi_engine *e);
 

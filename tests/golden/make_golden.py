@@ -44,33 +44,53 @@ CASES = {
     "cfg2_720p_ionly_idc1_s2": (1, 2, dict(nframes=3, dbf_idc1_pct=100), False),
     "cfg5_2160p_s200": (4, 200, dict(nframes=4), False),
 }
-# bench.py streams: config 3, seeds 100..107, 60 frames (4 warmup + 56 timed)
-for s in range(100, 108):
+# bench.py streams: config 3, 60 frames (4 warmup + 56 timed).  configs[3]
+# (64 streams, 8 per GPU) uses seeds 100..163: rank r of bench.py --gpus N owns
+# seeds 100 + 8r .. 100 + 8r + 7 (tests/test_gpu_parity.py decodes each shard)
+for s in range(100, 164):
     CASES[f"bench_1080p_s{s}"] = (3, s, dict(nframes=60), False)
 
 
-def main():
+def one_case(item):
+    """Generate one case's stream and decode it with the reference build."""
     from broadway_amd import gen
     import oracle as O
 
+    name, (cfg, seed, ov, nr) = item
+    stream = gen.generate(cfg, seed, **ov)
+    frames = O.refdec_frames(stream, no_reorder=nr)
+    p = gen.params(cfg, seed, **ov)
+    w, h = p.w_mbs * 16, p.h_mbs * 16
+    assert frames and all(len(f) == w * h * 3 // 2 for f in frames), name
+    return name, {
+        "config": cfg, "seed": seed, "overrides": ov, "no_reorder": nr,
+        "stream_bytes": len(stream), "stream_sha256": hashlib.sha256(stream).hexdigest(),
+        "width": w, "height": h,
+        "frames": [hashlib.md5(f).hexdigest() for f in frames],
+    }
+
+
+def main():
+    """--missing: keep the committed cases, add only the absent ones."""
+    import concurrent.futures as cf
+
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json")
     out = {"generator": "broadway_amd.gen (libh264gen.so)",
            "decoder": "reference C (Decoder/src, make.py file list + DecTestBench.c), gcc -O2",
            "frame_md5": "MD5 of each output frame: full MB-aligned I420 (w*h*3/2 bytes), output order",
            "cases": {}}
-    for name, (cfg, seed, ov, nr) in CASES.items():
-        stream = gen.generate(cfg, seed, **ov)
-        frames = O.refdec_frames(stream, no_reorder=nr)
-        p = gen.params(cfg, seed, **ov)
-        w, h = p.w_mbs * 16, p.h_mbs * 16
-        assert frames and all(len(f) == w * h * 3 // 2 for f in frames), name
-        out["cases"][name] = {
-            "config": cfg, "seed": seed, "overrides": ov, "no_reorder": nr,
-            "stream_bytes": len(stream), "stream_sha256": hashlib.sha256(stream).hexdigest(),
-            "width": w, "height": h,
-            "frames": [hashlib.md5(f).hexdigest() for f in frames],
-        }
-        print(f"{name}: {len(frames)} frames {w}x{h}", flush=True)
-    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden.json"), "w") as f:
+    old = {}
+    if "--missing" in sys.argv and os.path.exists(path):
+        old = json.load(open(path))["cases"]
+    todo = [(n, c) for n, c in CASES.items() if n not in old]
+    with cf.ProcessPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        done = dict(ex.map(one_case, todo))
+    for name in CASES:
+        out["cases"][name] = old[name] if name in old else done[name]
+        if name in done:
+            print(f"{name}: {len(done[name]['frames'])} frames {done[name]['width']}x{done[name]['height']}",
+                  flush=True)
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")
 

@@ -54,3 +54,56 @@ def test_two_rank_sharding_and_max():
         flat = [s for g in gathered for s in g]
         assert len(flat) == len(set(flat)) == 16     # disjoint stream sets
         assert sorted(flat) == list(range(100, 116))  # config 4: seeds 100.. 8 per GPU
+
+
+def _bench_worker(rank, world, port, q):
+    """One rank of `bench.py --gpus 2 --dry-run` (torch.distributed.run's
+    environment): sharding, host parse, warmup + timed step loop, the
+    max-over-ranks timing and the summed verification counts, no device."""
+    import contextlib
+    import io
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import bench
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        bench.main(["--gpus", str(world), "--dry-run", "--streams", "2", "--warmup", "1", "--steps", "3",
+                    "--config", "2", "--gen", "w_mbs=6,h_mbs=4,crop_bottom=0"])
+    q.put((rank, out.getvalue()))
+
+
+@pytest.mark.timeout(180)
+def test_bench_dry_run_two_ranks():
+    import json
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=160) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[1].strip() == ""                      # only rank 0 prints
+    line = json.loads(res[0].strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 3 and line["warmup"] == 1
+    assert line["config"]["total_streams"] == 4 and line["config"]["seeds"] == "100..103"
+    assert line["dry_run"]["launches"] == 4 and line["dry_run"]["seeds"] == [100, 101]
+    assert line["value"] > 0 and line["scaling"] == "weak"
+    assert line["bitexact_check"]["frames_expected"] == 2 * 2 * 4
+
+
+def test_bench_gpus_mismatch_refused(monkeypatch):
+    """--gpus N inside a torch.distributed environment of another size fails
+    loudly instead of reporting the wrong n_gpus."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    with pytest.raises(SystemExit):
+        bench.dist_setup(8)

@@ -62,30 +62,7 @@ def test_decoder_js_api_holds_reordered_pictures():
     assert 0 < len(got) < len(c["frames"]) and got == c["frames"][:len(got)]
 
 
-# single-picture launch kernels (engine environment -> the kernel it must run):
-# the default k_prep + k_wgpp (2 ping-pong row waves, 3 MC waves), k_wgpp with
-# 2 MC waves, the one-row-wave k_wg (with and without k_prep), and the
-# two-kernel k_mb + k_rows path
-KERNEL_MODES = [
-    ({}, "k_wgpp"),
-    ({"H264MI_WG_NMC": "2"}, "k_wgpp"),
-    ({"H264MI_WG_PP": "0"}, "k_wg"),
-    ({"H264MI_WG_PP": "0", "H264MI_WG_NMC": "2"}, "k_wg"),
-    ({"H264MI_WG_PP": "0", "H264MI_PREP": "0"}, "k_wg"),
-    ({"H264MI_KERNEL": "classic"}, "k_mb+k_rows"),
-]
-
-
-@pytest.fixture(params=KERNEL_MODES, ids=lambda m: m[1] + "".join(f"-{k[6:].lower()}{v}" for k, v in m[0].items()))
-def kernel_mode(request, monkeypatch):
-    for k in ("H264MI_KERNEL", "H264MI_WG_NMC", "H264MI_WG_PP", "H264MI_PREP"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in request.param[0].items():
-        monkeypatch.setenv(k, v)
-    return request.param[1]
-
-
-def test_engine_multistream_batch_vs_oracle_replay(kernel_mode):
+def test_engine_multistream_batch_vs_oracle_replay():
     streams = [gen.generate(2, 40 + i, nframes=6, w_mbs=10, h_mbs=6, crop_bottom=0, slices=2, gop=4)
                for i in range(4)]
     caps = [Capture(s) for s in streams]
@@ -101,11 +78,11 @@ def test_engine_multistream_batch_vs_oracle_replay(kernel_mode):
             replays[s].picture(p.rec, p.coef, p.cur_slot)
         for s, p in enumerate(pics):
             assert eng.read(s, p.cur_slot).tobytes() == replays[s].frame(p.cur_slot), f"stream {s} picture {k}"
-    assert eng.kernel_name() == kernel_mode
+    assert eng.kernel_name() == "k_wgpp"
     assert eng.errors() == 0
 
 
-def test_engine_bench_streams_vs_reference(kernel_mode):
+def test_engine_bench_streams_vs_reference():
     """The bench workload (configs[3]: 8 concurrent 1080p streams, one picture
     of each per launch), 12 pictures, every frame vs the reference MD5s."""
     names = [f"bench_1080p_s{s}" for s in range(100, 108)]
@@ -122,35 +99,28 @@ def test_engine_bench_streams_vs_reference(kernel_mode):
         for s, p in enumerate(pics):
             got = hashlib.md5(eng.read(s, p.cur_slot).tobytes()).hexdigest()
             assert got == CASES[names[s]]["frames"][k], f"stream {s} picture {k}"
-    assert eng.kernel_name() == kernel_mode
+    assert eng.kernel_name() == "k_wgpp"
     assert eng.errors() == 0
 
 
-@pytest.mark.parametrize("depth", [2, 3])
-def test_engine_pipelined_vs_reference(depth):
-    """Frame-pipelined launches (k_wg<PIPE>: `depth` consecutive pictures of
-    each of the 8 bench streams per launch, per-row progress waits on the
-    reference samples) on 12 pictures, every frame vs the reference MD5s."""
+@pytest.mark.parametrize("rank", range(8))
+def test_configs3_shard_vs_reference(rank):
+    """configs[3]: 64 streams, 8 per GPU.  Rank r's shard (seeds 100+8r ..
+    100+8r+7, bench.shard_seeds) through bench.py's own device-resident path
+    (records in HBM, one k_prep + k_wgpp launch pair per step) and its
+    verification pass: all 60 pictures of all 8 streams vs the reference
+    decoder's MD5s."""
     import bench
-    names = [f"bench_1080p_s{s}" for s in range(100, 108)]
-    n = 12
-    _, caps = bench.prepare(3, [CASES[x]["seed"] for x in names], n)
+    seeds = bench.shard_seeds(rank, 8)
+    n = 60
+    _, caps = bench.prepare(3, seeds, n)
     L = _lib.mi()
-    S, w, h = len(caps), caps[0].w_mbs, caps[0].h_mbs
-    ring = depth + 17
-    d_recs, d_coef, d_pics, pic_rec_bytes, nslots, _ = bench.upload(L, caps, n, depth, ring)
+    d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, n)
     try:
-        eng = Engine(w, h, S, nslots)
-        eng.set_pipeline(depth)
-        for k in range(n // depth):
-            lag = bench.row_reach(caps, k * depth, (k + 1) * depth) + 2
-            eng.decode_pipelined(S, depth, d_recs + k * depth * pic_rec_bytes, d_coef, d_pics + k * depth * S * 32,
-                                 k * depth, lag)
-        eng.sync()
-        for s in range(S):
-            for k in range(n):
-                got = hashlib.md5(eng.read(s, k % ring).tobytes()).hexdigest()
-                assert got == CASES[names[s]]["frames"][k], f"stream {s} picture {k}"
+        eng = Engine(caps[0].w_mbs, caps[0].h_mbs, 8, nslots)
+        step = lambda k: eng.decode_device(8, d_recs + k * step_rec_bytes, d_coef, d_pics + k * 8 * 32)
+        ok, checked, missing = bench.verify_all(eng, step, caps, seeds, 3, {}, n)
+        assert (ok, checked, missing) == (True, 8 * n, 0)
         assert eng.errors() == 0
         eng.close()
     finally:

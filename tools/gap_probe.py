@@ -13,7 +13,7 @@ L = _lib.mi()
 S, N = 8, 24
 streams, caps = bench.prepare(3, [100 + i for i in range(S)], N)
 w, h = caps[0].w_mbs, caps[0].h_mbs
-d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, N, 1, 0)
+d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, N)
 eng = Engine(w, h, S, nslots)
 
 

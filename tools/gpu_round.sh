@@ -20,5 +20,5 @@ if [ -x tools/ubench/fetch_calib ]; then
   timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/calib -o calib -- tools/ubench/fetch_calib > $OUT/calib.log 2>&1 || { tail -20 $OUT/calib.log; exit 1; }
 fi
 # row-chain decomposition of the profiling kernel (tools/prof_chain.py)
-H264MI_KERNEL=wg timeout -k 10 200 python tools/prof_chain.py > $OUT/chain_s8.log 2>&1 || { tail -20 $OUT/chain_s8.log; exit 1; }
-PROF_S=1 H264MI_KERNEL=wg timeout -k 10 200 python tools/prof_chain.py > $OUT/chain_s1.log 2>&1 || { tail -20 $OUT/chain_s1.log; exit 1; }
+timeout -k 10 200 python tools/prof_chain.py > $OUT/chain_s8.log 2>&1 || { tail -20 $OUT/chain_s8.log; exit 1; }
+PROF_S=1 timeout -k 10 200 python tools/prof_chain.py > $OUT/chain_s1.log 2>&1 || { tail -20 $OUT/chain_s1.log; exit 1; }

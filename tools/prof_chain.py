@@ -30,7 +30,7 @@ L = _lib.mi()
 S = int(os.environ.get("PROF_S", "8"))
 streams, caps = bench.prepare(3, [100 + i for i in range(S)], 6)
 w, h = caps[0].w_mbs, caps[0].h_mbs
-d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6, 1, 0)
+d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6)
 eng = Engine(w, h, S, nslots)
 print("kernel", eng.kernel_name())
 L.h264mi_engine_profile(eng._h, 1, None, 0)
