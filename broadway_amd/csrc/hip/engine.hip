@@ -35,11 +35,13 @@ struct h264mi_engine {
     const char *last_kernel;      // name of the last batch's reconstruction kernel (diagnostics)
     uint8_t *d_dbrec;         // 64 B per batch MB (x2: k_prep double buffer)
     int16_t *d_res;           // 384 x int16 per batch MB (x2)
-    // k_prep (deblocking records + residuals one batch ahead, on its own
-    // stream): buffer half prep_parity, ordered by events
+    // k_prep (deblocking records + residuals) writes buffer half prep_parity;
+    // a batch prepped by the previous launch's tail workgroups is `prepped`
     int prep_parity;
-    hipStream_t st2;
-    hipEvent_t ev_in, ev_prep, ev_wgdone[2];
+    const void *prepped_rec, *prepped_pics;
+    unsigned long long *d_rows_done;   // row workgroups finished, all launches (tail-prep trigger)
+    unsigned long long rows_launched;
+    int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
     MbRec *d_rec;
     int16_t *d_coef;
     size_t coef_cap;          // blocks
@@ -122,11 +124,7 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
               hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess &&
               hipEventCreate(&e->ev2) == hipSuccess &&
-              hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&e->ev_prep, hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&e->ev_wgdone[0], hipEventDisableTiming) == hipSuccess &&
-              hipEventCreateWithFlags(&e->ev_wgdone[1], hipEventDisableTiming) == hipSuccess;
+              hipMalloc(&e->d_rows_done, sizeof(unsigned long long)) == hipSuccess;
     ok = ok && alloc_pic_buffers(e, nstreams) == 0;
     if (!ok) {
         fprintf(stderr, "h264mi: engine allocation failed\n");
@@ -134,6 +132,11 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         return NULL;
     }
     (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * nslots * nstreams, e->st);
+    (void)hipMemsetAsync(e->d_rows_done, 0, sizeof(unsigned long long), e->st);
+    {
+        const char *pa = getenv("H264MI_PREP_AT");
+        e->prep_at_pct = pa ? atoi(pa) : 0;
+    }
     e->epoch = 0;
     (void)hipEventRecord(e->ev_staged, e->st);
     (void)hipStreamSynchronize(e->st);
@@ -144,7 +147,6 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
 {
     if (!e) return;
     if (e->st) (void)hipStreamSynchronize(e->st);
-    if (e->st2) (void)hipStreamSynchronize(e->st2);
     free_pic_buffers(e);
     (void)hipFree(e->d_rgba);
     (void)hipFree(e->d_frames); (void)hipFree(e->d_prof); (void)hipFree(e->d_rec); (void)hipFree(e->d_coef);
@@ -154,25 +156,44 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
-    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
-    if (e->ev_prep) (void)hipEventDestroy(e->ev_prep);
-    for (int i = 0; i < 2; i++)
-        if (e->ev_wgdone[i]) (void)hipEventDestroy(e->ev_wgdone[i]);
-    if (e->st2) (void)hipStreamDestroy(e->st2);
+    (void)hipFree(e->d_rows_done);
     h264mi_engine_set_timing(e, 0);
     if (e->st) (void)hipStreamDestroy(e->st);
     free(e);
 }
 
-// One reconstruction launch pair for a batch of npics pictures (one per
-// stream): k_prep (deblocking records + residuals, every MB in parallel) on
-// st2, then k_wgpp (one workgroup per (picture, MB row): MC waves + ping-pong
-// deblocking row waves) on st.  k_prep writes the buffer half the launch
-// before last read (ev_wgdone), so a device-resident batch's k_prep overlaps
-// the previous batch's k_wgpp; k_wgpp waits for its own k_prep (ev_prep).
-static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
-                        const PicDesc *d_pics, bool host_staged)
+// k_prep of a batch as its own launch (the batch was not prepped by the
+// previous launch's tail): deblocking records + residuals into buffer half hb
+static int launch_prep(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
+                       const PicDesc *d_pics, int hb)
 {
+    const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
+    PrepArgs pa;
+    pa.rec = d_rec; pa.coef = d_coef; pa.pics = d_pics;
+    pa.dbrec = e->d_dbrec + hb * mbs * 64;
+    pa.res = e->d_res + hb * mbs * 384;
+    pa.nmbs_total = npics * e->nmbs;
+    pa.w = e->w; pa.h = e->h;
+    hipLaunchKernelGGL(k_prep, dim3((pa.nmbs_total + 3) / 4), dim3(256), 0, e->st, pa);
+    HIPCHECK(hipGetLastError());
+    return 0;
+}
+
+// One reconstruction step for a batch of npics pictures (one per stream), all
+// on the engine's stream: k_prep unless the previous launch's tail already
+// prepped this batch, then k_wgpp -- one workgroup per (picture, MB row): MC
+// waves + ping-pong deblocking row waves -- plus, when the next batch is
+// known (next_rec != NULL), tail workgroups that run the next batch's k_prep
+// as this launch's rows drain.  k_prep outputs alternate between two buffer
+// halves; stream order separates writer and reader.
+static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
+                        const PicDesc *d_pics, const MbRec *next_rec, const int16_t *next_coef,
+                        const PicDesc *next_pics)
+{
+    const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
+    const int hb = e->prep_parity;
+    if (!(e->prepped_rec && e->prepped_rec == (const void *)d_rec && e->prepped_pics == (const void *)d_pics))
+        if (launch_prep(e, npics, d_rec, d_coef, d_pics, hb)) return -1;
     ReconArgs a;
     memset(&a, 0, sizeof(a));
     a.frames = e->d_frames;
@@ -183,7 +204,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.gjunk = e->d_gjunk;
     if (++e->epoch >= (1u << 20)) {           // granule tags: epoch in the high dword
         if (h264mi_engine_sync(e)) return -1;
-        HIPCHECK(hipMemsetAsync(e->d_mbx, 0, (size_t)e->pipe_cap * e->nmbs * 256, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st));
         e->epoch = 1;
     }
     a.epoch = e->epoch;
@@ -193,20 +214,20 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.w = e->w; a.h = e->h;
     a.err = e->d_err;
     a.S = npics;
-    const int pbuf = e->prep_parity;
-    e->prep_parity ^= 1;
-    const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
-    a.dbrec = e->d_dbrec + pbuf * mbs * 64;
-    a.res = e->d_res + pbuf * mbs * 384;
-    if (host_staged) {      // the upload is on st
-        HIPCHECK(hipEventRecord(e->ev_in, e->st));
-        HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_in, 0));
+    a.dbrec = e->d_dbrec + hb * mbs * 64;
+    a.res = e->d_res + hb * mbs * 384;
+    const int rows = npics * e->h;
+    if (next_rec) {
+        a.prep_wgs = 2048;
+        a.rows_done = e->d_rows_done;
+        a.prep_target = e->rows_launched + (unsigned long long)((long long)rows * e->prep_at_pct / 100);
+        a.n_rec = next_rec; a.n_coef = next_coef; a.n_pics = next_pics;
+        a.n_dbrec = e->d_dbrec + (hb ^ 1) * mbs * 64;
+        a.n_res = e->d_res + (hb ^ 1) * mbs * 384;
+        a.n_nmbs_total = npics * e->nmbs;
+    } else {
+        a.rows_done = e->d_rows_done;
     }
-    HIPCHECK(hipStreamWaitEvent(e->st2, e->ev_wgdone[pbuf], 0));
-    hipLaunchKernelGGL(k_prep, dim3((npics * e->nmbs + 3) / 4), dim3(256), 0, e->st2, a);
-    HIPCHECK(hipGetLastError());
-    HIPCHECK(hipEventRecord(e->ev_prep, e->st2));
-    HIPCHECK(hipStreamWaitEvent(e->st, e->ev_prep, 0));
     hipEvent_t t0 = e->ev0, t2 = e->ev2;
     bool rec_tev = false;
     if (e->tev && e->tev_n < e->tev_cap && e->tev_seq++ % (e->tev_stride > 0 ? e->tev_stride : 1) == 0) {
@@ -216,7 +237,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     }
     const bool rec = e->timing || rec_tev;
     e->last_kernel = "k_wgpp";
-    const dim3 grid(npics * e->h);
+    const dim3 grid(rows + a.prep_wgs);
     if (a.prof) {
         if (rec) (void)hipEventRecord(t0, e->st);
         hipLaunchKernelGGL((k_wgpp<3, true, true>), grid, dim3(320), 0, e->st, a);
@@ -228,7 +249,10 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
                               rec ? t2 : nullptr, 0, a);
     }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipEventRecord(e->ev_wgdone[pbuf], e->st));
+    e->rows_launched += rows;
+    e->prepped_rec = next_rec;
+    e->prepped_pics = next_pics;
+    e->prep_parity = hb ^ 1;                  // the half the next batch was (or will be) prepped into
     return 0;
 }
 
@@ -268,15 +292,24 @@ extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stre
     if (cbase) HIPCHECK(hipMemcpyAsync(e->d_coef, e->h_coef, cbase * 32, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipMemcpyAsync(e->d_pics, e->h_pics, sizeof(PicDesc) * npics, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipEventRecord(e->ev_staged, e->st));
-    return launch_batch(e, npics, e->d_rec, e->d_coef, e->d_pics, true);
+    return launch_batch(e, npics, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
 }
 
 extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
                                            const void *d_pics)
 {
-    if (!e || npics < 1 || npics > e->nstreams) return -1;
+    return h264mi_engine_decode_device_next(e, npics, d_recs, d_coef, d_pics, NULL, NULL, NULL);
+}
+
+extern "C" int h264mi_engine_decode_device_next(h264mi_engine *e, int npics, const void *d_recs,
+                                                const int16_t *d_coef, const void *d_pics, const void *next_recs,
+                                                const int16_t *next_coef, const void *next_pics)
+{
+    if (!e || npics < 1 || npics > e->nstreams || !d_recs || !d_pics) return -1;
+    if (next_recs && !next_pics) return -1;
     HIPCHECK(hipSetDevice(e->dev));
-    return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, false);
+    return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
+                        next_coef, (const PicDesc *)next_pics);
 }
 
 extern "C" const char *h264mi_engine_kernel(h264mi_engine *e)
@@ -289,7 +322,6 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     if (!e) return -1;
     HIPCHECK(hipSetDevice(e->dev));
     HIPCHECK(hipStreamSynchronize(e->st));
-    HIPCHECK(hipStreamSynchronize(e->st2));
     // per-picture error flags OR-accumulate over every launch since the last
     // sync (no per-launch reset): count the flagged picture slots, then clear
     HIPCHECK(hipMemcpy(e->h_err, e->d_err, sizeof(unsigned) * e->pipe_cap, hipMemcpyDeviceToHost));

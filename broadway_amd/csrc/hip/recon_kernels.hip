@@ -39,6 +39,17 @@ struct ReconArgs {
     unsigned long long *prof; // optional per-MB chain stamps (profiling k_wgpp)
     int S;                    // pictures (streams) of the batch
     unsigned long long *gjunk; // 64 KiB sink: 128 x 64 granules for lanes with nothing to store
+    // tail workgroups (blockIdx >= S * h): k_prep of the NEXT batch, started
+    // once *rows_done (row workgroups finished, all launches) >= prep_target
+    int prep_wgs;
+    unsigned long long *rows_done;
+    unsigned long long prep_target;
+    const MbRec *n_rec;
+    const int16_t *n_coef;
+    const PicDesc *n_pics;
+    uint8_t *n_dbrec;
+    int16_t *n_res;
+    int n_nmbs_total;
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -424,7 +435,7 @@ __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int
 }
 
 // ---------------------------------------------------------------------------
-// deblocking record (precomputed by k_mb, consumed by k_rows): 64 B per MB
+// deblocking record (computed by k_prep, consumed by k_wgpp): 64 B per MB
 //   [0..15]  bS nibbles, index (dir*16 + seg*4 + edge): dir 0 = vertical edges;
 //            the four edges crossed by one line are one 16-bit word
 //   [16..63] 8 bytes per (plane*3 + class), plane 0 luma / 1 chroma, class
@@ -441,17 +452,7 @@ __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int
 // the threshold-table loads are issued before the bS work.  srec is staged
 // by the caller (stage_recs_load).
 // the MB's, left and top records in LDS (srec: dwords 0..23, 24..47, 48..71)
-__device__ __forceinline__ void stage_recs_load(const ReconArgs &a, int gmb, int mbx, int mby, int lane, uint32_t &v0,
-                                                uint32_t &v1)
-{
-    const uint32_t *rq = (const uint32_t *)(a.rec + gmb);
-    const uint32_t *rl = (const uint32_t *)(a.rec + (mbx > 0 ? gmb - 1 : gmb));
-    const uint32_t *rt = (const uint32_t *)(a.rec + (mby > 0 ? gmb - a.w : gmb));
-    v0 = *(lane < 24 ? rq + lane : lane < 48 ? rl + (lane - 24) : rt + (lane - 48));
-    v1 = rt[16 + (lane & 7)];
-}
-
-__device__ void mb_dbrec(const ReconArgs &a, int lane, uint8_t *s_db, const uint32_t *srec, const Tabs &T)
+__device__ void mb_dbrec(int lane, uint8_t *s_db, const uint32_t *srec, const Tabs &T)
 {
     const MbRec *Q = (const MbRec *)srec;
     const bool fl = Q->avail & DB_LEFT, ft = Q->avail & DB_TOP;
@@ -511,31 +512,37 @@ struct McScratch {
 
 // k_prep: the per-MB work that does not depend on any reconstructed sample --
 // deblocking record (bS + thresholds) and residual (dequant + inverse
-// transforms) -- for every MB of a batch, fully parallel (four MBs per
-// workgroup, one wave each).  Runs on its own stream one batch ahead of k_wg,
-// filling the GPU beside the latency-bound row chain; k_wg's MC waves then
-// only load its outputs.  Outputs: a.dbrec (64 B per MB; byte 63 = residual
-// range error, a byte no consumer reads otherwise), a.res (384 x int16, for
-// MBs with coded blocks).
-__global__ __launch_bounds__(256) void k_prep(ReconArgs a)
+// transforms) -- for every MB of a batch, fully parallel (one wave per MB).
+// It runs one batch ahead of k_wgpp, whose MC waves then only load its
+// outputs: either as tail workgroups of the previous batch's k_wgpp launch
+// (prep_mb from k_wgpp, started once enough of that launch's rows are done)
+// or as its own launch (the first batch; host-staged batches).  Outputs:
+// dbrec (64 B per MB; byte 63 = residual range error, a byte no consumer reads
+// otherwise), res (384 x int16, for MBs with coded blocks).
+struct PrepArgs {
+    const MbRec *rec;
+    const int16_t *coef;
+    const PicDesc *pics;
+    uint8_t *dbrec;
+    int16_t *res;
+    int nmbs_total;           // MBs of the batch (npics * w * h)
+    int w, h;
+};
+
+__device__ __forceinline__ void prep_mb(const PrepArgs &a, int gidx, int lane, McScratch &Mw, int16_t *s_res,
+                                        uint8_t *s_db, const Tabs &T)
 {
-    __shared__ McScratch M[4];
-    __shared__ int16_t s_res[4][384];
-    __shared__ uint8_t s_db[4][64];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nmbs = a.w * a.h;
-    const int gidx = blockIdx.x * 4 + wv;
-    if (gidx >= a.npics * nmbs) return;            // wave-uniform; no workgroup barrier follows
     const int p = gidx / nmbs, mb = gidx - p * nmbs;
     const PicDesc &pd = a.pics[p];
     const int gmb = pd.rec_base + mb;
-    McScratch &Mw = M[wv];
-    const Tabs T = load_tabs(lane);
     {
-        uint32_t v0, v1;
-        stage_recs_load(a, gmb, mb % a.w, mb / a.w, lane, v0, v1);
-        Mw.srec[lane] = v0;
-        if (lane < 8) Mw.srec[64 + lane] = v1;
+        const int mbx = mb % a.w, mby = mb / a.w;
+        const uint32_t *rq = (const uint32_t *)(a.rec + gmb);
+        const uint32_t *rl = (const uint32_t *)(a.rec + (mbx > 0 ? gmb - 1 : gmb));
+        const uint32_t *rt = (const uint32_t *)(a.rec + (mby > 0 ? gmb - a.w : gmb));
+        Mw.srec[lane] = *(lane < 24 ? rq + lane : lane < 48 ? rl + (lane - 24) : rt + (lane - 48));
+        if (lane < 8) Mw.srec[64 + lane] = rt[16 + lane];
     }
     wave_sync();
     const MbRec &r = *(const MbRec *)Mw.srec;
@@ -551,7 +558,7 @@ __global__ __launch_bounds__(256) void k_prep(ReconArgs a)
         if (lane + 128 < ncw) cq2 = csrc[lane + 128];
         if (lane + 192 < ncw) cq3 = csrc[lane + 192];
     }
-    mb_dbrec(a, lane, s_db[wv], Mw.srec, T);
+    mb_dbrec(lane, s_db, Mw.srec, T);
     int e = 0;
     if (has_res) {
         if (lane < ncw) Mw.coef[lane] = cq0;
@@ -559,17 +566,30 @@ __global__ __launch_bounds__(256) void k_prep(ReconArgs a)
         if (lane + 128 < ncw) Mw.coef[lane + 128] = cq2;
         if (lane + 192 < ncw) Mw.coef[lane + 192] = cq3;
         wave_sync();
-        mb_residual(r, (const int16_t *)Mw.coef, s_res[wv], Mw.dc, lane, &e, T.ls);
-        const uint32_t *src = (const uint32_t *)s_res[wv];
+        mb_residual(r, (const int16_t *)Mw.coef, s_res, Mw.dc, lane, &e, T.ls);
+        const uint32_t *src = (const uint32_t *)s_res;
         uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
         dst[lane] = src[lane]; dst[64 + lane] = src[64 + lane]; dst[128 + lane] = src[128 + lane];
     }
     const int any_e = __builtin_amdgcn_ballot_w64(e != 0) != 0;
     if (lane < 16) {
-        uint32_t w = ((const uint32_t *)s_db[wv])[lane];
+        uint32_t w = ((const uint32_t *)s_db)[lane];
         if (lane == 15) w = (w & 0x00FFFFFFu) | (any_e ? 0x01000000u : 0u);
         ((uint32_t *)(a.dbrec + (size_t)gmb * 64))[lane] = w;
     }
+    wave_sync();
+}
+
+__global__ __launch_bounds__(256) void k_prep(PrepArgs a)
+{
+    __shared__ McScratch M[4];
+    __shared__ int16_t s_res[4][384];
+    __shared__ uint8_t s_db[4][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int gidx = blockIdx.x * 4 + wv;
+    if (gidx >= a.nmbs_total) return;            // wave-uniform; no workgroup barrier follows
+    const Tabs T = load_tabs(lane);
+    prep_mb(a, gidx, lane, M[wv], s_res[wv], s_db[wv], T);
 }
 
 // ---------------------------------------------------------------------------
@@ -1583,6 +1603,32 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     return rtype;
 }
 
+// k_wgpp tail workgroup: waves 0..NMC-1 run the next batch's k_prep over a
+// grid-stride share of its MBs, in the LDS of the MC scratch and ring (unused
+// by a tail workgroup), once enough row workgroups of this and earlier
+// launches have finished (their CUs are idle then; k_prep's memory traffic
+// beside live row chains would lengthen the chains' L2 hand-offs).  Tail
+// workgroups come after every row workgroup in dispatch order, so no row
+// ever waits for them; the poll is bounded.
+template <int NMC>
+__device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRing &R)
+{
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (wid >= NMC) return;
+    unsigned spins = 0;
+    while (__hip_atomic_load(a.rows_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.prep_target) {
+        __builtin_amdgcn_s_sleep(64);
+        if (++spins > (1u << 16)) break;            // bounded: ~0.5 s
+    }
+    PrepArgs pa;
+    pa.rec = a.n_rec; pa.coef = a.n_coef; pa.pics = a.n_pics; pa.dbrec = a.n_dbrec; pa.res = a.n_res;
+    pa.nmbs_total = a.n_nmbs_total; pa.w = a.w; pa.h = a.h;
+    const Tabs T = load_tabs(lane);
+    const int t = blockIdx.x - a.S * a.h;
+    for (int g = t * NMC + wid; g < pa.nmbs_total; g += a.prep_wgs * NMC)
+        prep_mb(pa, g, lane, M[wid], R.res[wid], R.db[wid], T);
+}
+
 template <int NMC, bool PROF, bool PREP>
 __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(NMC == 3 ? 4 : 3))) void k_wgpp(ReconArgs a)
 {
@@ -1592,6 +1638,10 @@ __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(
     const int S = a.S;
     // blockIdx = r * S + s: the S pictures' row r are dispatched together,
     // rows in order, so a row's workgroup only waits on earlier ones
+    if (blockIdx.x >= S * a.h) {        // tail workgroup: the next batch's k_prep
+        prep_tail<NMC>(a, M, R);
+        return;
+    }
     const int r = blockIdx.x / S, p = blockIdx.x - r * S;
     if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
     if (threadIdx.x == 0) { R.consumed = 0; L.hdone = 0; L.copied = 0; L.pdone = 0; }
@@ -1601,6 +1651,9 @@ __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(
     if (wid < 2) {
         __builtin_amdgcn_s_setprio(3);
         row_pp<PROF>(a, p, r, L, wid, lane, &R);
+        // row finished: progress for the tail workgroups' start
+        if (wid == 0 && lane == 0 && a.rows_done)
+            __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");

@@ -22,6 +22,27 @@
 
 H264Backend h264mi_hip_backend_create(int device);
 
+/* ---- application hooks (reference inc/H264SwDecApi.h:160-173) ----------
+ * The library allocates and frees its instances through H264SwDecMalloc /
+ * H264SwDecFree and fills them with H264SwDecMemset, as H264SwDecApi.c:147,
+ * :301 does; H264SwDecTrace receives the API trace strings when built with
+ * -DH264DEC_TRACE (H264SwDecApi.c:66-72).  These are the reference's default
+ * definitions (H264SwDecApi.c:78-96): an application that defines its own
+ * (DecTestBench.c:678-760, TestBenchMultipleInstance.c:396-446) overrides them
+ * by ordinary ELF symbol interposition -- the library calls them through its
+ * PLT. */
+void H264SwDecTrace(char *string) { (void)string; }
+void *H264SwDecMalloc(u32 size) { return malloc(size); }
+void H264SwDecFree(void *ptr) { free(ptr); }
+void H264SwDecMemcpy(void *dest, void *src, u32 count) { memcpy(dest, src, count); }
+void H264SwDecMemset(void *ptr, i32 value, u32 count) { memset(ptr, value, count); }
+
+#ifdef H264DEC_TRACE
+#define DEC_API_TRC(str) H264SwDecTrace((char *)(str))
+#else
+#define DEC_API_TRC(str) ((void)0)
+#endif
+
 enum { ST_UNINIT = 0, ST_INIT = 1, ST_NEW_HEADERS = 2 };
 
 typedef struct DecContainer {
@@ -38,24 +59,34 @@ static int backend_device(void)
 
 H264SwDecRet H264SwDecInit(H264SwDecInst *decInst, u32 noOutputReordering)
 {
-    if (decInst == NULL) return H264SWDEC_PARAM_ERR;
+    DEC_API_TRC("H264SwDecInit#");
+    if (decInst == NULL) {
+        DEC_API_TRC("H264SwDecInit# ERROR: decInst == NULL");
+        return H264SWDEC_PARAM_ERR;
+    }
     *decInst = NULL;
-    DecContainer *c = (DecContainer *)calloc(1, sizeof(DecContainer));
-    if (!c) return H264SWDEC_MEMFAIL;
+    DecContainer *c = (DecContainer *)H264SwDecMalloc((u32)sizeof(DecContainer));
+    if (!c) {
+        DEC_API_TRC("H264SwDecInit# ERROR: Memory allocation failed");
+        return H264SWDEC_MEMFAIL;
+    }
+    H264SwDecMemset(c, 0, (u32)sizeof(DecContainer));
     H264Backend be = h264mi_hip_backend_create(backend_device());
-    if (!be.ctx) { free(c); return H264SWDEC_MEMFAIL; }
+    if (!be.ctx) { H264SwDecFree(c); return H264SWDEC_MEMFAIL; }
     if (h264dec_init(&c->dec, (int)noOutputReordering, be)) {
         be.destroy(be.ctx);
-        free(c);
+        H264SwDecFree(c);
         return H264SWDEC_INITFAIL;
     }
     c->stat = ST_INIT;
     *decInst = c;
+    DEC_API_TRC("H264SwDecInit# OK");
     return H264SWDEC_OK;
 }
 
 H264SwDecRet H264SwDecGetInfo(H264SwDecInst decInst, H264SwDecInfo *pDecInfo)
 {
+    DEC_API_TRC("H264SwDecGetInfo#");
     if (decInst == NULL || pDecInfo == NULL) return H264SWDEC_PARAM_ERR;
     DecContainer *c = (DecContainer *)decInst;
     const Sps *s = h264dec_active_sps(&c->dec);
@@ -95,13 +126,15 @@ H264SwDecRet H264SwDecGetInfo(H264SwDecInst decInst, H264SwDecInfo *pDecInfo)
 void H264SwDecRelease(H264SwDecInst decInst)
 {
     if (!decInst) return;
+    DEC_API_TRC("H264SwDecRelease#");
     DecContainer *c = (DecContainer *)decInst;
     h264dec_release(&c->dec);
-    free(c);
+    H264SwDecFree(c);
 }
 
 H264SwDecRet H264SwDecDecode(H264SwDecInst decInst, H264SwDecInput *pInput, H264SwDecOutput *pOutput)
 {
+    DEC_API_TRC("H264SwDecDecode#");
     if (pInput == NULL || pOutput == NULL) return H264SWDEC_PARAM_ERR;
     if (pInput->pStream == NULL || pInput->dataLen == 0) return H264SWDEC_PARAM_ERR;
     DecContainer *c = (DecContainer *)decInst;
@@ -164,6 +197,7 @@ H264SwDecApiVersion H264SwDecGetAPIVersion(void)
 
 H264SwDecRet H264SwDecNextPicture(H264SwDecInst decInst, H264SwDecPicture *pOutput, u32 flushBuffer)
 {
+    DEC_API_TRC("H264SwDecNextPicture#");
     if (decInst == NULL || pOutput == NULL) return H264SWDEC_PARAM_ERR;
     DecContainer *c = (DecContainer *)decInst;
     if (flushBuffer) h264dec_flush(&c->dec);

@@ -99,6 +99,14 @@ class Engine:
         if self._L.h264mi_engine_decode_device(self._h, npics, d_recs, d_coef, d_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device failed")
 
+    def decode_device_next(self, npics: int, d_recs: int, d_coef: int, d_pics: int,
+                           n_recs: int, n_coef: int, n_pics: int) -> None:
+        """decode_device, naming the next batch: its k_prep runs in this
+        launch's tail."""
+        if self._L.h264mi_engine_decode_device_next(self._h, npics, d_recs, d_coef, d_pics,
+                                                    n_recs, n_coef, n_pics) != 0:
+            raise RuntimeError("h264mi_engine_decode_device_next failed")
+
     def read(self, stream: int, slot: int) -> np.ndarray:
         out = np.empty(self.frame_bytes, dtype=np.uint8)
         if self._L.h264mi_engine_read(self._h, stream, slot, out.ctypes.data) != 0:

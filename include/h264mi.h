@@ -100,7 +100,19 @@ H264SwDecRet H264SwDecNextPicture(H264SwDecInst decInst, H264SwDecPicture *pOutp
                                   u32 endOfStream);                              /* :524 */
 H264SwDecRet H264SwDecGetInfo(H264SwDecInst decInst, H264SwDecInfo *pDecInfo);  /* :204 */
 void H264SwDecRelease(H264SwDecInst decInst);                                    /* :259 */
-H264SwDecApiVersion H264SwDecGetAPIVersion(void);                                /* :487 */
+H264SwDecApiVersion H264SwDecGetAPIVersion(void);
+
+/* Application hooks (reference inc/H264SwDecApi.h:160-173).  The library
+ * allocates / frees each instance through H264SwDecMalloc / H264SwDecFree
+ * (H264SwDecApi.c:147, :301) and calls H264SwDecTrace with the API trace when
+ * built with -DH264DEC_TRACE.  libh264mi.so carries the reference's default
+ * definitions (malloc / free / memcpy / memset, H264SwDecApi.c:78-96); an
+ * application defining its own (DecTestBench.c:678-760) overrides them. */
+void  H264SwDecTrace(char *string);
+void *H264SwDecMalloc(u32 size);
+void  H264SwDecFree(void *ptr);
+void  H264SwDecMemcpy(void *dest, void *src, u32 count);
+void  H264SwDecMemset(void *ptr, i32 value, u32 count);                                /* :487 */
 /* NextPicture, the picture converted to RGBA on the GPU: what Decoder.js
  * delivers with `rgb: true` (templates/DecoderPost.js:82-97, the asm.js
  * converter :322-560, per pixel yuv2rgbcalc :514-560).  rgba: picWidth *
@@ -142,6 +154,13 @@ int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const i
  * to d_coef, d_pics = npics PicDesc. */
 int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
                                 const void *d_pics);
+/* Same, with the NEXT batch named (device pointers as above; it must be the
+ * batch of the following decode_device* call): this launch's tail
+ * workgroups compute the next batch's deblocking records and residuals as its
+ * own MB rows drain, so that batch needs no k_prep launch of its own. */
+int h264mi_engine_decode_device_next(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
+                                     const void *d_pics, const void *next_recs, const int16_t *next_coef,
+                                     const void *next_pics);
 
 int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */
 /* D2H of a slot as RGBA (w*16 * h*16 * 4 bytes), converted on the GPU

@@ -118,7 +118,12 @@ def test_configs3_shard_vs_reference(rank):
     d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, n)
     try:
         eng = Engine(caps[0].w_mbs, caps[0].h_mbs, 8, nslots)
-        step = lambda k: eng.decode_device(8, d_recs + k * step_rec_bytes, d_coef, d_pics + k * 8 * 32)
+        def step(k):   # bench.py's step: the next step's k_prep in this launch's tail
+            if k + 1 < n:
+                eng.decode_device_next(8, d_recs + k * step_rec_bytes, d_coef, d_pics + k * 8 * 32,
+                                       d_recs + (k + 1) * step_rec_bytes, d_coef, d_pics + (k + 1) * 8 * 32)
+            else:
+                eng.decode_device(8, d_recs + k * step_rec_bytes, d_coef, d_pics + k * 8 * 32)
         ok, checked, missing = bench.verify_all(eng, step, caps, seeds, 3, {}, n)
         assert (ok, checked, missing) == (True, 8 * n, 0)
         assert eng.errors() == 0
