@@ -51,8 +51,11 @@ def main(tag):
         kernels[k] = {"launches": n, "FETCH_SIZE_KiB": round(f_kib, 1), "WRITE_SIZE_KiB": round(w_kib, 1),
                       "read_bytes_corrected": int(2 * f_kib * 1024), "write_bytes": int(w_kib * 1024),
                       "hbm_bytes": int(hbm)}
-        step += hbm
-    out = {"tag": tag, "kernels": kernels,
+        step += hbm * n
+    # a step is one launch of the main kernel; the standalone k_prep launch
+    # (the pipeline's first step) is spread over them
+    step /= kernels[step_kernels[0]]["launches"]
+    out = {"tag": tag, "kernels": kernels, "hbm_bytes_per_step": int(step),
            "note": "FETCH_SIZE doubled per the gfx950 correction (calibrated for 16-B/lane streaming reads)"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
