@@ -72,7 +72,8 @@ class GenParams(C.Structure):
         "im_i4", "im_i16", "im_pcm", "i4_rem_pct", "qp_min", "qp_max", "qp_delta",
         "dbf_idc1_pct", "dbf_idc2_pct", "dbf_off", "num_ref_frames", "cip", "chroma_qp_offset",
         "poc_type", "coef_pct", "level_tail_pct", "mv_jitter", "offpic_pct",
-        "log2_max_frame_num", "poc_swap")] + [("seed", C.c_uint64)]
+        "log2_max_frame_num", "poc_swap",
+        "err_range_pct", "drop_slice_pct", "trunc_slice_pct", "drop_pic_pct", "gaps_allowed")] + [("seed", C.c_uint64)]
 
 
 HEADERS_CB = C.CFUNCTYPE(None, C.c_void_p)

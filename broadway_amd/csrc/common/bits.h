@@ -109,9 +109,16 @@ static inline uint32_t br_te(BitReader *br, uint32_t cmax)
     return !br_u1(br);
 }
 
+/* more_rbsp_data(): the reference's test (h264bsdMoreRbspData,
+ * h264bsd_util.c): data remain unless at most 8 bits are left and they are
+ * exactly the rbsp_stop_one_bit pattern 1 0..0 -- which is what decides
+ * where a damaged (truncated) slice stops */
 static inline int br_more_rbsp_data(const BitReader *br)
 {
-    return br->pos < br->end_bits;
+    if (br->pos >= br->size * 8) return br->pos > br->size * 8;   /* past the end: reference reads on */
+    const size_t bits = br->size * 8 - br->pos;
+    if (bits > 8) return 1;
+    return br_peek(br, (int)bits) != (1u << (bits - 1));
 }
 
 static inline int br_byte_aligned(const BitReader *br) { return (br->pos & 7) == 0; }

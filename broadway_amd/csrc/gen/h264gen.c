@@ -113,6 +113,10 @@ typedef struct Gen {
     int nref;            /* reference frames available */
     int gmx, gmy;        /* global motion, quarter-pel */
     int poc_lsb;
+    Rng erng;            /* damage decisions (err_* / drop_* knobs) */
+    int cur_mb;          /* MB being generated */
+    int range_mb;        /* MB of the current slice given an out-of-range residual, -1: none */
+    int drop_pic;        /* current picture's NALs are not emitted */
 } Gen;
 
 typedef struct SliceCfg {
@@ -248,7 +252,7 @@ static void write_sps(Gen *g)
     bw_ue(&bw, (uint32_t)p->poc_type);
     if (p->poc_type == 0) bw_ue(&bw, 4);   /* log2_max_pic_order_cnt_lsb_minus4 -> 256 */
     bw_ue(&bw, (uint32_t)p->num_ref_frames);
-    bw_put(&bw, 0, 1);             /* gaps_in_frame_num_value_allowed_flag */
+    bw_put(&bw, (uint32_t)(p->gaps_allowed != 0), 1);   /* gaps_in_frame_num_value_allowed_flag */
     bw_ue(&bw, (uint32_t)(p->w_mbs - 1));
     bw_ue(&bw, (uint32_t)(p->h_mbs - 1));
     bw_put(&bw, 1, 1);             /* frame_mbs_only_flag */
@@ -424,6 +428,15 @@ static void make_coefs(Gen *g, int is_i16, int cbp, int qp, MbCoefs *c)
             for (int b = 0; b < 4; b++)
                 if (pct(&g->rng, 60)) rand_block(g, c->cac[comp][b], 1, 16);
     while (!mb_residual_ok(is_i16, qp, qpc, c)) scale_down(c);
+    if (g->cur_mb == g->range_mb) {
+        /* one level large enough that the reference's ProcessBlock range
+         * check fails (h264bsd_transform.c:181-185, 196-197): the slice is
+         * then corrupted and concealed (slice_data.c:302-358, conceal.c) */
+        int16_t *lv = is_i16 ? c->ldc : NULL;
+        for (int b = 0; !lv && b < 16; b++) if (cbp & (1 << (b >> 2))) lv = c->luma[b];
+        if (!lv && (cbp >> 4)) lv = c->cdc[0];
+        if (lv) lv[0] = 2000;
+    }
 }
 
 static int pick_cbp(Gen *g)
@@ -621,11 +634,13 @@ static void gen_slice(Gen *g, int idr, int first, int last, const SliceCfg *sc)
 
     int qp = sc->qp;
     int skip_run = 0;
+    g->range_mb = (p->err_range_pct && pct(&g->erng, p->err_range_pct)) ? rnd_range(&g->erng, first, last) : -1;
     int pm_tot = p->pm_skip + p->pm_16x16 + p->pm_16x8 + p->pm_8x16 + p->pm_8x8 + p->pm_intra;
     for (int cur = first; cur <= last; cur++) {
         MbInfo *m = &g->pc.mb[cur];
         memset(m, 0, sizeof(*m));
         m->slice = sc->tag;
+        g->cur_mb = cur;
         int base_mv[2] = {g->gmx + rnd_range(&g->rng, -p->mv_jitter, p->mv_jitter),
                           g->gmy + rnd_range(&g->rng, -p->mv_jitter, p->mv_jitter)};
         if (sc->is_p) {
@@ -657,7 +672,11 @@ static void gen_slice(Gen *g, int idr, int first, int last, const SliceCfg *sc)
     }
     if (skip_run) bw_ue(&bw, (uint32_t)skip_run);
     bw_trailing(&bw);
-    emit_nal(&g->out, idr ? 3 : 2, idr ? 5 : 1, &bw);
+    int emit = !g->drop_pic;
+    if (emit && p->drop_slice_pct && pct(&g->erng, p->drop_slice_pct)) emit = 0;
+    if (emit && p->trunc_slice_pct && pct(&g->erng, p->trunc_slice_pct) && bw.nbytes > 4)
+        bw.nbytes = (size_t)rnd_range(&g->erng, 2, (int)bw.nbytes - 1);
+    if (emit) emit_nal(&g->out, idr ? 3 : 2, idr ? 5 : 1, &bw);
     bw_free(&bw);
 }
 
@@ -666,6 +685,7 @@ static void gen_picture(Gen *g, int idx)
     const GenParams *p = &g->p;
     int idr = (idx % p->gop) == 0;
     int nmb = p->w_mbs * p->h_mbs;
+    g->drop_pic = !idr && p->drop_pic_pct && pct(&g->erng, p->drop_pic_pct);
     if (idr) {
         write_sps(g);
         write_pps(g);
@@ -722,6 +742,8 @@ int h264gen_generate(const GenParams *p, uint8_t **out, size_t *out_len)
     g.p = *p;
     if (g.p.log2_max_frame_num < 4) g.p.log2_max_frame_num = 4;
     g.rng.s = p->seed * 0x2545F4914F6CDD1Dull + 0x1234567ull;
+    g.erng.s = p->seed * 0x9E3779B97F4A7C15ull + 0xE770Cull;
+    g.range_mb = -1;
     g.pc.w = p->w_mbs; g.pc.h = p->h_mbs; g.pc.cip = p->cip;
     g.pc.mb = (MbInfo *)calloc((size_t)p->w_mbs * p->h_mbs, sizeof(MbInfo));
     if (!g.pc.mb) return -1;

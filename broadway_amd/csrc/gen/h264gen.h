@@ -39,6 +39,13 @@ typedef struct GenParams {
     int offpic_pct;                /* partitions forced to reference off-picture */
     int log2_max_frame_num;        /* 4..16 */
     int poc_swap;                  /* POC type 0: swap display order of picture pairs (1,2),(3,4).. of a GOP */
+    /* damaged-stream knobs (error path / concealment); all 0
+     * leaves the stream byte-identical.  Decisions come from a second RNG. */
+    int err_range_pct;             /* per slice: one MB gets a residual outside [-512,511] */
+    int drop_slice_pct;            /* per slice: NAL not emitted */
+    int trunc_slice_pct;           /* per slice: NAL payload cut at a random byte */
+    int drop_pic_pct;              /* per non-IDR picture: none of its NALs emitted */
+    int gaps_allowed;              /* SPS gaps_in_frame_num_value_allowed_flag */
     uint64_t seed;
 } GenParams;
 

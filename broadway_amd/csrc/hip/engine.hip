@@ -499,16 +499,28 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
     return h264mi_engine_decode(c->e, 1, &stream, &cur_slot, recs, coefs, nc);
 }
 
+// the per-picture device error flags (ReconArgs::err: residual range, expired
+// bounded waits) gathered by the read's sync reach the caller as return 1
+static int hb_flagged(h264mi_engine *e)
+{
+    if (h264mi_engine_sync(e)) return -1;
+    const uint32_t n = h264mi_engine_errors(e);
+    if (n) fprintf(stderr, "h264mi: device reported %u flagged picture(s)\n", n);
+    return n ? 1 : 0;
+}
+
 static int hb_read(void *vctx, int slot, uint8_t *dst)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
-    return h264mi_engine_read(c->e, 0, slot, dst);
+    if (h264mi_engine_read(c->e, 0, slot, dst)) return -1;
+    return hb_flagged(c->e);
 }
 
 static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
-    return h264mi_engine_read_rgba(c->e, 0, slot, dst);
+    if (h264mi_engine_read_rgba(c->e, 0, slot, dst)) return -1;
+    return hb_flagged(c->e);
 }
 
 static void *hb_host_alloc(void *vctx, size_t bytes)

@@ -427,7 +427,7 @@ __device__ __forceinline__ int i4_pred(const uint8_t *T /* tile at block (0,0) i
 
 __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int bq, bool mb_edge)
 {
-    if (p.type >= MBT_I4x4 || q.type >= MBT_I4x4) return mb_edge ? 4 : 3;
+    if ((p.type >= MBT_I4x4) | (q.type >= MBT_I4x4) | (((p.dbf | q.dbf) & DBF_INTRA) != 0)) return mb_edge ? 4 : 3;
     if (((p.cbits >> bp) & 1) | ((q.cbits >> bq) & 1)) return 2;
     if (p.ref[bp >> 2] != q.ref[bq >> 2]) return 1;
     if (abs(p.mv[bp][0] - q.mv[bq][0]) >= 4 || abs(p.mv[bp][1] - q.mv[bq][1]) >= 4) return 1;

@@ -222,8 +222,11 @@ static int check_au_boundary(H264Dec *d, const NalHdr *nal, const BitReader *br,
         (d->active_sps >= 0 && d->active_sps < MAX_SPS && pps->sps_id != d->active_sps && nal->type != NAL_IDR))
         return DEC_FAIL(DEC_PARAM_SET_ERROR);
     const Sps *sps = &d->sps[pps->sps_id];
-    if (d->prev_nal.ref_idc != nal->ref_idc && (d->prev_nal.ref_idc == 0 || nal->ref_idc == 0)) *boundary = 1;
-    if ((d->prev_nal.type == NAL_IDR) != (nal->type == NAL_IDR)) *boundary = 1;
+    if (d->aub_prev_nal.ref_idc != nal->ref_idc && (d->aub_prev_nal.ref_idc == 0 || nal->ref_idc == 0)) *boundary = 1;
+    if ((d->aub_prev_nal.type == NAL_IDR) != (nal->type == NAL_IDR)) *boundary = 1;
+    /* each field is checked as the reference's h264bsdCheck* re-parse
+     * reads it: state updated before a failing read stays updated, and the
+     * previous NAL is only replaced when every read succeeded */
     BitReader b = *br;
     br_ue(&b); br_ue(&b); br_ue(&b);
     int fn = (int)br_u(&b, sps->log2_max_frame_num);
@@ -231,23 +234,27 @@ static int check_au_boundary(H264Dec *d, const NalHdr *nal, const BitReader *br,
     if (d->aub_prev_frame_num != fn) { d->aub_prev_frame_num = fn; *boundary = 1; }
     if (nal->type == NAL_IDR) {
         int id = (int)br_ue(&b);
-        if (d->prev_nal.type == NAL_IDR && d->aub_prev_idr_id != id) *boundary = 1;
+        if (b.err) return DEC_FAIL(DEC_ERROR);
+        if (d->aub_prev_nal.type == NAL_IDR && d->aub_prev_idr_id != id) *boundary = 1;
         d->aub_prev_idr_id = id;
     }
     if (sps->poc_type == 0) {
         int lsb = (int)br_u(&b, sps->log2_max_poc_lsb);
+        if (b.err) return DEC_FAIL(DEC_ERROR);
         if (d->aub_prev_poc_lsb != lsb) { d->aub_prev_poc_lsb = lsb; *boundary = 1; }
         if (pps->bottom_field_poc_present) {
             int db = br_se(&b);
+            if (b.err) return DEC_FAIL(DEC_ERROR);
             if (d->aub_prev_dpoc_bottom != db) { d->aub_prev_dpoc_bottom = db; *boundary = 1; }
         }
     } else if (sps->poc_type == 1 && !sps->delta_pic_order_always_zero) {
         int d0 = br_se(&b), d1 = pps->bottom_field_poc_present ? br_se(&b) : 0;
+        if (b.err) return DEC_FAIL(DEC_ERROR);
         if (d->aub_prev_dpoc[0] != d0) { d->aub_prev_dpoc[0] = d0; *boundary = 1; }
-        if (d->aub_prev_dpoc[1] != d1) { d->aub_prev_dpoc[1] = d1; *boundary = 1; }
+        if (pps->bottom_field_poc_present && d->aub_prev_dpoc[1] != d1) { d->aub_prev_dpoc[1] = d1; *boundary = 1; }
     }
-    d->prev_nal = *nal;          /* storage.c:774 (nuPrev aliases prevNalUnit) */
-    return b.err ? DEC_FAIL(DEC_ERROR) : 0;
+    d->aub_prev_nal = *nal;      /* aub->nuPrev (storage.c:774); prevNalUnit is set per decoded slice header */
+    return 0;
 }
 
 /* ---- parameter-set activation (reference storage.c:298-420) ----------- */
@@ -319,35 +326,6 @@ static void store_pps(H264Dec *d, const Pps *p)
     d->pps[id] = *p;
 }
 
-/* ---- error concealment of missing MBs (simplified) ------ */
-static int conceal_picture(H264Dec *d, int is_p, const int *ref_slot)
-{
-    PicBuild *pb = &d->pb;
-    int n = 0;
-    for (int i = 0; i < pb->nmbs; i++) {
-        if (pb->pc.mb[i].slice != SLICE_NONE) continue;
-        MbRec *r = &pb->rec[i];
-        memset(r, 0, sizeof(*r));
-        memset(&pb->pc.mb[i], 0, sizeof(MbInfo));
-        pb->pc.mb[i].slice = 0xFFFE;
-        if (is_p && ref_slot && ref_slot[0] >= 0) {
-            r->type = MBT_SKIP;
-            for (int k = 0; k < 4; k++) r->ref[k] = (uint8_t)ref_slot[0];
-        } else {
-            /* mid-grey I_PCM */
-            int16_t *c = NULL;
-            if (pb->ncoef + 12 <= pb->cap) { c = pb->coef + (size_t)pb->ncoef * 16; pb->ncoef += 12; }
-            if (!c) return -1;
-            memset(c, 128, 384);
-            r->type = MBT_IPCM;
-            r->coef = pb->ncoef - 12;
-        }
-        r->slice = 0xFFFE;
-        n++;
-    }
-    return n;
-}
-
 static int finish_picture(H264Dec *d, int concealed_mbs)
 {
     const Sps *sps = &d->sps[d->active_sps];
@@ -390,21 +368,26 @@ int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id
     if (boundary) {
         if (d->pic_started && d->active_sps >= 0 && d->active_sps < MAX_SPS) {
             if (d->pending_activation) return DEC_FAIL(DEC_ERROR);
-            int ref_slot[MAX_REFS];
-            int is_p = 1;
+            /* conceal what the picture is missing (decoder.c:240-268): as P
+             * after a fresh allocation and RefPicList0 init when no slice
+             * header was valid, else by the last valid slice's type */
+            int is_i;
             if (!d->valid_slice_in_au) {
                 d->cur_slot = dpb_alloc_current(&d->dpb);
                 if (d->cur_slot < 0) return DEC_FAIL(DEC_ERROR);
                 picbuild_reset(&d->pb, 0);
+                d->pb.cur_slot = d->cur_slot;
+                SliceHdr tmp = d->sh;
+                int ref_slot[MAX_REFS];
+                tmp.slice_type = 0;
+                tmp.ref_mod_flag = 0;
+                if (tmp.num_ref_idx_active < 1) tmp.num_ref_idx_active = 1;
+                dpb_build_list(&d->dpb, &tmp, ref_slot);
+                is_i = 0;
             } else {
-                is_p = d->sh.slice_type == 0;
+                is_i = d->sh.slice_type == 2;
             }
-            SliceHdr tmp = d->sh;
-            tmp.slice_type = 0;
-            tmp.ref_mod_flag = 0;
-            if (tmp.num_ref_idx_active < 1) tmp.num_ref_idx_active = 1;
-            dpb_build_list(&d->dpb, &tmp, ref_slot);
-            int n = conceal_picture(d, is_p, ref_slot);
+            int n = h264dec_conceal(d, is_i);
             if (n < 0) return DEC_FAIL(DEC_ERROR);
             d->num_concealed += n;
             *read_bytes = 0;
@@ -480,22 +463,18 @@ int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id
             d->cur_slot = dpb_alloc_current(&d->dpb);
             if (d->cur_slot < 0) return DEC_FAIL(DEC_ERROR);
             picbuild_reset(&d->pb, pps->cip);
+            d->pb.cur_slot = d->cur_slot;
         }
         d->sh = sh;
         d->valid_slice_in_au = 1;
         d->prev_nal = nh;
         int ref_slot[MAX_REFS];
         if (dpb_build_list(&d->dpb, &sh, ref_slot)) return DEC_FAIL(DEC_ERROR);
-        if (sh.slice_type == 0 && ref_slot[0] < 0) return DEC_FAIL(DEC_ERROR);
         d->pb.pc.cip = pps->cip;
-        if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot, (uint16_t)(sh.first_mb & 0xFFFF))) {
-            /* the reference un-marks the slice and conceals at the next AU
-             * boundary (slice_data.c:302-358); drop the slice's MBs */
-            for (int i = 0; i < d->pb.nmbs; i++)
-                if (d->pb.pc.mb[i].slice == (uint16_t)(sh.first_mb & 0xFFFF)) {
-                    d->pb.pc.mb[i].slice = SLICE_NONE;
-                    d->pb.ndecoded--;
-                }
+        if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot)) {
+            /* the slice is un-marked (decoder.c:462-467, slice_data.c:302-358);
+             * its MBs are concealed at the next access-unit boundary */
+            picbuild_mark_slice_corrupted(&d->pb, sh.first_mb);
             return DEC_FAIL(DEC_ERROR);
         }
         if (d->pb.ndecoded == d->pb.nmbs) {
@@ -528,9 +507,13 @@ const uint8_t *h264dec_next_output_rgba(H264Dec *d, uint32_t *pic_id, uint32_t *
     const DpbOut *o = dpb_next_output(&d->dpb);
     if (!o) return NULL;
     uint8_t *dst = rgba ? rgba : d->out_frames + d->frame_bytes * (size_t)o->slot;
-    if (rgba ? d->be.read_rgba(d->be.ctx, o->slot, dst) : d->be.read(d->be.ctx, o->slot, dst)) return NULL;
+    const int rr = rgba ? d->be.read_rgba(d->be.ctx, o->slot, dst) : d->be.read(d->be.ctx, o->slot, dst);
+    if (rr < 0) return NULL;
     if (pic_id) *pic_id = (uint32_t)o->pic_id;
     if (is_idr) *is_idr = (uint32_t)o->is_idr;
-    if (err_mbs) *err_mbs = (uint32_t)o->err_mbs;
+    /* rr > 0: the device flagged the reconstruction (a bounded wait that
+     * expired, or a residual range error the host check did not predict):
+     * the whole picture counts as erroneous */
+    if (err_mbs) *err_mbs = rr > 0 ? (uint32_t)d->pb.nmbs : (uint32_t)o->err_mbs;
     return dst;
 }

@@ -22,10 +22,12 @@ typedef struct H264Backend {
     /* reconstruct + deblock the picture described by pb into slot cur_slot
      * (may run asynchronously; records are consumed before returning) */
     int  (*decode)(void *ctx, const PicBuild *pb, int cur_slot);
-    /* copy slot as planar I420 (w*16 * h*16 * 3/2 bytes) to host memory */
+    /* copy slot as planar I420 (w*16 * h*16 * 3/2 bytes) to host memory;
+     * 0 ok, -1 failure, 1 copied but the device flagged an error in a
+     * reconstruction since the last read */
     int  (*read)(void *ctx, int slot, uint8_t *dst);
     /* copy slot converted to RGBA (w*16 * h*16 * 4 bytes, DecoderPost.js
-     * rgb output); NULL when the backend has no conversion */
+     * rgb output; same returns); NULL when the backend has no conversion */
     int  (*read_rgba)(void *ctx, int slot, uint8_t *dst);
     /* optional: host memory for the output frames (pinned by the HIP
      * backend, so each picture's D2H copy runs at DMA speed); NULL: malloc */
@@ -61,7 +63,8 @@ typedef struct H264Dec {
     /* picture state */
     int  pic_started, valid_slice_in_au, skip_redundant;
     SliceHdr sh;                   /* header of the last decoded slice */
-    NalHdr   prev_nal;
+    NalHdr   prev_nal;             /* prevNalUnit: NAL of the last valid slice header */
+    NalHdr   aub_prev_nal;         /* aub->nuPrev: last slice NAL seen by the boundary check */
     int  cur_pic_id;
     int  cur_slot;
     int  num_concealed;
@@ -98,6 +101,9 @@ const uint8_t *h264dec_next_output(H264Dec *d, uint32_t *pic_id, uint32_t *is_id
 const uint8_t *h264dec_next_output_rgba(H264Dec *d, uint32_t *pic_id, uint32_t *is_idr, uint32_t *err_mbs,
                                         uint8_t *rgba);
 int  h264dec_valid_param_sets(const H264Dec *d);
+/* conceal the current picture's missing MBs (conceal.c); returns their
+ * number or -1 */
+int  h264dec_conceal(H264Dec *d, int is_i);
 const Sps *h264dec_active_sps(const H264Dec *d);
 
 #endif

@@ -1,4 +1,18 @@
-/* Host DPB bookkeeping -- see dpb.h for the reference behaviour it keeps. */
+/* Host DPB bookkeeping -- see dpb.h.
+ *
+ * The entries are kept the way the reference keeps its dpbPicture_t buffer:
+ * an array of dpbSize + 1 positions re-sorted after every marking (and per
+ * inserted non-existing frame) by the same diminishing-increment sort and
+ * ordering -- short-term references by descending PicNum, long-term by
+ * ascending LongTermPicNum, then pictures waiting for display, then the rest
+ * (ShellSort / ComparePictures, h264bsd_dpb.c:138-196, 1612-1640).  The
+ * current picture always takes the last position (h264bsdAllocateDpbImage,
+ * :877-893), RefPicList0 starts as the first numRefFrames positions
+ * (h264bsdInitRefPicList, :1104-1116), and every scan runs over the same
+ * range as the reference's.  Each position carries the device frame slot its
+ * samples live in, moving with the entry as the reference's data pointer
+ * does, so slot reuse -- what an unwritten or partly written picture shows --
+ * is the reference's buffer reuse. */
 #include "dpb.h"
 
 #include <string.h>
@@ -6,6 +20,7 @@
 #define IS_REF(p) ((p)->status != PIC_UNUSED)
 #define IS_SHORT(p) ((p)->status == PIC_SHORT || (p)->status == PIC_NONEXIST)
 #define IS_LONG(p) ((p)->status == PIC_LONG)
+#define IS_EXISTING(p) ((p)->status > PIC_NONEXIST)
 
 void dpb_init(Dpb *d, int dpb_size, int max_ref_frames, int max_frame_num, int no_reorder)
 {
@@ -23,40 +38,44 @@ void dpb_init(Dpb *d, int dpb_size, int max_ref_frames, int max_frame_num, int n
     for (int i = 0; i <= MAX_REFS; i++) d->list[i] = -1;
 }
 
-static int slot_pending_output(const Dpb *d, int slot)
+/* ComparePictures (:138-196): < 0 if a sorts before b */
+static int compare(const DpbPic *a, const DpbPic *b)
 {
-    for (int i = d->out_index; i < d->num_out; i++) if (d->out[i].slot == slot) return 1;
-    return 0;
+    if (!IS_REF(a) && !IS_REF(b)) return (a->to_display && !b->to_display) ? -1 : (!a->to_display && b->to_display) ? 1 : 0;
+    if (!IS_REF(b)) return -1;
+    if (!IS_REF(a)) return 1;
+    if (IS_SHORT(a) && IS_SHORT(b)) return a->pic_num > b->pic_num ? -1 : a->pic_num < b->pic_num ? 1 : 0;
+    if (IS_SHORT(a)) return -1;
+    if (IS_SHORT(b)) return 1;
+    return a->pic_num > b->pic_num ? 1 : a->pic_num < b->pic_num ? -1 : 0;
 }
 
-static int find_free(const Dpb *d)
+/* ShellSort (:1612-1640): increments 7, 3, 1 -- not stable, so equal
+ * entries end where the reference's do only with the same increments */
+static void sort_entries(Dpb *d)
 {
-    int fallback = -1;
-    for (int i = 0; i < d->npic; i++) {
-        const DpbPic *p = &d->pic[i];
-        if (IS_REF(p) || p->to_display || i == d->cur) continue;
-        if (!slot_pending_output(d, p->slot)) return i;
-        if (fallback < 0) fallback = i;
-    }
-    if (fallback < 0)      /* the current entry may be reused */
-        for (int i = 0; i < d->npic; i++)
-            if (!IS_REF(&d->pic[i]) && !d->pic[i].to_display) return i;
-    return fallback;
+    for (int step = 7; step; step >>= 1)
+        for (int i = step; i < d->npic; i++) {
+            const DpbPic t = d->pic[i];
+            int j = i;
+            while (j >= step && compare(&d->pic[j - step], &t) > 0) {
+                d->pic[j] = d->pic[j - step];
+                j -= step;
+            }
+            d->pic[j] = t;
+        }
 }
 
 int dpb_alloc_current(Dpb *d)
 {
-    int saved = d->cur;
-    d->cur = -1;
-    int i = find_free(d);
-    if (i < 0) { d->cur = saved; return -1; }
-    d->cur = i;
-    return d->pic[i].slot;
+    d->cur = d->size;
+    return d->pic[d->cur].slot;
 }
 
+/* SetPicNums (:1189-1210) */
 static void set_pic_nums(Dpb *d, int curr_frame_num)
 {
-    for (int i = 0; i < d->npic; i++) {
+    for (int i = 0; i < d->num_ref; i++) {
         DpbPic *p = &d->pic[i];
         if (IS_SHORT(p))
             p->pic_num = p->frame_num > curr_frame_num ? p->frame_num - d->max_frame_num : p->frame_num;
@@ -70,6 +89,8 @@ static void unmark(Dpb *d, DpbPic *p)
     if (!p->to_display) d->fullness--;
 }
 
+/* OutputPicture + FindSmallestPicOrderCnt (:1398-1460): the first position
+ * with the smallest POC */
 static int output_picture(Dpb *d)
 {
     if (d->no_reorder) return -1;
@@ -87,27 +108,30 @@ static int output_picture(Dpb *d)
     return 0;
 }
 
+/* SlidingWindowRefPicMarking (:905-940): oldest short-term among the first
+ * numRefFrames positions */
 static int sliding_window(Dpb *d)
 {
     if (d->num_ref < d->max_ref) return 0;
     int best = -1;
-    for (int i = 0; i < d->npic; i++)
+    for (int i = 0; i < d->num_ref; i++)
         if (IS_SHORT(&d->pic[i]) && (best < 0 || d->pic[i].pic_num < d->pic[best].pic_num)) best = i;
     if (best < 0) return -1;
     unmark(d, &d->pic[best]);
     return 0;
 }
 
+/* FindDpbPic (:1132-1170): the first maxRefFrames positions */
 static int find_pic(Dpb *d, int pic_num, int short_term)
 {
-    for (int i = 0; i < d->npic; i++) {
+    for (int i = 0; i < d->max_ref && i < d->npic; i++) {
         DpbPic *p = &d->pic[i];
-        if (short_term ? IS_SHORT(p) : IS_LONG(p))
-            if (p->pic_num == pic_num) return i;
+        if ((short_term ? IS_SHORT(p) : IS_LONG(p)) && p->pic_num == pic_num) return i;
     }
     return -1;
 }
 
+/* h264bsdCheckGapsInFrameNum (:1245-1350) */
 int dpb_check_gaps(Dpb *d, int frame_num, int is_ref, int gaps_allowed)
 {
     d->num_out = 0;
@@ -116,16 +140,14 @@ int dpb_check_gaps(Dpb *d, int frame_num, int is_ref, int gaps_allowed)
     if (frame_num != d->prev_ref_frame_num &&
         frame_num != (d->prev_ref_frame_num + 1) % d->max_frame_num) {
         int fn = (d->prev_ref_frame_num + 1) % d->max_frame_num;
+        /* the last position's slot is what the current picture would get;
+         * it must not be a slot placed in the output queue below */
+        const int keep = d->pic[d->size].slot;
         do {
             set_pic_nums(d, fn);
             if (sliding_window(d)) return -1;
             while (d->fullness >= d->size) if (output_picture(d)) break;
-            int saved = d->cur;
-            d->cur = -1;
-            int e = find_free(d);
-            d->cur = saved;
-            if (e < 0) return -1;
-            DpbPic *p = &d->pic[e];
+            DpbPic *p = &d->pic[d->size];
             p->status = PIC_NONEXIST;
             p->frame_num = fn;
             p->pic_num = fn;
@@ -133,8 +155,19 @@ int dpb_check_gaps(Dpb *d, int frame_num, int is_ref, int gaps_allowed)
             p->to_display = 0;
             d->fullness++;
             d->num_ref++;
+            sort_entries(d);
             fn = (fn + 1) % d->max_frame_num;
         } while (fn != frame_num);
+        for (int i = 0; i < d->num_out; i++)
+            if (d->out[i].slot == d->pic[d->size].slot) {
+                for (int k = 0; k < d->size; k++)
+                    if (d->pic[k].slot == keep) {
+                        d->pic[k].slot = d->pic[d->size].slot;
+                        d->pic[d->size].slot = keep;
+                        break;
+                    }
+                break;
+            }
     } else if (is_ref && frame_num == d->prev_ref_frame_num) {
         return -1;
     }
@@ -144,33 +177,19 @@ int dpb_check_gaps(Dpb *d, int frame_num, int is_ref, int gaps_allowed)
     return 0;
 }
 
+/* h264bsdInitRefPicList (:1104-1116) + h264bsdReorderRefPicList (:224-300) */
 int dpb_build_list(Dpb *d, const SliceHdr *sh, int *ref_slot)
 {
-    int n = 0;
+    for (int i = 0; i < d->num_ref; i++) d->list[i] = i;
     set_pic_nums(d, sh->frame_num);
-    /* short-term by descending PicNum, then long-term by ascending LongTermPicNum */
-    int idx[DPB_MAX];
-    for (int i = 0; i < d->npic; i++) if (IS_SHORT(&d->pic[i])) idx[n++] = i;
-    for (int a = 1; a < n; a++)
-        for (int b = a; b > 0 && d->pic[idx[b]].pic_num > d->pic[idx[b - 1]].pic_num; b--) {
-            int t = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = t;
-        }
-    int ns = n;
-    for (int i = 0; i < d->npic; i++) if (IS_LONG(&d->pic[i])) idx[n++] = i;
-    for (int a = ns + 1; a < n; a++)
-        for (int b = a; b > ns && d->pic[idx[b]].pic_num < d->pic[idx[b - 1]].pic_num; b--) {
-            int t = idx[b]; idx[b] = idx[b - 1]; idx[b - 1] = t;
-        }
-    for (int i = 0; i <= MAX_REFS; i++) d->list[i] = i < n ? idx[i] : -1;
-
     if (sh->slice_type == 0 && sh->ref_mod_flag) {
-        int nact = sh->num_ref_idx_active;
+        const int nact = sh->num_ref_idx_active;
         int pred = sh->frame_num, ref_idx = 0;
         for (int k = 0; sh->ref_mod[k].idc != 3; k++) {
             int pn, st;
             if (sh->ref_mod[k].idc < 2) {
                 int nw;
-                int diff = (int)sh->ref_mod[k].val + 1;
+                const int diff = (int)sh->ref_mod[k].val + 1;
                 if (sh->ref_mod[k].idc == 0) { nw = pred - diff; if (nw < 0) nw += d->max_frame_num; }
                 else { nw = pred + diff; if (nw >= d->max_frame_num) nw -= d->max_frame_num; }
                 pred = nw;
@@ -180,27 +199,27 @@ int dpb_build_list(Dpb *d, const SliceHdr *sh, int *ref_slot)
                 pn = (int)sh->ref_mod[k].val;
                 st = 0;
             }
-            int e = find_pic(d, pn, st);
-            if (e < 0 || d->pic[e].status == PIC_NONEXIST) return -1;
+            const int e = find_pic(d, pn, st);
+            if (e < 0 || !IS_EXISTING(&d->pic[e])) return -1;
             for (int j = nact; j > ref_idx; j--) d->list[j] = d->list[j - 1];
             d->list[ref_idx++] = e;
             int w = ref_idx;
             for (int j = ref_idx; j <= nact; j++) if (d->list[j] != e) d->list[w++] = d->list[j];
-            for (; w <= nact; w++) d->list[w] = -1;
         }
     }
+    /* h264bsdGetRefPicData (:846-860) */
     for (int i = 0; i < MAX_REFS; i++) {
-        int e = i < sh->num_ref_idx_active ? d->list[i] : -1;
-        ref_slot[i] = (e >= 0 && d->pic[e].status > PIC_NONEXIST) ? d->pic[e].slot : -1;
+        const int e = i < sh->num_ref_idx_active ? d->list[i] : -1;
+        ref_slot[i] = (e >= 0 && IS_EXISTING(&d->pic[e])) ? d->pic[e].slot : -1;
     }
     return 0;
 }
 
+/* Mmcop5 (:520-545): every reference unused, everything displayable queued */
 static void mmco5(Dpb *d)
 {
     for (int i = 0; i < d->npic; i++) {
         DpbPic *p = &d->pic[i];
-        if (i == d->cur) continue;
         if (IS_REF(p)) {
             p->status = PIC_UNUSED;
             if (!p->to_display) d->fullness--;
@@ -212,14 +231,25 @@ static void mmco5(Dpb *d)
     d->prev_ref_frame_num = 0;
 }
 
+/* a long-term picture holding LongTermFrameIdx idx among the first
+ * maxRefFrames positions becomes unused (Mmcop3 / Mmcop6 :424-432, 582-590) */
+static void free_lt_idx(Dpb *d, int idx)
+{
+    for (int i = 0; i < d->max_ref && i < d->npic; i++)
+        if (IS_LONG(&d->pic[i]) && d->pic[i].pic_num == idx) {
+            unmark(d, &d->pic[i]);
+            break;
+        }
+}
+
+/* h264bsdMarkDecRefPic (:650-833) */
 int dpb_mark(Dpb *d, const SliceHdr *sh, int is_ref, int frame_num, int poc, int is_idr,
              int pic_id, int err_mbs)
 {
     DpbPic *c = &d->pic[d->cur];
     int status = 0;
-    int to_disp = !d->no_reorder;
+    const int to_disp = !d->no_reorder;
     d->last_mmco5 = 0;
-    set_pic_nums(d, frame_num);
     if (!is_ref) {
         c->status = PIC_UNUSED;
         c->frame_num = frame_num;
@@ -229,7 +259,6 @@ int dpb_mark(Dpb *d, const SliceHdr *sh, int is_ref, int frame_num, int poc, int
         if (!d->no_reorder) d->fullness++;
     } else if (is_idr) {
         d->num_out = d->out_index = 0;
-        c->to_display = 0;
         mmco5(d);
         if (sh->no_output_prior || d->no_reorder) d->num_out = d->out_index = 0;
         if (sh->long_term_ref) { c->status = PIC_LONG; d->max_lt_idx = 0; }
@@ -259,29 +288,26 @@ int dpb_mark(Dpb *d, const SliceHdr *sh, int is_ref, int frame_num, int poc, int
                     break;
                 case 3:
                     if (d->max_lt_idx < 0 || (int)m->lt_idx > d->max_lt_idx) { status = -1; break; }
-                    e = find_pic(d, (int)m->lt_idx, 0);
-                    if (e >= 0) unmark(d, &d->pic[e]);
+                    free_lt_idx(d, (int)m->lt_idx);
                     e = find_pic(d, frame_num - (int)m->diff, 1);
-                    if (e < 0 || d->pic[e].status == PIC_NONEXIST) { status = -1; break; }
+                    if (e < 0 || !IS_EXISTING(&d->pic[e])) { status = -1; break; }
                     d->pic[e].status = PIC_LONG;
                     d->pic[e].pic_num = (int)m->lt_idx;
                     break;
                 case 4:
                     d->max_lt_idx = (int)m->max_lt_idx - 1;
-                    for (int i = 0; i < d->npic; i++)
+                    for (int i = 0; i < d->max_ref && i < d->npic; i++)
                         if (IS_LONG(&d->pic[i]) && (d->max_lt_idx < 0 || d->pic[i].pic_num > d->max_lt_idx))
                             unmark(d, &d->pic[i]);
                     break;
                 case 5:
-                    c->to_display = 0;
                     mmco5(d);
                     d->last_mmco5 = 1;
                     frame_num = 0;
                     break;
                 case 6:
                     if (d->max_lt_idx < 0 || (int)m->lt_idx > d->max_lt_idx) { status = -1; break; }
-                    e = find_pic(d, (int)m->lt_idx, 0);
-                    if (e >= 0) unmark(d, &d->pic[e]);
+                    free_lt_idx(d, (int)m->lt_idx);
                     if (d->num_ref < d->max_ref) {
                         c->frame_num = frame_num;
                         c->pic_num = (int)m->lt_idx;
@@ -325,6 +351,7 @@ int dpb_mark(Dpb *d, const SliceHdr *sh, int is_ref, int frame_num, int poc, int
     } else {
         while (d->fullness > d->size) if (output_picture(d)) break;
     }
+    sort_entries(d);
     return status;
 }
 

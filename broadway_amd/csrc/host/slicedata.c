@@ -8,6 +8,7 @@
  * (intra_prediction.c:1885-1936). */
 #include "picbuild.h"
 #include "../common/cavlc.h"
+#include "../common/resid.h"
 #include "../common/tables.h"
 
 #include <stdlib.h>
@@ -19,22 +20,26 @@ int picbuild_init(PicBuild *pb, int w_mbs, int h_mbs)
     pb->w = w_mbs; pb->h = h_mbs; pb->nmbs = w_mbs * h_mbs;
     pb->rec = (MbRec *)calloc((size_t)pb->nmbs, sizeof(MbRec));
     pb->pc.mb = (MbInfo *)calloc((size_t)pb->nmbs, sizeof(MbInfo));
+    pb->decoded = (uint8_t *)calloc((size_t)pb->nmbs, 1);
     pb->cap = (uint32_t)pb->nmbs * 8 + 64;
     pb->coef = (int16_t *)malloc((size_t)pb->cap * 32);
     pb->pc.w = w_mbs; pb->pc.h = h_mbs;
-    if (!pb->rec || !pb->pc.mb || !pb->coef) { picbuild_free(pb); return -1; }
+    if (!pb->rec || !pb->pc.mb || !pb->coef || !pb->decoded) { picbuild_free(pb); return -1; }
     return 0;
 }
 
 void picbuild_free(PicBuild *pb)
 {
-    free(pb->rec); free(pb->pc.mb); free(pb->coef);
-    pb->rec = NULL; pb->pc.mb = NULL; pb->coef = NULL;
+    free(pb->rec); free(pb->pc.mb); free(pb->coef); free(pb->decoded);
+    pb->rec = NULL; pb->pc.mb = NULL; pb->coef = NULL; pb->decoded = NULL;
 }
 
 void picbuild_reset(PicBuild *pb, int cip)
 {
+    /* h264bsdResetStorage (storage.c:442-462): no MB decoded, no slice id */
     for (int i = 0; i < pb->nmbs; i++) pb->pc.mb[i].slice = SLICE_NONE;
+    memset(pb->decoded, 0, (size_t)pb->nmbs);
+    pb->last_mb_addr = 0;
     pb->pc.cip = cip;
     pb->ncoef = 0;
     pb->ndecoded = 0;
@@ -44,7 +49,7 @@ void picbuild_reset(PicBuild *pb, int cip)
     pb->n_inter = pb->n_intra = pb->n_coded_blocks = 0;
 }
 
-static int16_t *coef_alloc(PicBuild *pb, uint32_t nblk)
+int16_t *picbuild_coef_alloc(PicBuild *pb, uint32_t nblk)
 {
     if (pb->ncoef + nblk > pb->cap) {
         uint32_t nc = pb->cap * 2;
@@ -95,8 +100,44 @@ static void finish_rec(PicBuild *pb, int cur, const SliceHdr *sh, const Pps *pps
     r->rsv0 = 0;
 }
 
+/* The prediction-stage checks of h264bsdDecodeMacroblock that fail an MB:
+ * motion vectors outside [-2048, 2047.75] x [-512, 511.75]
+ * (inter_prediction.c:544-549, 620-628, ...) and intra modes that need an
+ * unavailable neighbour (intra_prediction.c:656-677 16x16, 770-821 4x4,
+ * 878-899 chroma).  Availability is the record's (slice + constrained
+ * intra applied). */
+static int mb_pred_valid(const MbRec *r)
+{
+    if (r->type == MBT_INTER || r->type == MBT_SKIP) {
+        for (int b = 0; b < 16; b++)
+            if ((uint32_t)(r->mv[b][0] + 8192) >= 16384u || (uint32_t)(r->mv[b][1] + 2048) >= 4096u) return 0;
+        return 1;
+    }
+    if (r->type == MBT_IPCM) return 1;
+    const int A = r->avail & AV_A, B = r->avail & AV_B, D = r->avail & AV_D;
+    if (r->type == MBT_I16) {
+        const int mode = r->pred & 3;
+        if ((mode == 0 && !B) || (mode == 1 && !A) || (mode == 3 && !(A && B && D))) return 0;
+    } else {
+        for (int b = 0; b < 16; b++) {
+            const int mode = (r->i4[b >> 1] >> ((b & 1) * 4)) & 15;
+            const int x = kBlkX[b], y = kBlkY[b];
+            const int L = x > 0 || A, T = y > 0 || B;
+            const int TL = (x > 0 && y > 0) || (x == 0 && y > 0 ? A : (y == 0 && x > 0 ? B : D));
+            if (((mode == 0 || mode == 3 || mode == 7) && !T) || ((mode == 1 || mode == 8) && !L) ||
+                ((mode >= 4 && mode <= 6) && !(T && L && TL)))
+                return 0;
+        }
+    }
+    const int cm = (r->pred >> 4) & 3;
+    return !((cm == 1 && !A) || (cm == 2 && !B) || (cm == 3 && !(A && B && D)));
+}
+
 static void decode_skip(PicBuild *pb, int cur, int qp, const int *ref_slot)
 {
+    /* P_Skip predicts from RefPicList0[0]; a missing picture fails the MB
+     * (h264bsdInterPrediction -> h264bsdDecodeMacroblock NOK) */
+    if (ref_slot[0] < 0) pb->mb_decode_err = 1;
     MbInfo *m = &pb->pc.mb[cur];
     MbRec *r = &pb->rec[cur];
     int16_t mv[2];
@@ -192,7 +233,7 @@ static int parse_inter_pred(PicBuild *pb, BitReader *br, int cur, int kind, int 
     }
     for (int i = 0; i < 4; i++) {
         int s = ref_slot[m->refidx[i]];
-        if (s < 0) return -1;                      /* reference picture missing */
+        if (s < 0) pb->mb_decode_err = 1;          /* reference picture missing: fails at reconstruction */
         r->ref[i] = (uint8_t)s;
     }
     memcpy(r->mv, m->mv, sizeof(r->mv));
@@ -217,7 +258,7 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     if (!inter && mbt == 25) {                       /* I_PCM, §7.3.5 */
         m->type = MBT_IPCM;
         while (!br_byte_aligned(br)) if (br_u1(br)) return -1;
-        int16_t *dst = coef_alloc(pb, 12);
+        int16_t *dst = picbuild_coef_alloc(pb, 12);
         if (!dst) return -1;
         uint8_t *d8 = (uint8_t *)dst;
         for (int i = 0; i < 384; i++) d8[i] = (uint8_t)br_u(br, 8);
@@ -322,8 +363,14 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
                 m->tcc[comp * 4 + b] = 0;
             }
         }
+    if (br->err) return -1;
+    /* h264bsdDecodeMacroblock -> ProcessResidual: a residual outside
+     * [-512, 511] fails the MB, hence the slice (resid.h) */
+    if (cbits && !mb_residual_in_range((const int16_t (*)[16])blk, cbits, is_i16, *qp,
+                                       kQpChroma[clip3(0, 51, *qp + pps->chroma_qp_offset)]))
+        pb->mb_decode_err = 1;
     int nblk = __builtin_popcount(cbits);
-    int16_t *dst = coef_alloc(pb, (uint32_t)nblk);
+    int16_t *dst = picbuild_coef_alloc(pb, (uint32_t)nblk);
     if (!dst) return -1;
     r->coef = pb->ncoef - (uint32_t)nblk;
     r->cbits = cbits;
@@ -333,26 +380,50 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     return br->err ? -1 : 0;
 }
 
+/* An MB whose syntax parsed but whose reconstruction fails (residual range,
+ * motion vector range, missing reference, intra mode without neighbours):
+ * the reference has already counted it decoded (macroblock_layer.c:988) and
+ * writes no samples for it.  Unless the slice's un-marking reaches it
+ * (slice_data.c:322-338 can stop short of an I slice's second MB) it stays in
+ * the picture with the slot's previous samples and its own deblocking
+ * parameters: a zero-vector copy of the current slot, filtered as intra if it
+ * was intra. */
+static void failed_mb(PicBuild *pb, int cur)
+{
+    MbRec *r = &pb->rec[cur];
+    const int intra = r->type >= MBT_I4x4;
+    r->type = MBT_SKIP;
+    r->cbits = 0;
+    memset(r->mv, 0, sizeof(r->mv));
+    for (int i = 0; i < 4; i++) r->ref[i] = (uint8_t)pb->cur_slot;
+    r->dbf = intra ? DBF_INTRA : 0;
+    pb->decoded[cur] = 1;
+}
+
 int parse_slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps *pps,
-                     const int *ref_slot, uint16_t tag)
+                     const int *ref_slot)
 {
     int cur = sh->first_mb;
     int qp = sh->slice_qp;
     int is_p = sh->slice_type == 0;
-    int more = 1;
+    int more = 1, count = 0;
+    const uint16_t tag = (uint16_t)++pb->nslices;     /* sliceId, slice_data.c:120 */
+    pb->last_mb_addr = 0;
     if (is_p) pb->is_p = 1;
-    pb->nslices++;
     while (more) {
         if (is_p) {
             uint32_t run = br_ue(br);
             if (br->err || run > (uint32_t)(pb->nmbs - cur)) return -1;
             for (uint32_t i = 0; i < run; i++, cur++) {
-                if (pb->pc.mb[cur].slice != SLICE_NONE) return -1;
+                if (pb->decoded[cur]) return -1;      /* primary picture, already decoded */
                 memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
                 pb->pc.mb[cur].slice = tag;
+                pb->mb_decode_err = 0;
                 decode_skip(pb, cur, qp, ref_slot);
                 finish_rec(pb, cur, sh, pps, tag);
-                pb->ndecoded++;
+                if (pb->mb_decode_err || !mb_pred_valid(&pb->rec[cur])) { failed_mb(pb, cur); return -1; }
+                pb->decoded[cur] = 1;
+                count++;
             }
             if (run > 0) {
                 more = br_more_rbsp_data(br);
@@ -360,14 +431,40 @@ int parse_slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps 
             }
         }
         if (cur >= pb->nmbs) return -1;
-        if (pb->pc.mb[cur].slice != SLICE_NONE) return -1;
+        if (pb->decoded[cur]) return -1;
         memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
-        pb->pc.mb[cur].slice = tag;
+        pb->pc.mb[cur].slice = tag;                   /* SetMbParams precedes the parse */
+        pb->mb_decode_err = 0;
         if (parse_mb(pb, br, cur, sh, pps, ref_slot, &qp)) return -1;
         finish_rec(pb, cur, sh, pps, tag);
-        pb->ndecoded++;
+        if (pb->mb_decode_err || !mb_pred_valid(&pb->rec[cur])) { failed_mb(pb, cur); return -1; }
+        pb->decoded[cur] = 1;
+        count++;
+        if (!is_p) pb->last_mb_addr = cur;            /* slice_data.c:208-211 */
         cur++;
         more = br_more_rbsp_data(br);
     }
-    return br->err ? -1 : 0;
+    if (br->err || pb->ndecoded + count > pb->nmbs) return -1;
+    pb->ndecoded += count;
+    return 0;
+}
+
+void picbuild_mark_slice_corrupted(PicBuild *pb, int first_mb)
+{
+    const uint16_t tag = (uint16_t)pb->nslices;
+    int cur = first_mb;
+    if (pb->last_mb_addr) {
+        /* I slice: keep all but the last max(width, 10) decoded MBs */
+        const int keep_back = pb->w > 10 ? pb->w : 10;
+        int i = pb->last_mb_addr - 1, n = 0;
+        while (i > cur) {
+            if (pb->pc.mb[i].slice == tag && ++n >= keep_back) break;
+            i--;
+        }
+        cur = i;
+    }
+    for (; cur < pb->nmbs; cur++) {
+        if (pb->pc.mb[cur].slice != tag || !pb->decoded[cur]) break;
+        pb->decoded[cur] = 0;
+    }
 }

@@ -50,13 +50,22 @@ enum {
     DB_LEFT = 16, DB_TOP = 32, DB_INNER = 64,
 };
 
+/* dbf bits */
+enum {
+    /* the MB counts as intra in the bS derivation although its samples are
+     * an inter copy: a concealed MB is set to I_4x4 "to perform filtering"
+     * (h264bsd_conceal.c:300-308) while P concealment copies the co-located
+     * MB of a reference picture (:310-332) */
+    DBF_INTRA = 1,
+};
+
 typedef struct MbRec {
     uint8_t  type;      /* MBT_* */
     uint8_t  qp;        /* QPY (I_PCM: 0) */
     uint8_t  qpc;       /* QPc = QpChroma[clip3(0,51,QPY+chroma_qp_index_offset)] */
     uint8_t  avail;     /* AV_* | DB_* */
     uint8_t  pred;      /* I16: mode (bits 0-1); chroma mode bits 4-5 */
-    uint8_t  dbf;       /* unused (reserved) */
+    uint8_t  dbf;       /* DBF_* */
     int8_t   offA;      /* FilterOffsetA = slice_alpha_c0_offset_div2 << 1 */
     int8_t   offB;      /* FilterOffsetB */
     uint32_t cbits;     /* coded-block mask, see above */

@@ -35,6 +35,8 @@ def lib() -> C.CDLL:
                                          C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_size_t)]
         L.oracle_result_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
         L.oracle_result_free.argtypes = [C.c_void_p]
+        L.oracle_result_pics.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_result_pics.restype = C.c_int
         L.oracle_replay_create.argtypes = [C.c_int, C.c_int, C.c_int]
         L.oracle_replay_create.restype = C.c_void_p
         L.oracle_replay_picture.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int]
@@ -48,9 +50,10 @@ def lib() -> C.CDLL:
     return _L
 
 
-def decode(stream: bytes, no_reorder: bool = False) -> Tuple[List[bytes], int, int, int, float]:
+def decode(stream: bytes, no_reorder: bool = False, info: bool = False):
     """Decode a whole Annex-B stream on the CPU (DecTestBench semantics incl.
-    the end-of-stream flush).  Returns (frames, errors, width, height, seconds)."""
+    the end-of-stream flush).  Returns (frames, errors, width, height, seconds)
+    [+ per output picture (pic_id, is_idr, nbrOfErrMBs) if info]."""
     L = lib()
     buf = C.create_string_buffer(stream, len(stream))
     secs = C.c_double()
@@ -59,9 +62,14 @@ def decode(stream: bytes, no_reorder: bool = False) -> Tuple[List[bytes], int, i
     L.oracle_result_info(res, C.byref(n), C.byref(e), C.byref(w), C.byref(h), C.byref(nb))
     data = np.empty(nb.value, dtype=np.uint8)
     L.oracle_result_copy(res, data.ctypes.data, nb.value)
+    pics = np.zeros(3 * max(n.value, 1), dtype=np.int32)
+    L.oracle_result_pics(res, pics.ctypes.data, int(pics.size))
     L.oracle_result_free(res)
     fb = w.value * h.value * 3 // 2
     frames = [data[i * fb:(i + 1) * fb].tobytes() for i in range(n.value)] if fb else []
+    if info:
+        return frames, e.value, w.value, h.value, secs.value, [tuple(int(x) for x in pics[3 * i:3 * i + 3])
+                                                               for i in range(n.value)]
     return frames, e.value, w.value, h.value, secs.value
 
 
@@ -90,8 +98,11 @@ def md5(b: bytes) -> str:
     return hashlib.md5(b).hexdigest()
 
 
-def refdec_frames(stream: bytes, no_reorder: bool = False) -> List[bytes]:
-    """Decode with the reference C decoder (only in the build container)."""
+def refdec_frames(stream: bytes, no_reorder: bool = False, info: bool = False):
+    """Decode with the reference C decoder (only in the build container).
+    info=True: also return one (pic_id, is_idr, concealed MBs) per output
+    picture, parsed from DecTestBench's "PIC n, type T[, decoded pic k]
+    [, concealed c]" lines (DecTestBench.c:313-323, 377-385)."""
     if not os.path.exists(REFDEC):
         raise FileNotFoundError(REFDEC)
     with tempfile.TemporaryDirectory() as td:
@@ -102,13 +113,25 @@ def refdec_frames(stream: bytes, no_reorder: bool = False) -> List[bytes]:
         args = [REFDEC, "-O" + yuv] + (["-R"] if no_reorder else []) + [src]
         out = subprocess.run(args, capture_output=True, text=True)
         w = h = None
+        pics = []
         for line in out.stdout.splitlines():
             if line.startswith("Width"):
                 parts = line.split()
                 w, h = int(parts[1]), int(parts[3])
+            elif line.startswith("PIC "):
+                f = [x.strip() for x in line.split(",")]
+                n = int(f[0].split()[1])
+                pid, conc = n, 0
+                for x in f[2:]:
+                    if x.startswith("decoded pic"):
+                        pid = int(x.split()[2])
+                    elif x.startswith("concealed"):
+                        conc = int(x.split()[1])
+                pics.append((pid, int(f[1] == "type IDR"), conc))
         data = open(yuv, "rb").read() if os.path.exists(yuv) else b""
     fb = w * h * 3 // 2 if w else 0
-    return [data[i:i + fb] for i in range(0, len(data), fb)] if fb else []
+    frames = [data[i:i + fb] for i in range(0, len(data), fb)] if fb else []
+    return (frames, pics) if info else frames
 
 
 def yuv2rgba(i420, width: int, height: int) -> bytes:

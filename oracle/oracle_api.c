@@ -14,6 +14,8 @@ typedef struct OracleOut {
     size_t   len, cap;
     int      npics, errors;
     int      w, h;
+    int     *info;           /* per output picture: pic_id, is_idr, err_mbs */
+    int      info_cap;
 } OracleOut;
 
 static void out_append(OracleOut *o, const uint8_t *p, size_t n)
@@ -34,6 +36,13 @@ static void drain(H264Dec *d, OracleOut *o)
     uint32_t id, idr, em;
     while ((pic = h264dec_next_output(d, &id, &idr, &em)) != NULL) {
         out_append(o, pic, d->frame_bytes);
+        if (o->npics >= o->info_cap) {
+            o->info_cap = o->info_cap ? o->info_cap * 2 : 64;
+            o->info = (int *)realloc(o->info, sizeof(int) * 3 * (size_t)o->info_cap);
+        }
+        o->info[3 * o->npics] = (int)id;
+        o->info[3 * o->npics + 1] = (int)idr;
+        o->info[3 * o->npics + 2] = (int)em;
         o->npics++;
         o->errors += (int)em;
     }
@@ -42,6 +51,8 @@ static void drain(H264Dec *d, OracleOut *o)
 /* Decode buf; returns an opaque result (frames concatenated, I420 MB-aligned). */
 void *oracle_decode_stream(const uint8_t *buf, size_t len, int no_reorder, double *seconds)
 {
+    /* DecTestBench feeds the whole remaining buffer and passes
+     * intraConcealmentMethod = 0 (DecTestBench.c:211) */
     OracleOut *o = (OracleOut *)calloc(1, sizeof(OracleOut));
     H264Dec *d = (H264Dec *)calloc(1, sizeof(H264Dec));
     if (!o || !d) { free(o); free(d); return NULL; }
@@ -49,7 +60,7 @@ void *oracle_decode_stream(const uint8_t *buf, size_t len, int no_reorder, doubl
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     const uint8_t *p = buf;
-    uint32_t left = (uint32_t)len, pic_id = 0;
+    uint32_t left = (uint32_t)len, pic_id = 1;   /* picDecodeNumber starts at 1 (DecTestBench.c:218) */
     while (left > 0) {
         uint32_t rb = 0;
         int r = h264dec_decode(d, p, left, pic_id, &rb);
@@ -87,10 +98,20 @@ int oracle_result_copy(void *res, uint8_t *dst, size_t cap)
     return 0;
 }
 
+/* per output picture (pic_id, is_idr, nbrOfErrMBs), 3 ints each */
+int oracle_result_pics(void *res, int *dst, int cap)
+{
+    OracleOut *o = (OracleOut *)res;
+    if (!o || cap < 3 * o->npics) return -1;
+    if (o->npics) memcpy(dst, o->info, sizeof(int) * 3 * (size_t)o->npics);
+    return o->npics;
+}
+
 void oracle_result_free(void *res)
 {
     OracleOut *o = (OracleOut *)res;
     if (!o) return;
+    free(o->info);
     free(o->data);
     free(o);
 }

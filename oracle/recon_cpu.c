@@ -22,7 +22,7 @@
  *              tables :77-98
  * Parity of this restatement is pinned against the reference decoder itself
  * (oracle/_ref/refdec, built by oracle/Makefile.ref) through the per-frame MD5
- * fixtures in tests/golden/ (tests/gen_golden.py).
+ * fixtures in tests/golden/ (tests/golden/make_golden.py).
  */
 #include "recon_cpu.h"
 #include "../broadway_amd/csrc/common/tables.h"
@@ -438,7 +438,7 @@ static void recon_inter(const OracleCtx *c, Planes *pl, int mbx, int mby, const 
 /* ---------------------------------------------------------- deblock --- */
 static int bs_edge(const MbRec *p, int bp, const MbRec *q, int bq, int mb_edge)
 {
-    if (p->type >= MBT_I4x4 || q->type >= MBT_I4x4) return mb_edge ? 4 : 3;
+    if (p->type >= MBT_I4x4 || q->type >= MBT_I4x4 || ((p->dbf | q->dbf) & DBF_INTRA)) return mb_edge ? 4 : 3;
     if (((p->cbits >> bp) & 1) || ((q->cbits >> bq) & 1)) return 2;
     if (p->ref[bp >> 2] != q->ref[bq >> 2]) return 1;
     if (iabs(p->mv[bp][0] - q->mv[bq][0]) >= 4 || iabs(p->mv[bp][1] - q->mv[bq][1]) >= 4) return 1;

@@ -1,45 +1,57 @@
 """DecTestBench-style driver of the product H264SwDec* C-ABI (ctypes): feed
 the whole Annex-B buffer, drain NextPicture after every PIC_RDY, flush at end
-of stream (reference DecTestBench.c:254-416 call protocol)."""
+of stream (reference DecTestBench.c:218-416 call protocol: picId counts
+decoded pictures from 1; STRM_PROCESSED / STRM_ERR end a byte-stream run)."""
 import ctypes as C
 
 from broadway_amd import _lib
 
 
-def swdec_decode(stream: bytes, no_reorder: bool = False):
+def swdec_decode(stream: bytes, no_reorder: bool = False, info: bool = False):
+    """Returns (frames, error_returns) [+ per output picture (picId,
+    isIdrPicture, nbrOfErrMBs) if info]."""
     L = _lib.mi()
     inst = C.c_void_p()
     assert L.H264SwDecInit(C.byref(inst), int(no_reorder)) == _lib.H264SWDEC_OK
     buf = (C.c_uint8 * len(stream)).from_buffer_copy(stream)
     inp, out = _lib.H264SwDecInput(), _lib.H264SwDecOutput()
-    pic, info = _lib.H264SwDecPicture(), _lib.H264SwDecInfo()
+    pic, dinfo = _lib.H264SwDecPicture(), _lib.H264SwDecInfo()
     inp.pStream = C.cast(buf, C.POINTER(C.c_uint8))
     inp.dataLen = len(stream)
-    base = C.addressof(buf)
-    frames, size, errors = [], 0, 0
+    inp.intraConcealmentMethod = 0
+    frames, pics, size, errors = [], [], 0, 0
 
     def drain(flush):
         while L.H264SwDecNextPicture(inst, C.byref(pic), flush) == _lib.H264SWDEC_PIC_RDY:
             frames.append(C.string_at(C.cast(pic.pOutputPicture, C.c_void_p), size))
+            pics.append((pic.picId, pic.isIdrPicture, pic.nbrOfErrMBs))
 
-    pic_id = 0
+    def advance():
+        consumed = C.cast(out.pStrmCurrPos, C.c_void_p).value - C.cast(inp.pStream, C.c_void_p).value
+        inp.dataLen -= consumed
+        inp.pStream = C.cast(C.c_void_p(C.cast(inp.pStream, C.c_void_p).value + consumed), C.POINTER(C.c_uint8))
+
+    pic_id = 1
     while inp.dataLen > 0:
         inp.picId = pic_id
         ret = L.H264SwDecDecode(inst, C.byref(inp), C.byref(out))
         if ret == _lib.H264SWDEC_HDRS_RDY_BUFF_NOT_EMPTY:
-            assert L.H264SwDecGetInfo(inst, C.byref(info)) == _lib.H264SWDEC_OK
-            size = info.picWidth * info.picHeight * 3 // 2
+            assert L.H264SwDecGetInfo(inst, C.byref(dinfo)) == _lib.H264SWDEC_OK
+            size = dinfo.picWidth * dinfo.picHeight * 3 // 2
+            advance()
         elif ret in (_lib.H264SWDEC_PIC_RDY, _lib.H264SWDEC_PIC_RDY_BUFF_NOT_EMPTY):
+            if ret == _lib.H264SWDEC_PIC_RDY_BUFF_NOT_EMPTY:
+                advance()
+            else:
+                inp.dataLen = 0
             pic_id += 1
             drain(0)
-        elif ret < 0:
+        elif ret in (_lib.H264SWDEC_STRM_PROCESSED, _lib.H264SWDEC_STRM_ERR):
+            errors += ret == _lib.H264SWDEC_STRM_ERR
+            inp.dataLen = 0
+        else:
             errors += 1
-        consumed = C.cast(out.pStrmCurrPos, C.c_void_p).value - C.cast(inp.pStream, C.c_void_p).value
-        inp.dataLen -= consumed
-        inp.pStream = C.cast(C.c_void_p(C.cast(inp.pStream, C.c_void_p).value + consumed), C.POINTER(C.c_uint8))
-        if consumed == 0 and ret < 0:
             break
     drain(1)
     L.H264SwDecRelease(inst)
-    del base
-    return frames, errors
+    return (frames, errors, pics) if info else (frames, errors)

@@ -44,6 +44,29 @@ CASES = {
     "cfg2_720p_ionly_idc1_s2": (1, 2, dict(nframes=3, dbf_idc1_pct=100), False),
     "cfg5_2160p_s200": (4, 200, dict(nframes=4), False),
 }
+# Damaged streams (generator knobs err_range_pct / drop_* /
+# trunc_slice_pct / gaps_allowed): residuals out of range, lost and truncated
+# slices, lost pictures -> the reference's slice un-marking and concealment.
+# Their fixtures also hold every output picture's (picId, isIdr, nbrOfErrMBs)
+# as DecTestBench prints it.
+_B = dict(nframes=12, w_mbs=11, h_mbs=9, crop_bottom=0, slices=3, gop=6)
+ERR_CASES = {
+    # I slices: includes an error on a slice's second MB, which the
+    # reference's un-marking does not reach (slice_data.c:322-338)
+    "err_range_i_9x6": (1, 2, dict(nframes=4, w_mbs=9, h_mbs=6, slices=4, err_range_pct=60), False),
+    "err_range_p_11x9": (2, 6, dict(_B, err_range_pct=60), False),
+    "err_drop_slice_11x9": (2, 7, dict(_B, drop_slice_pct=25), False),
+    "err_trunc_slice_11x9": (2, 8, dict(_B, trunc_slice_pct=25), False),
+    "err_drop_pic_gaps_11x9": (2, 10, dict(_B, drop_pic_pct=20, gaps_allowed=1), False),
+    # POC type 0 reordering + truncation inside slice headers (the access-unit
+    # boundary check fails part-way, storage.c:632-776)
+    "err_mixed_poc0_9x2": (2, 5822, dict(nframes=12, w_mbs=9, h_mbs=2, slices=4, crop_bottom=0, gop=7,
+                                         num_ref_frames=2, poc_type=0, dbf_idc2_pct=60, poc_swap=1,
+                                         err_range_pct=10, trunc_slice_pct=30, drop_pic_pct=10), False),
+    "err_720p_ionly_conceal": (1, 3, dict(nframes=3, drop_slice_pct=30, trunc_slice_pct=30), False),
+    "err_1080p_mixed": (3, 300, dict(nframes=8, err_range_pct=20, drop_slice_pct=10, trunc_slice_pct=10), False),
+}
+CASES.update(ERR_CASES)
 # bench.py streams: config 3, 60 frames (4 warmup + 56 timed).  configs[3]
 # (64 streams, 8 per GPU) uses seeds 100..163: rank r of bench.py --gpus N owns
 # seeds 100 + 8r .. 100 + 8r + 7 (tests/test_gpu_parity.py decodes each shard)
@@ -58,16 +81,19 @@ def one_case(item):
 
     name, (cfg, seed, ov, nr) = item
     stream = gen.generate(cfg, seed, **ov)
-    frames = O.refdec_frames(stream, no_reorder=nr)
+    frames, pics = O.refdec_frames(stream, no_reorder=nr, info=True)
     p = gen.params(cfg, seed, **ov)
     w, h = p.w_mbs * 16, p.h_mbs * 16
     assert frames and all(len(f) == w * h * 3 // 2 for f in frames), name
-    return name, {
+    out = {
         "config": cfg, "seed": seed, "overrides": ov, "no_reorder": nr,
         "stream_bytes": len(stream), "stream_sha256": hashlib.sha256(stream).hexdigest(),
         "width": w, "height": h,
         "frames": [hashlib.md5(f).hexdigest() for f in frames],
     }
+    if name in ERR_CASES:
+        out["pics"] = [list(x) for x in pics]
+    return name, out
 
 
 def main():

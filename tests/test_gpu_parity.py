@@ -54,6 +54,22 @@ def test_swdec_api_vs_reference(name):
     assert md5s(frames) == c["frames"]
 
 
+ERR = [n for n in CASES if "pics" in CASES[n]]
+
+
+@pytest.mark.parametrize("name", ERR)
+def test_swdec_damaged_stream_vs_reference(name):
+    """Damaged streams through H264SwDec* on the GPU: residuals out of range,
+    lost / truncated slices and lost pictures give the reference's frames,
+    picture ids and nbrOfErrMBs (slice un-marking slice_data.c:302-358,
+    concealment conceal.c:125-590: P copies, two-pass neighbour concealment
+    of I pictures, whole-picture grey / copy)."""
+    c = CASES[name]
+    frames, _, pics = swdec_decode(stream(c), no_reorder=c["no_reorder"], info=True)
+    assert [list(p) for p in pics] == c["pics"]
+    assert md5s(frames) == c["frames"]
+
+
 def test_decoder_js_api_holds_reordered_pictures():
     """Decoder.js never flushes (Decoder.c:140): with display reordering the
     emitted pictures are a prefix of the reference output."""

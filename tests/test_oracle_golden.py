@@ -13,10 +13,25 @@ FAST = [n for n in CASES if not n.startswith("bench_")] + ["bench_1080p_s100", "
 @pytest.mark.parametrize("name", FAST)
 def test_oracle_matches_reference(name):
     c = CASES[name]
-    frames, errs, w, h, _ = O.decode(stream(c), no_reorder=c["no_reorder"])
-    assert errs == 0
+    frames, errs, w, h, _, pics = O.decode(stream(c), no_reorder=c["no_reorder"], info=True)
     assert (w, h) == (c["width"], c["height"])
     assert md5s(frames) == c["frames"]
+    if "pics" in c:
+        # damaged stream: same pictures, ids, IDR flags and concealed-MB
+        # counts (nbrOfErrMBs) as the reference decoder printed
+        assert [list(p) for p in pics] == c["pics"]
+        assert errs > 0
+    else:
+        assert errs == 0
+
+
+def test_error_fixtures_exercise_concealment():
+    """The damaged-stream fixtures cover P-copy and neighbour (intra)
+    concealment, whole lost pictures and the I-slice un-marking quirk."""
+    err = {n: c for n, c in CASES.items() if "pics" in c}
+    assert len(err) >= 8
+    assert any(p[2] == c["width"] * c["height"] // 256 for c in err.values() for p in c["pics"])
+    assert all(sum(p[2] for p in c["pics"]) > 0 for c in err.values())
 
 
 def test_fixture_inventory():
