@@ -86,6 +86,7 @@ static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_
             uint8_t b = *p++;
             cnt++;
             if (!b) zeros++;
+            if (b == 3 && zeros == 2) emul = 1;      /* hasEmulation (byte_stream.c:142-145) */
             if (b == 1 && zeros >= 2) {
                 size = cnt - init - zeros - 1;
                 zeros -= zeros < 3 ? zeros : 3;
@@ -98,7 +99,6 @@ static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_
         }
         *read_bytes = size + init + zeros;
         if (invalid) return -1;
-        emul = 1;
     } else {
         size = len;
         *read_bytes = len;

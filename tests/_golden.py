@@ -17,6 +17,12 @@ def stream(case):
     from broadway_amd import gen
     s = gen.generate(case["config"], case["seed"], **case["overrides"])
     assert hashlib.sha256(s).hexdigest() == case["stream_sha256"], "generator drift"
+    if case.get("patch"):          # byte patches recorded with the fixture
+        b = bytearray(s)
+        for off, hexb in case["patch"]:
+            v = bytes.fromhex(hexb)
+            b[off:off + len(v)] = v
+        s = bytes(b)
     return s
 
 

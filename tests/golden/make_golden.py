@@ -65,13 +65,37 @@ ERR_CASES = {
                                          err_range_pct=10, trunc_slice_pct=30, drop_pic_pct=10), False),
     "err_720p_ionly_conceal": (1, 3, dict(nframes=3, drop_slice_pct=30, trunc_slice_pct=30), False),
     "err_1080p_mixed": (3, 300, dict(nframes=8, err_range_pct=20, drop_slice_pct=10, trunc_slice_pct=10), False),
+    # 00 00 02 inside a slice NAL without any 00 00 03 (patched in, see
+    # find_patch): no emulation check, the slice fails to parse instead
+    "err_000002_no_epb": (1, 12, dict(nframes=3, w_mbs=12, h_mbs=6, slices=1), False),
 }
+PATCHED = {"err_000002_no_epb"}
 CASES.update(ERR_CASES)
 # bench.py streams: config 3, 60 frames (4 warmup + 56 timed).  configs[3]
 # (64 streams, 8 per GPU) uses seeds 100..163: rank r of bench.py --gpus N owns
 # seeds 100 + 8r .. 100 + 8r + 7 (tests/test_gpu_parity.py decodes each shard)
 for s in range(100, 164):
     CASES[f"bench_1080p_s{s}"] = (3, s, dict(nframes=60), False)
+
+
+def find_patch(stream: bytes):
+    """A byte patch that puts 00 00 02 inside a slice NAL that has no
+    emulation-prevention byte: the reference then skips the emulation check
+    (byte_stream.c:142-145, 193) and parses the bytes as slice data."""
+    starts = [i for i in range(len(stream) - 3) if stream[i:i + 4] == b"\0\0\0\1"] + [len(stream)]
+    for a, b in zip(starts, starts[1:]):
+        nal = stream[a + 4:b]
+        if (nal[0] & 31) in (1, 5) and b"\0\0\3" not in nal and len(nal) > 200:
+            return [[a + 4 + len(nal) * 3 // 4, "000002"]]
+    raise RuntimeError("no candidate NAL")
+
+
+def apply_patch(stream: bytes, patch) -> bytes:
+    s = bytearray(stream)
+    for off, hexb in patch or []:
+        b = bytes.fromhex(hexb)
+        s[off:off + len(b)] = b
+    return bytes(s)
 
 
 def one_case(item):
@@ -81,16 +105,21 @@ def one_case(item):
 
     name, (cfg, seed, ov, nr) = item
     stream = gen.generate(cfg, seed, **ov)
+    base_sha = hashlib.sha256(stream).hexdigest()
+    patch = find_patch(stream) if name in PATCHED else None
+    stream = apply_patch(stream, patch)
     frames, pics = O.refdec_frames(stream, no_reorder=nr, info=True)
     p = gen.params(cfg, seed, **ov)
     w, h = p.w_mbs * 16, p.h_mbs * 16
     assert frames and all(len(f) == w * h * 3 // 2 for f in frames), name
     out = {
         "config": cfg, "seed": seed, "overrides": ov, "no_reorder": nr,
-        "stream_bytes": len(stream), "stream_sha256": hashlib.sha256(stream).hexdigest(),
+        "stream_bytes": len(stream), "stream_sha256": base_sha,
         "width": w, "height": h,
         "frames": [hashlib.md5(f).hexdigest() for f in frames],
     }
+    if patch:
+        out["patch"] = patch
     if name in ERR_CASES:
         out["pics"] = [list(x) for x in pics]
     return name, out
