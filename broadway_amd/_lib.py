@@ -73,7 +73,8 @@ class GenParams(C.Structure):
         "dbf_idc1_pct", "dbf_idc2_pct", "dbf_off", "num_ref_frames", "cip", "chroma_qp_offset",
         "poc_type", "coef_pct", "level_tail_pct", "mv_jitter", "offpic_pct",
         "log2_max_frame_num", "poc_swap",
-        "err_range_pct", "drop_slice_pct", "trunc_slice_pct", "drop_pic_pct", "gaps_allowed")] + [("seed", C.c_uint64)]
+        "err_range_pct", "drop_slice_pct", "trunc_slice_pct", "drop_pic_pct", "gaps_allowed",
+        "nonref_pct", "ref_mod_pct", "mmco_pct", "lt_idr_pct")] + [("seed", C.c_uint64)]
 
 
 HEADERS_CB = C.CFUNCTYPE(None, C.c_void_p)

@@ -110,7 +110,17 @@ typedef struct Gen {
     PicCtx pc;
     int frame_num;
     int idr_id;
-    int nref;            /* reference frames available */
+    int nref;            /* reference frames available (= nrefs) */
+    /* reference model: what the decoder's DPB holds after each picture
+     * (sliding window / MMCO, H.264 §8.2.5), for valid modification and
+     * marking commands */
+    struct { int frame_num, lt; } refs[16];   /* lt: LongTermFrameIdx, -1 short-term */
+    int nrefs, max_lt;   /* max_lt: MaxLongTermFrameIdx, -1 "no long-term frame indices" */
+    int cur_ref;         /* current picture is a reference picture */
+    int prev_ref;        /* previous picture was a reference picture */
+    Rng mrng;            /* reference-knob decisions */
+    int nops, op[8], opa[8], opb[8];          /* planned MMCO of the current picture */
+    int lt_idr;          /* current IDR: long_term_reference_flag */
     int gmx, gmy;        /* global motion, quarter-pel */
     int poc_lsb;
     Rng erng;            /* damage decisions (err_* / drop_* knobs) */
@@ -610,6 +620,185 @@ static void gen_inter_mb(Gen *g, BitWriter *bw, int cur, int kind, const SliceCf
     }
 }
 
+/* ------------------------------------------------- reference model --- */
+static int max_fn(const Gen *g) { return 1 << (g->p.log2_max_frame_num < 4 ? 4 : g->p.log2_max_frame_num); }
+/* FrameNumWrap of a short-term reference for the current frame_num */
+static int fn_wrap(const Gen *g, int fn) { return fn > g->frame_num ? fn - max_fn(g) : fn; }
+
+static void ref_remove(Gen *g, int i)
+{
+    for (int k = i; k + 1 < g->nrefs; k++) g->refs[k] = g->refs[k + 1];
+    g->nrefs--;
+}
+
+static int find_lt(const Gen *g, int idx)
+{
+    for (int i = 0; i < g->nrefs; i++) if (g->refs[i].lt == idx) return i;
+    return -1;
+}
+
+/* ref_pic_list_modification() of a P slice (§7.3.3.1): 1..3 commands that
+ * move random references to the front, sometimes the same picture twice
+ * (two indices then name one picture: bS must compare pictures) */
+static void write_ref_mod(Gen *g, BitWriter *bw, int nact)
+{
+    if (!g->p.ref_mod_pct || !pct(&g->mrng, g->p.ref_mod_pct) || g->nrefs < 1) { bw_put(bw, 0, 1); return; }
+    bw_put(bw, 1, 1);
+    int ncmd = 1 + rnd(&g->mrng, nact < 3 ? nact : 3);
+    int pred = g->frame_num, last = -1;
+    for (int c = 0; c < ncmd; c++) {
+        int i = (last >= 0 && pct(&g->mrng, 30)) ? last : rnd(&g->mrng, g->nrefs);
+        last = i;
+        if (g->refs[i].lt >= 0) {
+            bw_ue(bw, 2);
+            bw_ue(bw, (uint32_t)g->refs[i].lt);
+        } else {
+            const int M = max_fn(g), t = g->refs[i].frame_num;
+            int down = (pred - t + M) % M, up = (t - pred + M) % M;
+            if (!down) down = M;
+            if (!up) up = M;
+            const int use_up = pct(&g->mrng, 50);
+            bw_ue(bw, use_up ? 1u : 0u);
+            bw_ue(bw, (uint32_t)((use_up ? up : down) - 1));
+            pred = t;
+        }
+    }
+    bw_ue(bw, 3);
+}
+
+/* decide the current picture's reference marking; the commands are written
+ * into every slice header and applied to the model after the picture */
+static void plan_marking(Gen *g, int idr)
+{
+    g->nops = 0;
+    g->lt_idr = idr && g->p.lt_idr_pct && pct(&g->mrng, g->p.lt_idr_pct);
+    if (idr || !g->cur_ref) return;
+    if (!g->p.mmco_pct || !pct(&g->mrng, g->p.mmco_pct)) {
+        /* the sliding window needs a short-term picture to drop when the
+         * buffer is full (a full buffer of long-term pictures leaves no
+         * room, dpb.c:905-940) */
+        int nshort = 0;
+        for (int j = 0; j < g->nrefs; j++) nshort += g->refs[j].lt < 0;
+        if (g->nrefs >= g->p.num_ref_frames && !nshort && g->nrefs) {
+            g->op[0] = 2; g->opa[0] = g->refs[0].lt; g->nops = 1;
+        }
+        return;
+    }
+    struct { int frame_num, lt; } r[16];       /* the model, as the ops leave it */
+    int n = g->nrefs, max_lt = g->max_lt, cur_lt = 0;
+    memcpy(r, g->refs, sizeof(r));
+    /* MMCO 5: everything unused; the next picture has frame_num 1, so this
+     * one must not (the access-unit boundary is found by frame_num) */
+    if (g->p.poc_type == 2 && g->frame_num > 1 && pct(&g->mrng, 8)) {
+        g->op[0] = 5; g->nops = 1;
+        return;
+    }
+    const int want = 1 + rnd(&g->mrng, 3);
+    int n4 = 0;                                          /* at most one MMCO 4 and one MMCO 6 */
+    for (int k = 0; k < 8 && g->nops < want && !cur_lt; k++) {
+        const int pick = 1 + rnd(&g->mrng, 5);            /* 1,2,3,4 and 5 -> MMCO 6 */
+        const int m = g->nops;
+        int cs[16], ns = 0, cl[16], nl = 0;
+        for (int j = 0; j < n; j++) { if (r[j].lt < 0) cs[ns++] = j; else cl[nl++] = j; }
+        if (pick == 1 && ns) {
+            const int i = cs[rnd(&g->mrng, ns)];
+            g->op[m] = 1; g->opa[m] = g->frame_num - fn_wrap(g, r[i].frame_num) - 1;
+            r[i] = r[--n];
+        } else if (pick == 2 && nl) {
+            const int i = cl[rnd(&g->mrng, nl)];
+            g->op[m] = 2; g->opa[m] = r[i].lt;
+            r[i] = r[--n];
+        } else if (pick == 3 && ns && max_lt >= 0) {
+            const int fnum = r[cs[rnd(&g->mrng, ns)]].frame_num;
+            const int idx = rnd(&g->mrng, max_lt + 1);
+            g->op[m] = 3; g->opa[m] = g->frame_num - fn_wrap(g, fnum) - 1; g->opb[m] = idx;
+            for (int j = 0; j < n; j++) if (r[j].lt == idx) { r[j] = r[--n]; break; }
+            for (int j = 0; j < n; j++) if (r[j].lt < 0 && r[j].frame_num == fnum) { r[j].lt = idx; break; }
+        } else if (pick == 4 && !n4++) {
+            const int v = rnd(&g->mrng, (g->p.num_ref_frames < 3 ? g->p.num_ref_frames : 3) + 1);   /* max_long_term_frame_idx_plus1 */
+            g->op[m] = 4; g->opa[m] = v;
+            max_lt = v - 1;
+            for (int j = 0; j < n;) { if (r[j].lt >= 0 && r[j].lt > max_lt) r[j] = r[--n]; else j++; }
+        } else if (pick == 5 && max_lt >= 0) {
+            const int idx = rnd(&g->mrng, max_lt + 1);
+            int nn = n;
+            for (int j = 0; j < nn; j++) if (r[j].lt == idx) { nn--; break; }
+            if (nn >= g->p.num_ref_frames) continue;     /* no room for the current picture */
+            for (int j = 0; j < n; j++) if (r[j].lt == idx) { r[j] = r[--n]; break; }
+            g->op[m] = 6; g->opa[m] = idx;
+            cur_lt = 1;                                  /* MMCO 6 last */
+        } else {
+            continue;
+        }
+        g->nops++;
+    }
+    /* the current picture needs a free place: adaptive marking has no
+     * sliding window (dpb.c:784-801) */
+    if (!cur_lt && n >= g->p.num_ref_frames) {
+        int i = -1, best = 0;
+        for (int j = 0; j < n; j++)
+            if (r[j].lt < 0 && (i < 0 || fn_wrap(g, r[j].frame_num) < best)) { i = j; best = fn_wrap(g, r[j].frame_num); }
+        if (i >= 0) { g->op[g->nops] = 1; g->opa[g->nops] = g->frame_num - best - 1; }
+        else { g->op[g->nops] = 2; g->opa[g->nops] = r[0].lt; }
+        g->nops++;
+    }
+}
+
+/* apply the current picture's marking to the model (after its slices) */
+static void apply_marking(Gen *g, int idr)
+{
+    if (!g->cur_ref) return;
+    if (idr) {
+        g->nrefs = 1;
+        g->refs[0].frame_num = 0;
+        g->refs[0].lt = g->lt_idr ? 0 : -1;
+        g->max_lt = g->lt_idr ? 0 : -1;
+        return;
+    }
+    int cur_lt = -1, fn = g->frame_num;
+    if (g->nops) {
+        for (int k = 0; k < g->nops; k++) {
+            const int op = g->op[k];
+            if (op == 1 || op == 3) {
+                const int pn = g->frame_num - (g->opa[k] + 1);
+                for (int j = 0; j < g->nrefs; j++)
+                    if (g->refs[j].lt < 0 && fn_wrap(g, g->refs[j].frame_num) == pn) {
+                        if (op == 1) { ref_remove(g, j); break; }
+                        const int o = find_lt(g, g->opb[k]);
+                        if (o >= 0) { ref_remove(g, o); if (o < j) j--; }
+                        g->refs[j].lt = g->opb[k];
+                        break;
+                    }
+            } else if (op == 2) {
+                const int o = find_lt(g, g->opa[k]);
+                if (o >= 0) ref_remove(g, o);
+            } else if (op == 4) {
+                g->max_lt = g->opa[k] - 1;
+                for (int j = 0; j < g->nrefs;) { if (g->refs[j].lt >= 0 && g->refs[j].lt > g->max_lt) ref_remove(g, j); else j++; }
+            } else if (op == 5) {
+                g->nrefs = 0;
+                g->max_lt = -1;
+                fn = 0;
+            } else if (op == 6) {
+                const int o = find_lt(g, g->opa[k]);
+                if (o >= 0) ref_remove(g, o);
+                cur_lt = g->opa[k];
+            }
+        }
+    } else if (g->nrefs >= g->p.num_ref_frames) {
+        /* sliding window: the short-term with the smallest FrameNumWrap */
+        int i = -1;
+        for (int j = 0; j < g->nrefs; j++)
+            if (g->refs[j].lt < 0 && (i < 0 || fn_wrap(g, g->refs[j].frame_num) < fn_wrap(g, g->refs[i].frame_num))) i = j;
+        if (i >= 0) ref_remove(g, i);
+    }
+    if (g->nrefs < 16) {
+        g->refs[g->nrefs].frame_num = fn;
+        g->refs[g->nrefs].lt = cur_lt;
+        g->nrefs++;
+    }
+}
+
 static void gen_slice(Gen *g, int idr, int first, int last, const SliceCfg *sc)
 {
     const GenParams *p = &g->p;
@@ -624,10 +813,21 @@ static void gen_slice(Gen *g, int idr, int first, int last, const SliceCfg *sc)
         int override = sc->nref_active != p->num_ref_frames;
         bw_put(&bw, (uint32_t)override, 1);
         if (override) bw_ue(&bw, (uint32_t)(sc->nref_active - 1));
-        bw_put(&bw, 0, 1);         /* ref_pic_list_modification_flag_l0 */
+        write_ref_mod(g, &bw, sc->nref_active);
     }
-    if (idr) { bw_put(&bw, 0, 1); bw_put(&bw, 0, 1); }
-    else bw_put(&bw, 0, 1);        /* adaptive_ref_pic_marking_mode_flag */
+    if (g->cur_ref) {               /* dec_ref_pic_marking() */
+        if (idr) { bw_put(&bw, 0, 1); bw_put(&bw, (uint32_t)g->lt_idr, 1); }
+        else {
+            bw_put(&bw, g->nops > 0, 1);    /* adaptive_ref_pic_marking_mode_flag */
+            for (int i = 0; i < g->nops; i++) {
+                const int op = g->op[i];
+                bw_ue(&bw, (uint32_t)op);
+                if (op == 1 || op == 3 || op == 2 || op == 6 || op == 4) bw_ue(&bw, (uint32_t)g->opa[i]);
+                if (op == 3) bw_ue(&bw, (uint32_t)g->opb[i]);
+            }
+            if (g->nops > 0) bw_ue(&bw, 0);
+        }
+    }
     bw_se(&bw, sc->qp - 26);
     bw_ue(&bw, (uint32_t)sc->idc);
     if (sc->idc != 1) { bw_se(&bw, sc->offa); bw_se(&bw, sc->offb); }
@@ -676,7 +876,7 @@ static void gen_slice(Gen *g, int idr, int first, int last, const SliceCfg *sc)
     if (emit && p->drop_slice_pct && pct(&g->erng, p->drop_slice_pct)) emit = 0;
     if (emit && p->trunc_slice_pct && pct(&g->erng, p->trunc_slice_pct) && bw.nbytes > 4)
         bw.nbytes = (size_t)rnd_range(&g->erng, 2, (int)bw.nbytes - 1);
-    if (emit) emit_nal(&g->out, idr ? 3 : 2, idr ? 5 : 1, &bw);
+    if (emit) emit_nal(&g->out, idr ? 3 : g->cur_ref ? 2 : 0, idr ? 5 : 1, &bw);
     bw_free(&bw);
 }
 
@@ -691,8 +891,13 @@ static void gen_picture(Gen *g, int idx)
         write_pps(g);
         g->frame_num = 0;
         g->nref = 0;
+        g->nrefs = 0;
         g->poc_lsb = 0;
     }
+    /* non-reference pictures: never two in a row with POC type 2 (equal
+     * picture order counts) */
+    g->cur_ref = idr || !p->nonref_pct || (p->poc_type == 2 && !g->prev_ref) || !pct(&g->mrng, p->nonref_pct);
+    plan_marking(g, idr);
     {   /* display order: 2 * index in GOP, optionally swapped in pairs */
         int k = idx % p->gop, d = k;
         int last = p->gop - 1;
@@ -716,21 +921,29 @@ static void gen_picture(Gen *g, int idx)
         if (last < first) last = first;
         if (last > nmb - 1 - (ns - 1 - s)) last = nmb - 1 - (ns - 1 - s);
         SliceCfg sc;
-        sc.is_p = !idr && g->nref > 0;
+        sc.is_p = !idr && g->nrefs > 0;
         sc.qp = rnd_range(&g->rng, p->qp_min, p->qp_max);
         int u = rnd(&g->rng, 100);
         sc.idc = u < p->dbf_idc1_pct ? 1 : (u < p->dbf_idc1_pct + p->dbf_idc2_pct ? 2 : 0);
         sc.offa = rnd_range(&g->rng, -p->dbf_off, p->dbf_off);
         sc.offb = rnd_range(&g->rng, -p->dbf_off, p->dbf_off);
-        sc.nref_active = g->nref < p->num_ref_frames ? g->nref : p->num_ref_frames;
+        sc.nref_active = g->nrefs < p->num_ref_frames ? g->nrefs : p->num_ref_frames;
         if (sc.nref_active < 1) sc.nref_active = 1;
         sc.tag = (uint16_t)s;
         gen_slice(g, idr, first, last, &sc);
         first = last + 1;
     }
     if (idr) g->idr_id = (g->idr_id + 1) & 0xFFFF;
-    g->frame_num = (g->frame_num + 1) & ((1 << p->log2_max_frame_num) - 1);
-    if (g->nref < p->num_ref_frames) g->nref++;
+    apply_marking(g, idr);
+    g->nref = g->nrefs;
+    /* frame_num: previous reference picture's + 1 (after MMCO 5 that
+     * picture counts as frame_num 0) */
+    if (g->cur_ref) {
+        int mm5 = 0;
+        for (int k = 0; k < g->nops; k++) mm5 |= g->op[k] == 5;
+        g->frame_num = ((mm5 ? 0 : g->frame_num) + 1) & ((1 << p->log2_max_frame_num) - 1);
+    }
+    g->prev_ref = g->cur_ref;
 }
 
 int h264gen_generate(const GenParams *p, uint8_t **out, size_t *out_len)
@@ -743,6 +956,9 @@ int h264gen_generate(const GenParams *p, uint8_t **out, size_t *out_len)
     if (g.p.log2_max_frame_num < 4) g.p.log2_max_frame_num = 4;
     g.rng.s = p->seed * 0x2545F4914F6CDD1Dull + 0x1234567ull;
     g.erng.s = p->seed * 0x9E3779B97F4A7C15ull + 0xE770Cull;
+    g.mrng.s = p->seed * 0xD6E8FEB86659FD93ull + 0x3EF5ull;
+    g.max_lt = -1;
+    g.prev_ref = 1;
     g.range_mb = -1;
     g.pc.w = p->w_mbs; g.pc.h = p->h_mbs; g.pc.cip = p->cip;
     g.pc.mb = (MbInfo *)calloc((size_t)p->w_mbs * p->h_mbs, sizeof(MbInfo));

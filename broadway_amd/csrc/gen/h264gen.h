@@ -46,6 +46,13 @@ typedef struct GenParams {
     int trunc_slice_pct;           /* per slice: NAL payload cut at a random byte */
     int drop_pic_pct;              /* per non-IDR picture: none of its NALs emitted */
     int gaps_allowed;              /* SPS gaps_in_frame_num_value_allowed_flag */
+    /* reference-picture knobs (RefPicList0 modification, MMCO, long-term,
+     * non-reference pictures; dpb.c / h264bsd_dpb.c paths).  All 0 leaves
+     * the stream byte-identical; decisions come from a third RNG. */
+    int nonref_pct;                /* per non-IDR picture: nal_ref_idc = 0 */
+    int ref_mod_pct;               /* per P slice: ref_pic_list_modification commands */
+    int mmco_pct;                  /* per non-IDR reference picture: adaptive marking (MMCO 1-4, 6; 5 with POC type 2) */
+    int lt_idr_pct;                /* per IDR: long_term_reference_flag */
     uint64_t seed;
 } GenParams;
 

@@ -97,7 +97,9 @@ static void finish_rec(PicBuild *pb, int cur, const SliceHdr *sh, const Pps *pps
     r->qpc = kQpChroma[clip3(0, 51, r->qp + pps->chroma_qp_offset)];
     r->slice = tag;
     r->dbf = 0;
-    r->rsv0 = 0;
+    r->refidx = 0;
+    if (r->type == MBT_INTER)
+        for (int i = 0; i < 4; i++) r->refidx |= (uint16_t)((pc->mb[cur].refidx[i] & 15) << (4 * i));
 }
 
 /* The prediction-stage checks of h264bsdDecodeMacroblock that fail an MB:

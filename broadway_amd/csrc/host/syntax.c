@@ -255,32 +255,48 @@ int parse_slice_header(BitReader *br, const NalHdr *nal, const Sps *sps, const P
                 if (idc == 3) break;
                 h->ref_mod[i].val = br_ue(br);
                 if (br->err) return -1;
+                /* abs_diff_pic_num_minus1 < MaxPicNum (slice_header.c:RefPicListReordering) */
+                if (idc < 2 && h->ref_mod[i].val >= (uint32_t)(1u << sps->log2_max_frame_num)) return -1;
                 i++;
             }
             if (i == 0) return -1;
         }
     }
     if (nal->ref_idc) {
+        /* dec_ref_pic_marking() with the reference's checks (slice_header.c
+         * DecRefPicMarking): long-term IDR needs reference frames, at most
+         * 2 * num_ref_frames + 3 operations, max_long_term_frame_idx_plus1
+         * <= num_ref_frames, one each of MMCO 4, 5, 6, no MMCO 5 with 1-3 */
         if (idr) {
             h->no_output_prior = (int)br_u1(br);
             h->long_term_ref = (int)br_u1(br);
+            if (!sps->num_ref_frames && h->long_term_ref) return -1;
         } else {
             h->adaptive_marking = (int)br_u1(br);
             if (h->adaptive_marking) {
-                int i = 0;
+                int i = 0, n4 = 0, n5 = 0, n6 = 0, n13 = 0;
                 for (;;) {
+                    if (i > 2 * sps->num_ref_frames + 2 || i >= 65) return -1;
                     uint32_t op = br_ue(br);
-                    if (op > 6 || i >= 65) return -1;
+                    if (br->err || op > 6) return -1;
                     h->mmco[i].op = (int)op;
                     if (op == 0) break;
                     if (op == 1 || op == 3) h->mmco[i].diff = br_ue(br) + 1;
                     if (op == 2) h->mmco[i].lt_pic_num = br_ue(br);
                     if (op == 3 || op == 6) h->mmco[i].lt_idx = br_ue(br);
-                    if (op == 4) h->mmco[i].max_lt_idx = br_ue(br);
+                    if (op == 4) {
+                        h->mmco[i].max_lt_idx = br_ue(br);
+                        if (h->mmco[i].max_lt_idx > (uint32_t)sps->num_ref_frames) return -1;
+                        n4++;
+                    }
                     if (br->err) return -1;
+                    n5 += op == 5;
+                    n6 += op == 6;
+                    n13 += op <= 3;
                     i++;
                 }
                 h->nmmco = i;
+                if (n4 > 1 || n5 > 1 || n6 > 1 || (n13 && n5)) return -1;
             }
         }
     }

@@ -74,7 +74,9 @@ typedef struct MbRec {
     uint8_t  ref[4];    /* DPB slot per 8x8 partition (inter only) */
     int16_t  mv[16][2]; /* per 4x4 block, z-scan, quarter-pel (x, y) */
     uint16_t slice;     /* slice id within the picture */
-    uint16_t rsv0;
+    uint16_t refidx;    /* RefPicList0 index per 8x8 partition, 4 bits each (inter only).
+                           Informational: bS compares the pictures (ref slots), not the
+                           indices (deblocking.c:348, 402); two indices can name one picture */
 } MbRec;
 
 #ifdef __cplusplus

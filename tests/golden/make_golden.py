@@ -71,6 +71,25 @@ ERR_CASES = {
 }
 PATCHED = {"err_000002_no_epb"}
 CASES.update(ERR_CASES)
+# Reference-picture management (generator knobs ref_mod_pct / mmco_pct /
+# lt_idr_pct / nonref_pct): RefPicList0 modification incl. two indices naming
+# one picture (bS compares pictures, deblocking.c:348, 402), MMCO 1-6,
+# long-term pictures, non-reference pictures, gaps (dpb.c:224-1350).
+REF_CASES = {
+    "ref_mod_alias_12x8": (2, 3, dict(nframes=10, w_mbs=12, h_mbs=8, crop_bottom=0, slices=2, gop=10,
+                                      num_ref_frames=4, ref_mod_pct=90, mv_jitter=2), False),
+    "ref_mmco_lt_12x8": (2, 22, dict(nframes=30, w_mbs=12, h_mbs=8, crop_bottom=0, slices=2, gop=15,
+                                     num_ref_frames=4, log2_max_frame_num=4, mmco_pct=60, lt_idr_pct=100,
+                                     ref_mod_pct=40), False),
+    "ref_mmco_poc0_reorder": (2, 22, dict(nframes=24, w_mbs=10, h_mbs=6, crop_bottom=0, slices=2, gop=12,
+                                          num_ref_frames=3, poc_type=0, poc_swap=1, mmco_pct=50,
+                                          nonref_pct=30, lt_idr_pct=50, ref_mod_pct=40), False),
+    "ref_nonref_gaps_poc0": (2, 23, dict(nframes=24, w_mbs=10, h_mbs=6, crop_bottom=0, slices=2, gop=12,
+                                         num_ref_frames=3, poc_type=0, poc_swap=1, nonref_pct=40,
+                                         drop_pic_pct=20, gaps_allowed=1), False),
+    "ref_all_1080p": (3, 400, dict(nframes=16, ref_mod_pct=50, mmco_pct=40, lt_idr_pct=50, nonref_pct=20), False),
+}
+CASES.update(REF_CASES)
 # bench.py streams: config 3, 60 frames (4 warmup + 56 timed).  configs[3]
 # (64 streams, 8 per GPU) uses seeds 100..163: rank r of bench.py --gpus N owns
 # seeds 100 + 8r .. 100 + 8r + 7 (tests/test_gpu_parity.py decodes each shard)
@@ -120,7 +139,7 @@ def one_case(item):
     }
     if patch:
         out["patch"] = patch
-    if name in ERR_CASES:
+    if name in ERR_CASES or name in REF_CASES:
         out["pics"] = [list(x) for x in pics]
     return name, out
 

@@ -54,16 +54,19 @@ def test_swdec_api_vs_reference(name):
     assert md5s(frames) == c["frames"]
 
 
-ERR = [n for n in CASES if "pics" in CASES[n]]
+PICS = [n for n in CASES if "pics" in CASES[n]]
 
 
-@pytest.mark.parametrize("name", ERR)
-def test_swdec_damaged_stream_vs_reference(name):
-    """Damaged streams through H264SwDec* on the GPU: residuals out of range,
-    lost / truncated slices and lost pictures give the reference's frames,
-    picture ids and nbrOfErrMBs (slice un-marking slice_data.c:302-358,
-    concealment conceal.c:125-590: P copies, two-pass neighbour concealment
-    of I pictures, whole-picture grey / copy)."""
+@pytest.mark.parametrize("name", PICS)
+def test_swdec_damaged_and_refpic_streams_vs_reference(name):
+    """Through H264SwDec* on the GPU, every output picture, picture id, IDR
+    flag and nbrOfErrMBs equals the reference decoder's:
+    err_*: residuals out of range, lost / truncated slices, lost pictures
+    (slice un-marking slice_data.c:302-358, concealment conceal.c:125-590:
+    P copies, two-pass neighbour concealment of I pictures, whole-picture
+    grey / copy);  ref_*: RefPicList0 modification with aliased indices, MMCO
+    1-6, long-term and non-reference pictures, gaps in frame_num
+    (dpb.c:224-1350, deblocking.c:348, 402)."""
     c = CASES[name]
     frames, _, pics = swdec_decode(stream(c), no_reorder=c["no_reorder"], info=True)
     assert [list(p) for p in pics] == c["pics"]

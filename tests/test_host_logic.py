@@ -15,7 +15,7 @@ CASES = cases()
 
 REC_DT = np.dtype([("type", "u1"), ("qp", "u1"), ("qpc", "u1"), ("avail", "u1"), ("pred", "u1"),
                    ("dbf", "u1"), ("offA", "i1"), ("offB", "i1"), ("cbits", "<u4"), ("coef", "<u4"),
-                   ("i4", "u1", 8), ("ref", "u1", 4), ("mv", "<i2", 32), ("slice", "<u2"), ("rsv", "<u2")])
+                   ("i4", "u1", 8), ("ref", "u1", 4), ("mv", "<i2", 32), ("slice", "<u2"), ("refidx", "<u2")])
 
 
 def test_record_layout():
@@ -79,3 +79,125 @@ def test_oracle_no_reorder_changes_order_only():
     a = CASES["poc0_reorder"]["frames"]
     b = CASES["poc0_noreorder"]["frames"]
     assert sorted(a) == sorted(b) and a != b
+
+
+# ---- reference-picture management coverage (fixtures ref_*) ---------------
+_BX = [0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3]
+_BY = [0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3]
+_ZB = {(_BX[b], _BY[b]): b for b in range(16)}
+
+
+def _aliased_edges(cap):
+    """Filtered 4x4 edges between two inter blocks without coefficients and
+    with motion vectors < 1 pel apart whose RefPicList0 indices differ but
+    name the same picture: bS is 0 by pictures (deblocking.c:348, 402) and
+    would be 1 by indices."""
+    n = 0
+    for i in range(cap.npics):
+        r = np.frombuffer(cap.records_bytes(i), dtype=REC_DT)
+        for m in range(r.shape[0]):
+            q = r[m]
+            if q["type"] > 1 or q["dbf"] & 1:
+                continue
+            for d in (0, 1):
+                for e in range(4):
+                    if (e == 0 and not q["avail"] & (16 if d == 0 else 32)) or (e > 0 and not q["avail"] & 64):
+                        continue
+                    for k in range(4):
+                        bq = _ZB[(e, k)] if d == 0 else _ZB[(k, e)]
+                        if e == 0:
+                            p = r[m - 1] if d == 0 else r[m - cap.w_mbs]
+                            bp = _ZB[(3, k)] if d == 0 else _ZB[(k, 3)]
+                        else:
+                            p, bp = q, (_ZB[(e - 1, k)] if d == 0 else _ZB[(k, e - 1)])
+                        if p["type"] > 1 or p["dbf"] & 1 or (p["cbits"] >> bp) & 1 or (q["cbits"] >> bq) & 1:
+                            continue
+                        if p["ref"][bp >> 2] != q["ref"][bq >> 2]:
+                            continue
+                        if (abs(int(p["mv"][2 * bp]) - int(q["mv"][2 * bq])) >= 4 or
+                                abs(int(p["mv"][2 * bp + 1]) - int(q["mv"][2 * bq + 1])) >= 4):
+                            continue
+                        ip = (int(p["refidx"]) >> (4 * (bp >> 2))) & 15 if p["type"] == 0 else 0
+                        iq = (int(q["refidx"]) >> (4 * (bq >> 2))) & 15 if q["type"] == 0 else 0
+                        n += ip != iq
+    return n
+
+
+def test_aliased_reference_indices_reach_deblocking():
+    """ref_mod_alias_12x8 (GPU-tested against the reference MD5s) has edges
+    whose bS depends on comparing pictures rather than ref_idx."""
+    cap = Capture(stream(CASES["ref_mod_alias_12x8"]))
+    assert cap.errors == 0
+    assert _aliased_edges(cap) >= 10
+
+
+def _marking_ops(s, log2_fn, poc_type, nref_default):
+    """dec_ref_pic_marking() / modification commands of every slice header of
+    a generated stream (syntax §7.3.3; PPS values as the generator writes)."""
+    ops, cmds, lt_idr = [], [], 0
+    for nal in split_annexb(s):
+        body = nal[nal.index(b"\1") + 1:]
+        t, ref = body[0] & 31, (body[0] >> 5) & 3
+        if t not in (1, 5):
+            continue
+        raw = body[1:].replace(b"\0\0\3", b"\0\0")
+        bits = "".join(f"{b:08b}" for b in raw)
+        pos = [0]
+
+        def u(n):
+            v = int(bits[pos[0]:pos[0] + n] or "0", 2)
+            pos[0] += n
+            return v
+
+        def ue():
+            z = 0
+            while bits[pos[0]] == "0":
+                z += 1
+                pos[0] += 1
+            pos[0] += 1
+            return (1 << z) - 1 + u(z)
+
+        ue()
+        st = ue() % 5
+        ue()
+        u(log2_fn)
+        if t == 5:
+            ue()
+        if poc_type == 0:
+            u(8)
+        if st == 0:
+            if u(1):
+                ue()
+            if u(1):
+                while True:
+                    c = ue()
+                    if c == 3:
+                        break
+                    cmds.append((c, ue()))
+        if ref:
+            if t == 5:
+                u(1)
+                lt_idr += u(1)
+            elif u(1):
+                while True:
+                    op = ue()
+                    if op == 0:
+                        break
+                    ops.append(op)
+                    if op in (1, 2, 3, 4, 6):
+                        ue()
+                    if op == 3:
+                        ue()
+    return ops, cmds, lt_idr
+
+
+def test_reference_management_fixtures_cover_every_operation():
+    c = CASES["ref_mmco_lt_12x8"]
+    ops, cmds, lt_idr = _marking_ops(stream(c), 4, 2, 4)
+    assert set(ops) == {1, 2, 3, 4, 5, 6} and lt_idr > 0
+    assert {0, 1, 2} <= {k for k, _ in cmds}
+    c = CASES["ref_mmco_poc0_reorder"]
+    ops, cmds, lt_idr = _marking_ops(stream(c), 8, 0, 3)
+    assert {1, 2, 3, 4, 6} <= set(ops)
+    nals = split_annexb(stream(CASES["ref_nonref_gaps_poc0"]))
+    assert any((n[n.index(b"\1") + 1] >> 5) & 3 == 0 and n[n.index(b"\1") + 1] & 31 == 1 for n in nals)
