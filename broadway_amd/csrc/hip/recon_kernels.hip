@@ -147,13 +147,27 @@ __device__ __forceinline__ int blk_of(int x4, int y4) { return ((y4 >> 1) * 2 + 
 
 // ---------------------------------------------------------------------------
 // residual: dequant + inverse transforms (transform.c:94-398) for one MB.
-// res: LDS int16[384] (luma 16x16 raster, Cb 8x8, Cr 8x8). dc: LDS int32[24].
+// Residual hand-off k_prep -> k_wgpp, compact: only the 4x4 blocks that can
+// carry a residual travel, 32 B each, in cbits bit order, from the start of
+// the MB's 768-B slot.  res_mask: AC-coded blocks plus every block of a plane
+// whose DC transform is coded (I16 luma DC, chroma DC of that plane).
+__device__ __forceinline__ uint32_t res_mask(int type, uint32_t cbits)
+{
+    uint32_t m = cbits & 0xFFFFFFu;
+    if (type == MBT_I16 && ((cbits >> 24) & 1)) m |= 0xFFFFu;
+    if ((cbits >> 25) & 1) m |= 0xF0000u;
+    if ((cbits >> 26) & 1) m |= 0xF00000u;
+    return m;
+}
+
+// res: the MB's compact residual slot (global, res_mask blocks in bit order,
+// 16 raster int16 each).  dc: LDS int32[24].
 // Returns (through *err) a nonzero flag if a sample leaves [-512,511].
 // ---------------------------------------------------------------------------
 // base: the MB's coded blocks in cbits order (staged in LDS by the caller).
 // ls: the levelScale register table (Tabs::ls).
 __device__ void mb_residual(const MbRec &r, const int16_t *base, int16_t *res,
-                            int32_t *dc, int lane, int *range_err, uint32_t ls)
+                            int32_t *dc, int lane, int *range_err, uint32_t ls, uint32_t m)
 {
     const uint32_t cb = r.cbits;
     const bool i16 = r.type == MBT_I16;
@@ -254,18 +268,17 @@ __device__ void mb_residual(const MbRec &r, const int16_t *base, int16_t *res,
 #pragma unroll
             for (int i = 0; i < 16; i++) o[i] = 0;
         }
-        if (luma) {
-            const int bx = blk_x(lane) * 4, by = blk_y(lane) * 4;
+        // compact hand-off: the block's 16 samples (raster) at its rank
+        // among the MB's res_mask blocks, 32 B straight from registers
+        if ((m >> lane) & 1) {
+            uint32_t w[8];
 #pragma unroll
-            for (int i = 0; i < 16; i++) res[(by + (i >> 2)) * 16 + bx + (i & 3)] = (int16_t)o[i];
-        } else {
-            const int comp = (lane - 16) >> 2, b = (lane - 16) & 3;
-            const int bx = (b & 1) * 4, by = (b >> 1) * 4;
-#pragma unroll
-            for (int i = 0; i < 16; i++) res[256 + comp * 64 + (by + (i >> 2)) * 8 + bx + (i & 3)] = (int16_t)o[i];
+            for (int i = 0; i < 8; i++) w[i] = ((uint32_t)o[2 * i] & 0xFFFFu) | ((uint32_t)o[2 * i + 1] << 16);
+            uint4 *q = (uint4 *)(res + __popc(m & ((1u << lane) - 1)) * 16);
+            q[0] = make_uint4(w[0], w[1], w[2], w[3]);
+            q[1] = make_uint4(w[4], w[5], w[6], w[7]);
         }
     }
-    wave_sync();
 }
 
 // ---------------------------------------------------------------------------
@@ -529,7 +542,7 @@ struct PrepArgs {
     int w, h;
 };
 
-__device__ __forceinline__ void prep_mb(const PrepArgs &a, int gidx, int lane, McScratch &Mw, int16_t *s_res,
+__device__ __forceinline__ void prep_mb(const PrepArgs &a, int gidx, int lane, McScratch &Mw,
                                         uint8_t *s_db, const Tabs &T)
 {
     const int nmbs = a.w * a.h;
@@ -566,10 +579,8 @@ __device__ __forceinline__ void prep_mb(const PrepArgs &a, int gidx, int lane, M
         if (lane + 128 < ncw) Mw.coef[lane + 128] = cq2;
         if (lane + 192 < ncw) Mw.coef[lane + 192] = cq3;
         wave_sync();
-        mb_residual(r, (const int16_t *)Mw.coef, s_res, Mw.dc, lane, &e, T.ls);
-        const uint32_t *src = (const uint32_t *)s_res;
-        uint32_t *dst = (uint32_t *)(a.res + (size_t)gmb * 384);
-        dst[lane] = src[lane]; dst[64 + lane] = src[64 + lane]; dst[128 + lane] = src[128 + lane];
+        mb_residual(r, (const int16_t *)Mw.coef, a.res + (size_t)gmb * 384, Mw.dc, lane, &e, T.ls,
+                    res_mask(rtype, rcbits));
     }
     const int any_e = __builtin_amdgcn_ballot_w64(e != 0) != 0;
     if (lane < 16) {
@@ -583,13 +594,12 @@ __device__ __forceinline__ void prep_mb(const PrepArgs &a, int gidx, int lane, M
 __global__ __launch_bounds__(256) void k_prep(PrepArgs a)
 {
     __shared__ McScratch M[4];
-    __shared__ int16_t s_res[4][384];
     __shared__ uint8_t s_db[4][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int gidx = blockIdx.x * 4 + wv;
     if (gidx >= a.nmbs_total) return;            // wave-uniform; no workgroup barrier follows
     const Tabs T = load_tabs(lane);
-    prep_mb(a, gidx, lane, M[wv], s_res[wv], s_db[wv], T);
+    prep_mb(a, gidx, lane, M[wv], s_db[wv], T);
 }
 
 // ---------------------------------------------------------------------------
@@ -1455,7 +1465,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 // ---------------------------------------------------------------------------
 struct McLoad {
     uint32_t lw[3][3], cw[3][2];     // reference windows (luma rows lsub+4k, chroma rows)
-    uint32_t dbw, r0, r1, r2;        // k_prep outputs
+    uint32_t dbw, r0, r1, r2, r3;    // k_prep outputs (r*: half a residual block, lanes 0..47)
     int l_x0, l_ax, c_x0, c_ax;      // window geometry (per lane)
 };
 
@@ -1508,10 +1518,14 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
         }
     }
     L.dbw = ldg32(pdb, (uint32_t)(lane & 15) * 4);
-    L.r0 = L.r1 = L.r2 = 0;
-    if (has_res) {      // residual dwords 3*lane .. 3*lane+2: one dwordx3 load
-        const uint3 t = *(const uint3 *)(a.res + (size_t)gmb * 384 + lane * 6);
-        L.r0 = t.x; L.r1 = t.y; L.r2 = t.z;
+    L.r0 = L.r1 = L.r2 = L.r3 = 0;
+    // lane 2b + h (< 48) takes rows 2h, 2h+1 of block bit b: 16 B of the
+    // compact residual (one dwordx4 load), zero if the block has none
+    const int rb = lane >> 1;
+    if (has_res && lane < 48 && ((res_mask(rtype, cbits) >> rb) & 1)) {
+        const int k = __popc(res_mask(rtype, cbits) & ((1u << rb) - 1));
+        const uint4 t = *(const uint4 *)(a.res + (size_t)gmb * 384 + (k * 2 + (lane & 1)) * 8);
+        L.r0 = t.x; L.r1 = t.y; L.r2 = t.z; L.r3 = t.w;
     }
 }
 
@@ -1525,9 +1539,14 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     if (lane < 24) M.srec[lane] = v0;
     if (lane < 16) ((uint32_t *)db)[lane] = L.dbw;
     if (lane == 15 && (L.dbw >> 24)) atomicOr(a.err + p, 1u);        // k_prep's range-error byte
-    if (has_res || rtype < MBT_I4x4) {
-        uint32_t *d = (uint32_t *)s_res + 3 * lane;
-        d[0] = L.r0; d[1] = L.r1; d[2] = L.r2;
+    if ((has_res || rtype < MBT_I4x4) && lane < 48) {
+        const int b = lane >> 1, h = lane & 1;
+        uint32_t *d = (uint32_t *)s_res;
+        const int o = b < 16 ? (blk_y(b) * 4 + h * 2) * 8 + blk_x(b) * 2
+                             : 128 + ((b - 16) >> 2) * 32 + ((((b - 16) >> 1) & 1) * 4 + h * 2) * 4 + (b & 1) * 2;
+        const int st = b < 16 ? 8 : 4;
+        *(uint2 *)(d + o) = make_uint2(L.r0, L.r1);
+        *(uint2 *)(d + o + st) = make_uint2(L.r2, L.r3);
     }
     if (rtype >= MBT_I4x4) { wave_sync(); return rtype; }
     const int W16 = a.w * 16, CW = W16 / 2;
@@ -1626,7 +1645,7 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
     const Tabs T = load_tabs(lane);
     const int t = blockIdx.x - a.S * a.h;
     for (int g = t * NMC + wid; g < pa.nmbs_total; g += a.prep_wgs * NMC)
-        prep_mb(pa, g, lane, M[wid], R.res[wid], R.db[wid], T);
+        prep_mb(pa, g, lane, M[wid], R.db[wid], T);
 }
 
 template <int NMC, bool PROF, bool PREP>
