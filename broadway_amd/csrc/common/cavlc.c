@@ -6,7 +6,14 @@
 
 int cavlc_decode_block(BitReader *br, int nC, int maxcoef, int16_t *coef)
 {
+    uint32_t sum;
+    return cavlc_decode_block_sum(br, nC, maxcoef, coef, &sum);
+}
+
+int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, uint32_t *abs_sum)
+{
     int len;
+    *abs_sum = 0;
     memset(coef, 0, sizeof(int16_t) * (size_t)maxcoef);
     int sym = vlc_decode(&gCoeffTokenDec[coeff_token_class(nC)], br_peek(br, 16), &len);
     if (sym < 0) return -1;
@@ -20,6 +27,7 @@ int cavlc_decode_block(BitReader *br, int nC, int maxcoef, int16_t *coef)
     for (int i = 0; i < tc; i++) {
         if (i < t1) {
             level[i] = br_u1(br) ? -1 : 1;
+            ++*abs_sum;
             continue;
         }
         /* level_prefix: leading zero bits then a one (§9.2.2.1) */
@@ -38,6 +46,7 @@ int cavlc_decode_block(BitReader *br, int nC, int maxcoef, int16_t *coef)
         level[i] = lv;
         if (suffix_len == 0) suffix_len = 1;
         int alv = lv < 0 ? -lv : lv;
+        *abs_sum += (uint32_t)alv;
         if (alv > (3 << (suffix_len - 1)) && suffix_len < 6) suffix_len++;
     }
 

@@ -12,6 +12,8 @@
  * order (coef[0] is the first coded scan position of the block).  Returns
  * TotalCoeff (>= 0) or -1 on a syntax error. */
 int cavlc_decode_block(BitReader *br, int nC, int maxcoef, int16_t *coef);
+/* same, also returning the sum of |level| (the host residual range bound) */
+int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, uint32_t *abs_sum);
 
 /* Encode one residual block (levels in scan order); returns TotalCoeff or -1
  * if a level cannot be represented in Baseline (level_prefix > 15). */

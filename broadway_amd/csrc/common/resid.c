@@ -32,14 +32,13 @@ static int idct_in_range(const int32_t *d)
     return 1;
 }
 
-/* one block: levels lv (scan order from `start`), DC value dc already
- * dequantized (start == 1).  |output| <= sum |d| + 5 before the final
- * rounding, so a sum below 32730 cannot leave the range. */
-static int block_in_range(const int16_t *lv, int start, int32_t dc, int qp)
+/* one block: levels lv (scan order from `start`) whose |level| sum is sum,
+ * DC value dc already dequantized (start == 1).  |output| <= sum |d| + 5
+ * before the final rounding, so a sum below 32730 cannot leave the range. */
+static int block_in_range(const int16_t *lv, uint32_t sum, int start, int32_t dc, int qp)
 {
     const int q6 = qp / 6, m6 = qp % 6;
-    uint32_t sum = 0;
-    if (lv) for (int s = start; s < 16; s++) sum += (uint32_t)(lv[s] < 0 ? -lv[s] : lv[s]);
+    if (!lv) sum = 0;
     const uint64_t bound = (uint64_t)sum * (uint64_t)(kLevelScale[m6][1] << q6) + (uint64_t)(dc < 0 ? -(int64_t)dc : dc);
     if (bound < 32000) return 1;
     int32_t d[16];
@@ -53,8 +52,18 @@ static int block_in_range(const int16_t *lv, int start, int32_t dc, int qp)
     return idct_in_range(d);
 }
 
-int mb_residual_in_range(const int16_t (*blk)[16], uint32_t cbits, int is_i16, int qp, int qpc)
+int mb_residual_in_range(const int16_t (*blk)[16], const uint32_t *bsum, uint32_t cbits, int is_i16,
+                         int qp, int qpc)
 {
+    /* whole-MB bound first: every block's DC and AC magnitudes are at most
+     * the MB's level sum times the largest scale (DC transforms are sums of
+     * +-levels with smaller scales) */
+    {
+        uint32_t total = 0;
+        for (uint32_t m = cbits & 0x7FFFFFFu; m; m &= m - 1) total += bsum[__builtin_ctz(m)];
+        const int q6 = (qp > qpc ? qp : qpc) / 6;
+        if ((uint64_t)total * (uint64_t)(29 << q6) < 32000) return 1;
+    }
     /* luma: h264bsdProcessLumaDc (transform.c:252-335) for I16, then one
      * ProcessBlock per block that has a DC or coded AC levels */
     int32_t dcy[16];
@@ -83,8 +92,8 @@ int mb_residual_in_range(const int16_t (*blk)[16], uint32_t cbits, int is_i16, i
         const int16_t *lv = (cbits & (1u << b)) ? blk[b] : NULL;
         if (is_i16) {
             const int32_t dc = dcy[kBlkY[b] * 4 + kBlkX[b]];
-            if ((lv || dc) && !block_in_range(lv, 1, dc, qp)) return 0;
-        } else if (lv && !block_in_range(lv, 0, 0, qp)) {
+            if ((lv || dc) && !block_in_range(lv, bsum[b], 1, dc, qp)) return 0;
+        } else if (lv && !block_in_range(lv, bsum[b], 0, 0, qp)) {
             return 0;
         }
     }
@@ -103,7 +112,7 @@ int mb_residual_in_range(const int16_t (*blk)[16], uint32_t cbits, int is_i16, i
         for (int b = 0; b < 4; b++) {
             const int bit = 16 + comp * 4 + b;
             const int16_t *lv = (cbits & (1u << bit)) ? blk[bit] : NULL;
-            if ((lv || f[b]) && !block_in_range(lv, 1, f[b], qpc)) return 0;
+            if ((lv || f[b]) && !block_in_range(lv, bsum[bit], 1, f[b], qpc)) return 0;
         }
     }
     return 1;

@@ -16,7 +16,9 @@
 /* blk: the parser's coefficient blocks in scan order -- [0..15] luma (I16:
  * position 0 unused), [16..23] Cb/Cr AC (position 0 unused), [24] I16 luma
  * DC, [25]/[26] Cb/Cr DC (4 levels); only blocks whose cbits bit is set are
- * read.  Returns 1 if every processed block stays in range. */
-int mb_residual_in_range(const int16_t (*blk)[16], uint32_t cbits, int is_i16, int qp, int qpc);
+ * read.  bsum[b]: sum of |level| of block b (from the CAVLC decode).
+ * Returns 1 if every processed block stays in range. */
+int mb_residual_in_range(const int16_t (*blk)[16], const uint32_t *bsum, uint32_t cbits, int is_i16,
+                         int qp, int qpc);
 
 #endif

@@ -42,6 +42,7 @@ struct h264mi_engine {
     unsigned long long *d_rows_done;   // row workgroups finished, all launches (tail-prep trigger)
     unsigned long long rows_launched;
     int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
+    int mc_waves;                      // MC waves per row workgroup: 3, or 2 (H264MI_MC_WAVES, sizing study)
     MbRec *d_rec;
     int16_t *d_coef;
     size_t coef_cap;          // blocks
@@ -136,6 +137,8 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     {
         const char *pa = getenv("H264MI_PREP_AT");
         e->prep_at_pct = pa ? atoi(pa) : 0;
+        const char *mw = getenv("H264MI_MC_WAVES");
+        e->mc_waves = (mw && atoi(mw) == 2) ? 2 : 3;
     }
     e->epoch = 0;
     (void)hipEventRecord(e->ev_staged, e->st);
@@ -242,6 +245,10 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
         if (rec) (void)hipEventRecord(t0, e->st);
         hipLaunchKernelGGL((k_wgpp<3, true, true>), grid, dim3(320), 0, e->st, a);
         if (rec) (void)hipEventRecord(t2, e->st);
+    } else if (e->mc_waves == 2) {
+        // sizing study (H264MI_MC_WAVES=2): two MC waves per row workgroup
+        hipExtLaunchKernelGGL((k_wgpp<2, false, true>), grid, dim3(256), 0, e->st, rec ? t0 : nullptr,
+                              rec ? t2 : nullptr, 0, a);
     } else {
         // the timing events ride on the kernel's own dispatch packet
         // (hipExtLaunchKernelGGL): no marker packets between launches

@@ -325,9 +325,10 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
 
     /* residual(), §7.3.5.3 */
     int16_t blk[27][16];
+    uint32_t bsum[27];
     uint32_t cbits = 0;
     if (is_i16) {
-        int tc = cavlc_decode_block(br, mbctx_nc_luma(&pb->pc, cur, 0), 16, blk[24]);
+        int tc = cavlc_decode_block_sum(br, mbctx_nc_luma(&pb->pc, cur, 0), 16, blk[24], &bsum[24]);
         if (tc < 0) return -1;
         if (tc) cbits |= 1u << 24;
     }
@@ -335,8 +336,8 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
         if (cbp & (1 << (b >> 2))) {
             int nc = mbctx_nc_luma(&pb->pc, cur, b);
             int tc;
-            if (is_i16) { blk[b][0] = 0; tc = cavlc_decode_block(br, nc, 15, blk[b] + 1); }
-            else tc = cavlc_decode_block(br, nc, 16, blk[b]);
+            if (is_i16) { blk[b][0] = 0; tc = cavlc_decode_block_sum(br, nc, 15, blk[b] + 1, &bsum[b]); }
+            else tc = cavlc_decode_block_sum(br, nc, 16, blk[b], &bsum[b]);
             if (tc < 0) return -1;
             m->tc[b] = (uint8_t)tc;
             if (tc) cbits |= 1u << b;
@@ -347,7 +348,7 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     int cc = cbp >> 4;
     if (cc) {
         for (int comp = 0; comp < 2; comp++) {
-            int tc = cavlc_decode_block(br, -1, 4, blk[25 + comp]);
+            int tc = cavlc_decode_block_sum(br, -1, 4, blk[25 + comp], &bsum[25 + comp]);
             if (tc < 0) return -1;
             if (tc) cbits |= 1u << (25 + comp);
         }
@@ -357,7 +358,7 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
             int idx = 16 + comp * 4 + b;
             if (cc & 2) {
                 blk[idx][0] = 0;
-                int tc = cavlc_decode_block(br, mbctx_nc_chroma(&pb->pc, cur, comp, b), 15, blk[idx] + 1);
+                int tc = cavlc_decode_block_sum(br, mbctx_nc_chroma(&pb->pc, cur, comp, b), 15, blk[idx] + 1, &bsum[idx]);
                 if (tc < 0) return -1;
                 m->tcc[comp * 4 + b] = (uint8_t)tc;
                 if (tc) cbits |= 1u << idx;
@@ -368,7 +369,7 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     if (br->err) return -1;
     /* h264bsdDecodeMacroblock -> ProcessResidual: a residual outside
      * [-512, 511] fails the MB, hence the slice (resid.h) */
-    if (cbits && !mb_residual_in_range((const int16_t (*)[16])blk, cbits, is_i16, *qp,
+    if (cbits && !mb_residual_in_range((const int16_t (*)[16])blk, bsum, cbits, is_i16, *qp,
                                        kQpChroma[clip3(0, 51, *qp + pps->chroma_qp_offset)]))
         pb->mb_decode_err = 1;
     int nblk = __builtin_popcount(cbits);

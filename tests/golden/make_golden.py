@@ -90,6 +90,10 @@ REF_CASES = {
     "ref_all_1080p": (3, 400, dict(nframes=16, ref_mod_pct=50, mmco_pct=40, lt_idr_pct=50, nonref_pct=20), False),
 }
 CASES.update(REF_CASES)
+# bench.py config legs: 24 pictures each
+for s in (1, 2, 3, 4):
+    CASES[f"leg_cfg2_720p_s{s}"] = (1, s, dict(nframes=24), False)
+CASES["leg_cfg5_2160p_s100"] = (4, 100, dict(nframes=24), False)
 # bench.py streams: config 3, 60 frames (4 warmup + 56 timed).  configs[3]
 # (64 streams, 8 per GPU) uses seeds 100..163: rank r of bench.py --gpus N owns
 # seeds 100 + 8r .. 100 + 8r + 7 (tests/test_gpu_parity.py decodes each shard)

@@ -7,7 +7,8 @@ import oracle as O
 from _golden import cases, md5s, stream
 
 CASES = cases()
-FAST = [n for n in CASES if not n.startswith("bench_")] + ["bench_1080p_s100", "bench_1080p_s105"]
+FAST = [n for n in CASES if not n.startswith(("bench_", "leg_"))] + ["bench_1080p_s100", "bench_1080p_s105",
+                                                                     "leg_cfg2_720p_s1"]
 
 
 @pytest.mark.parametrize("name", FAST)
