@@ -22,6 +22,11 @@ int h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be)
     d->be = be;
     d->aub_first_call = 1;
     d->cur_slot = -1;
+    /* worker threads for speculative slice parsing: H264MI_PARSE_THREADS
+     * (default 3; 0 = off) */
+    const char *pt = getenv("H264MI_PARSE_THREADS");
+    const int nth = pt ? atoi(pt) : 3;
+    d->spec = nth > 0 ? spec_create(nth > 16 ? 16 : nth) : NULL;
     return 0;
 }
 
@@ -34,6 +39,8 @@ static void out_frames_free(H264Dec *d)
 
 void h264dec_release(H264Dec *d)
 {
+    spec_destroy(d->spec);
+    d->spec = NULL;
     if (d->pb_ready) picbuild_free(&d->pb);
     free(d->rbsp);
     out_frames_free(d);
@@ -55,8 +62,10 @@ int h264dec_valid_param_sets(const H264Dec *d)
 }
 
 /* ---- byte stream: reference byte_stream.c:80-236 semantics ----------- */
-static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_t **nal,
-                       uint32_t *nal_len, uint32_t *read_bytes)
+/* locate the next NAL unit: payload at bs + *init, *size bytes; *emul: an
+ * emulation-prevention pattern was seen (or raw NAL mode) */
+int nal_scan(const uint8_t *bs, uint32_t len, uint32_t *init_out, uint32_t *size_out, uint32_t *read_bytes,
+             int *emul_out)
 {
     uint32_t init = 0, size, zeros = 0;
     int emul = 0;
@@ -104,7 +113,51 @@ static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_
         *read_bytes = len;
         emul = 1;
     }
-    const uint8_t *src = bs + init;
+    *init_out = init;
+    *size_out = size;
+    *emul_out = emul;
+    return 0;
+}
+
+/* emulation-prevention removal (byte_stream.c:191-229) into dst (>= size
+ * bytes); returns the RBSP length or -1 on an invalid sequence */
+int nal_unescape(const uint8_t *src, uint32_t size, int emul, uint8_t *dst)
+{
+    uint32_t w = 0;
+    if (!emul) {
+        memcpy(dst, src, size);
+        return (int)size;
+    }
+    int zc = 0;
+    for (uint32_t i = 0; i < size; i++) {
+        if (zc == 0) {
+            /* copy up to the next zero byte in one go */
+            const uint8_t *z = (const uint8_t *)memchr(src + i, 0, size - i);
+            const uint32_t n = z ? (uint32_t)(z - (src + i)) : size - i;
+            memcpy(dst + w, src + i, n);
+            w += n;
+            i += n;
+            if (i == size) break;
+        }
+        uint8_t b = src[i];
+        if (zc == 2 && b == 3) {
+            if (i == size - 1 || src[i + 1] > 3) return -1;
+            zc = 0;
+            continue;
+        }
+        if (zc == 2 && b <= 2) return -1;
+        zc = b == 0 ? zc + 1 : 0;
+        dst[w++] = b;
+    }
+    return (int)w;
+}
+
+static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_t **nal,
+                       uint32_t *nal_len, uint32_t *read_bytes)
+{
+    uint32_t init, size;
+    int emul;
+    if (nal_scan(bs, len, &init, &size, read_bytes, &emul)) return -1;
     if (d->rbsp_cap < size + 8) {
         size_t nc = size + 64 + size / 2;
         uint8_t *r = (uint8_t *)realloc(d->rbsp, nc);
@@ -112,35 +165,10 @@ static int extract_nal(H264Dec *d, const uint8_t *bs, uint32_t len, const uint8_
         d->rbsp = r;
         d->rbsp_cap = nc;
     }
-    uint32_t w = 0;
-    if (emul) {
-        int zc = 0;
-        for (uint32_t i = 0; i < size; i++) {
-            if (zc == 0) {
-                /* copy up to the next zero byte in one go */
-                const uint8_t *z = (const uint8_t *)memchr(src + i, 0, size - i);
-                const uint32_t n = z ? (uint32_t)(z - (src + i)) : size - i;
-                memcpy(d->rbsp + w, src + i, n);
-                w += n;
-                i += n;
-                if (i == size) break;
-            }
-            uint8_t b = src[i];
-            if (zc == 2 && b == 3) {
-                if (i == size - 1 || src[i + 1] > 3) return -1;
-                zc = 0;
-                continue;
-            }
-            if (zc == 2 && b <= 2) return -1;
-            zc = b == 0 ? zc + 1 : 0;
-            d->rbsp[w++] = b;
-        }
-    } else {
-        memcpy(d->rbsp, src, size);
-        w = size;
-    }
+    int w = nal_unescape(bs + init, size, emul, d->rbsp);
+    if (w < 0) return -1;
     *nal = d->rbsp;
-    *nal_len = w;
+    *nal_len = (uint32_t)w;
     return 0;
 }
 
@@ -457,7 +485,8 @@ int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id
             if (!d->pps[sh.pps_id].valid || d->pps[sh.pps_id].sps_id != d->active_sps) return DEC_FAIL(DEC_ERROR);
             pps = &d->pps[sh.pps_id];
         }
-        if (!d->valid_slice_in_au) {
+        const int first_slice = !d->valid_slice_in_au;
+        if (first_slice) {
             if (!is_idr && dpb_check_gaps(&d->dpb, sh.frame_num, nh.ref_idc != 0, sps->gaps_allowed))
                 return DEC_FAIL(DEC_ERROR);
             d->cur_slot = dpb_alloc_current(&d->dpb);
@@ -471,7 +500,13 @@ int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id
         int ref_slot[MAX_REFS];
         if (dpb_build_list(&d->dpb, &sh, ref_slot)) return DEC_FAIL(DEC_ERROR);
         d->pb.pc.cip = pps->cip;
-        if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot)) {
+        /* the picture's later slices already in the buffer are parsed ahead
+         * on worker threads; this thread takes their results when it gets
+         * there (specparse.c), else parses them itself */
+        if (first_slice) spec_launch(d->spec, d, sps, pps, &nh, &sh, buf, *read_bytes, len);
+        if (!first_slice && spec_take(d->spec, d, buf, *read_bytes, &sh, pps, ref_slot)) {
+            /* taken: identical to parsing it here */
+        } else if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot)) {
             /* the slice is un-marked (decoder.c:462-467, slice_data.c:302-358);
              * its MBs are concealed at the next access-unit boundary */
             picbuild_mark_slice_corrupted(&d->pb, sh.first_mb);

@@ -43,6 +43,8 @@ enum {
     DEC_PARAM_SET_ERROR = 4, DEC_MEMALLOC_ERROR = 5,
 };
 
+typedef struct SpecPool SpecPool;
+
 typedef struct PocState {
     int prev_msb, prev_lsb;
     int prev_frame_num_offset, prev_frame_num;
@@ -86,6 +88,8 @@ typedef struct H264Dec {
     int      nslots;
     /* statistics */
     uint64_t pics_decoded, alg_ref_bytes, coded_blocks;
+    /* speculative parallel slice parsing (specparse.c); NULL: off */
+    SpecPool *spec;
 } H264Dec;
 
 int  h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be);
@@ -104,6 +108,19 @@ int  h264dec_valid_param_sets(const H264Dec *d);
 /* conceal the current picture's missing MBs (conceal.c); returns their
  * number or -1 */
 int  h264dec_conceal(H264Dec *d, int is_i);
+
+/* Annex-B NAL unit location and emulation-prevention removal (decoder.c) */
+int  nal_scan(const uint8_t *bs, uint32_t len, uint32_t *init, uint32_t *size, uint32_t *read_bytes, int *emul);
+int  nal_unescape(const uint8_t *src, uint32_t size, int emul, uint8_t *dst);
+
+/* speculative parallel slice parsing (specparse.c) */
+SpecPool *spec_create(int nthreads);
+void spec_destroy(SpecPool *sp);
+void spec_drain(SpecPool *sp);
+void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps, const NalHdr *nh,
+                 const SliceHdr *sh, const uint8_t *buf, uint32_t first_bytes, uint32_t len);
+int  spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
+               const Pps *pps, const int *ref_slot);
 const Sps *h264dec_active_sps(const H264Dec *d);
 
 #endif

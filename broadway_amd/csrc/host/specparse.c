@@ -1,0 +1,269 @@
+/* Speculative parallel slice-data parsing (host throughput of the end-to-end
+ * path; no reference counterpart -- the reference parses one NAL per call).
+ *
+ * The C API is sequential: every call decodes the next NAL unit.  When a
+ * picture's first slice is decoded and the caller's buffer already holds the
+ * picture's next slice NAL units (a byte stream handed over whole, as
+ * DecTestBench does), worker threads parse those slices ahead -- header,
+ * RefPicList0 from a snapshot of the DPB, and the whole slice_data() into a
+ * private PicBuild -- while the calling thread parses the first slice.
+ * Slices are independent in slice_data() (neighbours in other slices are
+ * unavailable, H.264 §6.4.x), so a private parse sees exactly what the
+ * sequential one sees.
+ *
+ * The sequential path stays the authority: when the calling thread reaches
+ * such a NAL it parses the slice header itself and takes the worker's result
+ * only if the NAL bytes, the slice header, the parameter sets and the
+ * reference list are identical and the slice parsed without error and
+ * overlaps no decoded MB; otherwise it parses the slice itself.  Results are
+ * therefore the sequential decoder's, bit for bit. */
+#include "decoder.h"
+
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define SPEC_MAX_JOBS 16
+
+typedef struct SpecJob {
+    /* set by the caller */
+    const uint8_t *nal_ptr;    /* caller's buffer position of the NAL unit */
+    uint32_t read_bytes;       /* bytes the NAL consumes (nal_scan) */
+    uint8_t *raw;              /* private copy of those bytes */
+    uint32_t raw_cap;
+    uint8_t *rbsp;
+    uint32_t rbsp_cap;
+    /* worker results */
+    int      done, ok;
+    SliceHdr sh;
+    int      ref_slot[MAX_REFS];
+    PicBuild pb;
+    int      pb_ready;
+} SpecJob;
+
+struct SpecPool {
+    pthread_t       *th;
+    int              nth;
+    pthread_mutex_t  mu;
+    pthread_cond_t   cv_work, cv_done;
+    int              stop;
+    SpecJob          jobs[SPEC_MAX_JOBS];
+    int              njobs, next;   /* jobs[next..njobs) wait for a worker */
+    int              running;
+    unsigned long    taken, declined;   /* statistics (H264MI_SPEC_STATS) */
+    /* snapshot of the picture the jobs belong to */
+    Sps              sps;
+    Pps              pps;
+    Dpb              dpb;
+    SliceHdr         first;         /* the picture's first slice header */
+    NalHdr           nh;
+    int              w, h, cip, cur_slot;
+};
+
+static void run_job(SpecPool *sp, SpecJob *j)
+{
+    j->ok = 0;
+    uint32_t init, size;
+    int emul;
+    if (nal_scan(j->raw, j->read_bytes, &init, &size, &j->read_bytes, &emul)) return;
+    if (j->rbsp_cap < size + 8) {
+        free(j->rbsp);
+        j->rbsp_cap = size + 64 + size / 2;
+        j->rbsp = (uint8_t *)malloc(j->rbsp_cap);
+        if (!j->rbsp) { j->rbsp_cap = 0; return; }
+    }
+    const int n = nal_unescape(j->raw + init, size, emul, j->rbsp);
+    if (n < 2 || (j->rbsp[0] & 0x80)) return;
+    const NalHdr nh = {(j->rbsp[0] >> 5) & 3, j->rbsp[0] & 31};
+    if (nh.type != sp->nh.type || (nh.ref_idc != 0) != (sp->nh.ref_idc != 0)) return;
+    BitReader br;
+    br_init(&br, j->rbsp + 1, (size_t)n - 1);
+    if (parse_slice_header(&br, &nh, &sp->sps, &sp->pps, &j->sh)) return;
+    const SliceHdr *f = &sp->first;
+    if (j->sh.pps_id != f->pps_id || j->sh.frame_num != f->frame_num || j->sh.idr_pic_id != f->idr_pic_id ||
+        j->sh.poc_lsb != f->poc_lsb || j->sh.delta_poc_bottom != f->delta_poc_bottom ||
+        j->sh.first_mb <= f->first_mb)
+        return;                                   /* not a later slice of this picture */
+    Dpb dpb = sp->dpb;                            /* dpb_build_list updates list / PicNums */
+    if (dpb_build_list(&dpb, &j->sh, j->ref_slot)) return;
+    if (!j->pb_ready || j->pb.w != sp->w || j->pb.h != sp->h) {
+        if (j->pb_ready) picbuild_free(&j->pb);
+        j->pb_ready = 0;
+        if (picbuild_init(&j->pb, sp->w, sp->h)) return;
+        j->pb_ready = 1;
+    }
+    picbuild_reset(&j->pb, sp->cip);
+    j->pb.cur_slot = sp->cur_slot;
+    if (parse_slice_data(&j->pb, &br, &j->sh, &sp->pps, j->ref_slot)) return;
+    j->ok = 1;
+}
+
+static void *worker(void *arg)
+{
+    SpecPool *sp = (SpecPool *)arg;
+    pthread_mutex_lock(&sp->mu);
+    for (;;) {
+        while (!sp->stop && sp->next >= sp->njobs) pthread_cond_wait(&sp->cv_work, &sp->mu);
+        if (sp->stop) break;
+        SpecJob *j = &sp->jobs[sp->next++];
+        sp->running++;
+        pthread_mutex_unlock(&sp->mu);
+        run_job(sp, j);
+        pthread_mutex_lock(&sp->mu);
+        j->done = 1;
+        sp->running--;
+        pthread_cond_broadcast(&sp->cv_done);
+    }
+    pthread_mutex_unlock(&sp->mu);
+    return NULL;
+}
+
+SpecPool *spec_create(int nthreads)
+{
+    if (nthreads < 1) return NULL;
+    SpecPool *sp = (SpecPool *)calloc(1, sizeof(SpecPool));
+    if (!sp) return NULL;
+    pthread_mutex_init(&sp->mu, NULL);
+    pthread_cond_init(&sp->cv_work, NULL);
+    pthread_cond_init(&sp->cv_done, NULL);
+    sp->th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int i = 0; sp->th && i < nthreads; i++)
+        if (pthread_create(&sp->th[i], NULL, worker, sp) == 0) sp->nth++;
+    if (!sp->nth) { spec_destroy(sp); return NULL; }
+    return sp;
+}
+
+/* wait for the workers, then forget every job */
+void spec_drain(SpecPool *sp)
+{
+    if (!sp) return;
+    pthread_mutex_lock(&sp->mu);
+    sp->next = sp->njobs;                         /* nothing more starts */
+    while (sp->running) pthread_cond_wait(&sp->cv_done, &sp->mu);
+    sp->njobs = sp->next = 0;
+    pthread_mutex_unlock(&sp->mu);
+}
+
+void spec_destroy(SpecPool *sp)
+{
+    if (!sp) return;
+    if (getenv("H264MI_SPEC_STATS"))
+        fprintf(stderr, "h264mi: speculative slices taken %lu, parsed again %lu\n", sp->taken, sp->declined);
+    pthread_mutex_lock(&sp->mu);
+    sp->stop = 1;
+    pthread_cond_broadcast(&sp->cv_work);
+    pthread_mutex_unlock(&sp->mu);
+    for (int i = 0; i < sp->nth; i++) pthread_join(sp->th[i], NULL);
+    for (int i = 0; i < SPEC_MAX_JOBS; i++) {
+        free(sp->jobs[i].raw);
+        free(sp->jobs[i].rbsp);
+        if (sp->jobs[i].pb_ready) picbuild_free(&sp->jobs[i].pb);
+    }
+    free(sp->th);
+    pthread_mutex_destroy(&sp->mu);
+    pthread_cond_destroy(&sp->cv_work);
+    pthread_cond_destroy(&sp->cv_done);
+    free(sp);
+}
+
+/* Start of a picture: its first slice (header sh, NAL header nh) was just
+ * read from buf[0..first_bytes); queue the slice NAL units that follow it in
+ * buf[first_bytes..len). */
+void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps, const NalHdr *nh,
+                 const SliceHdr *sh, const uint8_t *buf, uint32_t first_bytes, uint32_t len)
+{
+    if (!sp) return;
+    spec_drain(sp);
+    pthread_mutex_lock(&sp->mu);
+    sp->sps = *sps;
+    sp->pps = *pps;
+    sp->dpb = d->dpb;
+    sp->first = *sh;
+    sp->nh = *nh;
+    sp->w = d->pb.w; sp->h = d->pb.h; sp->cip = pps->cip; sp->cur_slot = d->cur_slot;
+    uint32_t pos = first_bytes;
+    while (sp->njobs < SPEC_MAX_JOBS && pos < len) {
+        uint32_t init, size, rb;
+        int emul;
+        if (nal_scan(buf + pos, len - pos, &init, &size, &rb, &emul) || size < 2 || rb == 0) break;
+        const uint8_t t = buf[pos + init] & 31;
+        if (t != NAL_SLICE && t != NAL_IDR) break;     /* a non-slice NAL ends the access unit */
+        SpecJob *j = &sp->jobs[sp->njobs];
+        if (j->raw_cap < rb) {
+            free(j->raw);
+            j->raw_cap = rb + rb / 2 + 64;
+            j->raw = (uint8_t *)malloc(j->raw_cap);
+            if (!j->raw) { j->raw_cap = 0; break; }
+        }
+        memcpy(j->raw, buf + pos, rb);           /* the caller may reuse its buffer */
+        j->nal_ptr = buf + pos;
+        j->read_bytes = rb;
+        j->done = j->ok = 0;
+        sp->njobs++;
+        pos += rb;
+    }
+    pthread_cond_broadcast(&sp->cv_work);
+    pthread_mutex_unlock(&sp->mu);
+}
+
+static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
+                  const Pps *pps, const int *ref_slot);
+
+/* The calling thread reached the slice NAL at buf (read_bytes long) whose
+ * header it parsed into sh, with reference list ref_slot: take a matching
+ * worker result into d->pb.  1: taken (the slice is decoded), 0: parse it. */
+int spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
+              const Pps *pps, const int *ref_slot)
+{
+    if (!sp) return 0;
+    pthread_mutex_lock(&sp->mu);
+    SpecJob *j = NULL;
+    for (int i = 0; i < sp->njobs; i++)
+        if (sp->jobs[i].nal_ptr == buf && sp->jobs[i].read_bytes == read_bytes) { j = &sp->jobs[i]; break; }
+    if (j) {
+        if (j - sp->jobs >= sp->next) {          /* not started: parse it here instead */
+            pthread_mutex_unlock(&sp->mu);
+            return 0;
+        }
+        while (!j->done) pthread_cond_wait(&sp->cv_done, &sp->mu);
+    }
+    pthread_mutex_unlock(&sp->mu);
+    const int r = j && j->ok && commit(sp, j, d, buf, read_bytes, sh, pps, ref_slot);
+    if (j) { if (r) sp->taken++; else sp->declined++; }
+    return r;
+}
+
+static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
+                  const Pps *pps, const int *ref_slot)
+{
+    PicBuild *pb = &d->pb, *q = &j->pb;
+    if (memcmp(j->raw, buf, read_bytes) || memcmp(&j->sh, sh, sizeof(*sh)) ||
+        memcmp(j->ref_slot, ref_slot, sizeof(j->ref_slot)) || memcmp(&sp->pps, pps, sizeof(*pps)) ||
+        pb->cur_slot != sp->cur_slot || pb->pc.cip != sp->cip)
+        return 0;
+    const int first = sh->first_mb, count = q->ndecoded;
+    if (first + count > pb->nmbs || pb->ndecoded + count > pb->nmbs) return 0;
+    for (int i = first; i < first + count; i++) if (pb->decoded[i]) return 0;
+    const uint32_t off = pb->ncoef;
+    int16_t *dst = picbuild_coef_alloc(pb, q->ncoef);
+    if (!dst && q->ncoef) return 0;
+    if (q->ncoef) memcpy(dst, q->coef, (size_t)q->ncoef * 32);
+    const uint16_t tag = (uint16_t)++pb->nslices;
+    for (int i = first; i < first + count; i++) {
+        pb->rec[i] = q->rec[i];
+        pb->rec[i].coef += off;
+        pb->rec[i].slice = tag;
+        pb->pc.mb[i] = q->pc.mb[i];
+        pb->pc.mb[i].slice = tag;
+        pb->decoded[i] = 1;
+    }
+    pb->ndecoded += count;
+    pb->last_mb_addr = q->last_mb_addr;
+    pb->is_p |= q->is_p;
+    pb->alg_ref_bytes += q->alg_ref_bytes;
+    pb->n_inter += q->n_inter;
+    pb->n_intra += q->n_intra;
+    pb->n_coded_blocks += q->n_coded_blocks;
+    return 1;
+}
