@@ -330,8 +330,10 @@ def end_to_end(streams, nframes, reps=3):
                          f"(H264SwDec* C-ABI) per stream: host parse + H2D + kernels + D2H of every picture; "
                          f"{pics} frames in {t:.2f} s"}
         if parts and pics:
-            res["per_picture_ms"] = {k[2:]: round(v * 1e3 / pics * len(streams) / len(streams), 3)
-                                     for k, v in sorted(parts.items())}
+            # per picture inside one decoder process (H264SwDecGetTiming):
+            # host parse / record upload + launch / wait for the GPU / D2H copy
+            res["per_picture_ms"] = {k[2:]: round(v * 1e3 / pics, 3) for k, v in sorted(parts.items())}
+            res["parse_threads_per_process"] = 1 + int(os.environ.get("H264MI_PARSE_THREADS", "3"))
         return res
     finally:
         shutil.rmtree(td, ignore_errors=True)

@@ -516,6 +516,12 @@ static int hb_flagged(h264mi_engine *e)
     return n ? 1 : 0;
 }
 
+static int hb_sync(void *vctx)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    return h264mi_engine_sync(c->e);
+}
+
 static int hb_read(void *vctx, int slot, uint8_t *dst)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
@@ -573,6 +579,7 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     be.host_alloc = hb_host_alloc;
     be.host_free = hb_host_free;
     be.copy = hb_copy;
+    be.sync = hb_sync;
     be.destroy = hb_destroy;
     return be;
 }

@@ -229,6 +229,19 @@ H264SwDecRet H264SwDecNextPictureRGBA(H264SwDecInst decInst, H264SwDecPicture *p
     return H264SWDEC_PIC_RDY;
 }
 
+H264SwDecRet H264SwDecGetTiming(H264SwDecInst decInst, double *parse_s, double *submit_s, double *wait_s,
+                                double *copy_s, u32 *pictures)
+{
+    if (decInst == NULL) return H264SWDEC_PARAM_ERR;
+    const DecContainer *c = (const DecContainer *)decInst;
+    if (parse_s) *parse_s = c->dec.t_parse;
+    if (submit_s) *submit_s = c->dec.t_submit;
+    if (wait_s) *wait_s = c->dec.t_wait;
+    if (copy_s) *copy_s = c->dec.t_copy;
+    if (pictures) *pictures = (u32)c->dec.n_output;
+    return H264SWDEC_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* wasm / JS glue (Decoder.c): one global instance per process               */
 /* ------------------------------------------------------------------------ */

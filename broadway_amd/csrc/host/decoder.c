@@ -6,6 +6,15 @@
 #include <string.h>
 
 #include <stdio.h>
+#include <time.h>
+
+double h264dec_now(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 static int dbg_enabled(void) { static int e = -1; if (e < 0) e = getenv("H264MI_DEBUG") != NULL; return e; }
 #define DEC_FAIL(code) (dbg_enabled() ? (fprintf(stderr, "h264mi: %s:%d -> %d\n", __FILE__, __LINE__, (code)), (code)) : (code))
 #define SPS_FORCE (MAX_SPS + 1)
@@ -357,7 +366,10 @@ static void store_pps(H264Dec *d, const Pps *p)
 static int finish_picture(H264Dec *d, int concealed_mbs)
 {
     const Sps *sps = &d->sps[d->active_sps];
-    if (d->be.decode(d->be.ctx, &d->pb, d->cur_slot)) return DEC_FAIL(DEC_ERROR);
+    const double t0 = h264dec_now();
+    const int rc = d->be.decode(d->be.ctx, &d->pb, d->cur_slot);
+    d->t_submit += h264dec_now() - t0;
+    if (rc) return DEC_FAIL(DEC_ERROR);
     d->pics_decoded++;
     d->alg_ref_bytes += d->pb.alg_ref_bytes;
     d->coded_blocks += d->pb.n_coded_blocks;
@@ -372,7 +384,17 @@ static int finish_picture(H264Dec *d, int concealed_mbs)
     return DEC_PIC_RDY;
 }
 
+static int decode_nal(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id, uint32_t *read_bytes);
+
 int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id, uint32_t *read_bytes)
+{
+    const double t0 = h264dec_now(), s0 = d->t_submit;
+    const int r = decode_nal(d, buf, len, pic_id, read_bytes);
+    d->t_parse += h264dec_now() - t0 - (d->t_submit - s0);
+    return r;
+}
+
+static int decode_nal(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id, uint32_t *read_bytes)
 {
     const uint8_t *nal;
     uint32_t nal_len;
@@ -503,8 +525,9 @@ int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id
         /* the picture's later slices already in the buffer are parsed ahead
          * on worker threads; this thread takes their results when it gets
          * there (specparse.c), else parses them itself */
-        if (first_slice) spec_launch(d->spec, d, sps, pps, &nh, &sh, buf, *read_bytes, len);
-        if (!first_slice && spec_take(d->spec, d, buf, *read_bytes, &sh, pps, ref_slot)) {
+        if (first_slice && !spec_active_for(d->spec, buf))
+            spec_launch(d->spec, d, sps, pps, &nh, &sh, buf, *read_bytes, len);
+        if (spec_take(d->spec, d, buf, *read_bytes, &sh, pps, ref_slot)) {
             /* taken: identical to parsing it here */
         } else if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot)) {
             /* the slice is un-marked (decoder.c:462-467, slice_data.c:302-358);
@@ -514,7 +537,11 @@ int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id
         }
         if (d->pb.ndecoded == d->pb.nmbs) {
             d->skip_redundant = 1;
-            return finish_picture(d, d->num_concealed);
+            const int r = finish_picture(d, d->num_concealed);
+            /* the next picture's slices, if the buffer holds them, are parsed
+             * while the caller fetches this one */
+            if (r == DEC_PIC_RDY && *read_bytes < len) spec_launch_ahead(d->spec, d, buf + *read_bytes, len - *read_bytes);
+            return r;
         }
         return DEC_RDY;
     }
@@ -542,7 +569,13 @@ const uint8_t *h264dec_next_output_rgba(H264Dec *d, uint32_t *pic_id, uint32_t *
     const DpbOut *o = dpb_next_output(&d->dpb);
     if (!o) return NULL;
     uint8_t *dst = rgba ? rgba : d->out_frames + d->frame_bytes * (size_t)o->slot;
+    const double t0 = h264dec_now();
+    if (d->be.sync && d->be.sync(d->be.ctx)) return NULL;
+    const double t1 = h264dec_now();
     const int rr = rgba ? d->be.read_rgba(d->be.ctx, o->slot, dst) : d->be.read(d->be.ctx, o->slot, dst);
+    d->t_wait += t1 - t0;
+    d->t_copy += h264dec_now() - t1;
+    d->n_output++;
     if (rr < 0) return NULL;
     if (pic_id) *pic_id = (uint32_t)o->pic_id;
     if (is_idr) *is_idr = (uint32_t)o->is_idr;

@@ -35,6 +35,9 @@ typedef struct H264Backend {
     void (*host_free)(void *ctx, void *p);
     /* copy one slot into another (error concealment of lost pictures) */
     int  (*copy)(void *ctx, int dst_slot, int src_slot);
+    /* optional: wait for the reconstructions issued so far (timing split of
+     * the output path into device wait and copy) */
+    int  (*sync)(void *ctx);
     void (*destroy)(void *ctx);
 } H264Backend;
 
@@ -90,7 +93,13 @@ typedef struct H264Dec {
     uint64_t pics_decoded, alg_ref_bytes, coded_blocks;
     /* speculative parallel slice parsing (specparse.c); NULL: off */
     SpecPool *spec;
+    /* end-to-end time split (seconds): host parse, record upload + launch,
+     * wait for the device, output copy; pictures output */
+    double   t_parse, t_submit, t_wait, t_copy;
+    uint64_t n_output;
 } H264Dec;
+
+double h264dec_now(void);
 
 int  h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be);
 void h264dec_release(H264Dec *d);
@@ -121,6 +130,8 @@ void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps,
                  const SliceHdr *sh, const uint8_t *buf, uint32_t first_bytes, uint32_t len);
 int  spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
                const Pps *pps, const int *ref_slot);
+void spec_launch_ahead(SpecPool *sp, const H264Dec *d, const uint8_t *buf, uint32_t len);
+int  spec_active_for(const SpecPool *sp, const uint8_t *buf);
 const Sps *h264dec_active_sps(const H264Dec *d);
 
 #endif

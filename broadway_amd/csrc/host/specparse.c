@@ -34,6 +34,8 @@ typedef struct SpecJob {
     uint32_t raw_cap;
     uint8_t *rbsp;
     uint32_t rbsp_cap;
+    int      is_first;         /* the picture's first slice (launched ahead) */
+    int      started;          /* claimed by a worker or by the calling thread */
     /* worker results */
     int      done, ok;
     SliceHdr sh;
@@ -49,7 +51,8 @@ struct SpecPool {
     pthread_cond_t   cv_work, cv_done;
     int              stop;
     SpecJob          jobs[SPEC_MAX_JOBS];
-    int              njobs, next;   /* jobs[next..njobs) wait for a worker */
+    int              njobs, next;   /* jobs[order[next..njobs)] wait for a worker */
+    int              order[SPEC_MAX_JOBS];
     int              running;
     unsigned long    taken, declined;   /* statistics (H264MI_SPEC_STATS) */
     /* snapshot of the picture the jobs belong to */
@@ -57,6 +60,7 @@ struct SpecPool {
     Pps              pps;
     Dpb              dpb;
     SliceHdr         first;         /* the picture's first slice header */
+    const uint8_t   *pic_ptr;       /* buffer position of the picture's first slice NAL */
     NalHdr           nh;
     int              w, h, cip, cur_slot;
 };
@@ -83,8 +87,8 @@ static void run_job(SpecPool *sp, SpecJob *j)
     const SliceHdr *f = &sp->first;
     if (j->sh.pps_id != f->pps_id || j->sh.frame_num != f->frame_num || j->sh.idr_pic_id != f->idr_pic_id ||
         j->sh.poc_lsb != f->poc_lsb || j->sh.delta_poc_bottom != f->delta_poc_bottom ||
-        j->sh.first_mb <= f->first_mb)
-        return;                                   /* not a later slice of this picture */
+        (j->is_first ? j->sh.first_mb != f->first_mb : j->sh.first_mb <= f->first_mb))
+        return;                                   /* not a slice of this picture */
     Dpb dpb = sp->dpb;                            /* dpb_build_list updates list / PicNums */
     if (dpb_build_list(&dpb, &j->sh, j->ref_slot)) return;
     if (!j->pb_ready || j->pb.w != sp->w || j->pb.h != sp->h) {
@@ -104,9 +108,11 @@ static void *worker(void *arg)
     SpecPool *sp = (SpecPool *)arg;
     pthread_mutex_lock(&sp->mu);
     for (;;) {
-        while (!sp->stop && sp->next >= sp->njobs) pthread_cond_wait(&sp->cv_work, &sp->mu);
+        while (!sp->stop && sp->next < sp->njobs && sp->jobs[sp->order[sp->next]].started) sp->next++;
         if (sp->stop) break;
-        SpecJob *j = &sp->jobs[sp->next++];
+        if (sp->next >= sp->njobs) { pthread_cond_wait(&sp->cv_work, &sp->mu); continue; }
+        SpecJob *j = &sp->jobs[sp->order[sp->next++]];
+        j->started = 1;
         sp->running++;
         pthread_mutex_unlock(&sp->mu);
         run_job(sp, j);
@@ -167,6 +173,8 @@ void spec_destroy(SpecPool *sp)
     free(sp);
 }
 
+static void queue_slices(SpecPool *sp, const uint8_t *buf, uint32_t pos, uint32_t len, int first_is_first);
+
 /* Start of a picture: its first slice (header sh, NAL header nh) was just
  * read from buf[0..first_bytes); queue the slice NAL units that follow it in
  * buf[first_bytes..len). */
@@ -182,7 +190,16 @@ void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps,
     sp->first = *sh;
     sp->nh = *nh;
     sp->w = d->pb.w; sp->h = d->pb.h; sp->cip = pps->cip; sp->cur_slot = d->cur_slot;
-    uint32_t pos = first_bytes;
+    sp->pic_ptr = buf;
+    queue_slices(sp, buf, first_bytes, len, 0);
+    pthread_cond_broadcast(&sp->cv_work);
+    pthread_mutex_unlock(&sp->mu);
+}
+
+/* queue the slice NAL units of buf[pos..len) up to the first non-slice NAL
+ * (caller holds the lock) */
+static void queue_slices(SpecPool *sp, const uint8_t *buf, uint32_t pos, uint32_t len, int first_is_first)
+{
     while (sp->njobs < SPEC_MAX_JOBS && pos < len) {
         uint32_t init, size, rb;
         int emul;
@@ -199,12 +216,74 @@ void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps,
         memcpy(j->raw, buf + pos, rb);           /* the caller may reuse its buffer */
         j->nal_ptr = buf + pos;
         j->read_bytes = rb;
-        j->done = j->ok = 0;
+        j->is_first = first_is_first && sp->njobs == 0;
+        j->done = j->ok = j->started = 0;
+        sp->order[sp->njobs] = sp->njobs;
         sp->njobs++;
         pos += rb;
     }
+    /* workers take the picture's first slice last: the calling thread, when
+     * it gets there before any worker, parses that one itself */
+    if (first_is_first && sp->njobs > 1) {
+        for (int i = 0; i + 1 < sp->njobs; i++) sp->order[i] = i + 1;
+        sp->order[sp->njobs - 1] = 0;
+    }
+}
+
+/* A picture was just finished and buf[0..len) continues the stream: when it
+ * starts with the next picture's first slice, parse that picture's slices
+ * ahead -- all of them -- against the DPB as the finished picture left it
+ * and the frame slot the next picture will take (dpb_alloc_current).  A gap
+ * in frame_num or new parameter sets make the results differ; spec_take then
+ * declines them. */
+void spec_launch_ahead(SpecPool *sp, const H264Dec *d, const uint8_t *buf, uint32_t len)
+{
+    if (!sp || !len || d->active_sps < 0 || d->active_sps >= MAX_SPS) return;
+    spec_drain(sp);
+    uint32_t init, size, rb;
+    int emul;
+    if (nal_scan(buf, len, &init, &size, &rb, &emul) || size < 2) return;
+    const uint8_t t = buf[init] & 31;
+    if (t != NAL_SLICE && t != NAL_IDR) return;
+    /* the first slice's header, from its first bytes */
+    uint8_t hdr[256];
+    const uint32_t hs = size < 200 ? size : 200;
+    uint32_t k = 0;
+    int zc = 0;
+    for (uint32_t i = 0; i < hs; i++) {             /* emulation-prevention removal, prefix only */
+        const uint8_t b = buf[init + i];
+        if (zc == 2 && b == 3 && emul) { zc = 0; continue; }
+        zc = b == 0 ? zc + 1 : 0;
+        hdr[k++] = b;
+    }
+    if (hdr[0] & 0x80) return;
+    const NalHdr nh = {(hdr[0] >> 5) & 3, hdr[0] & 31};
+    BitReader br;
+    br_init(&br, hdr + 1, k - 1);
+    int pps_id;
+    if (peek_slice_pps_id(&br, &pps_id) || !d->pps[pps_id].valid || d->pps[pps_id].sps_id != d->active_sps) return;
+    const Sps *sps = &d->sps[d->active_sps];
+    const Pps *pps = &d->pps[pps_id];
+    SliceHdr sh;
+    if (parse_slice_header(&br, &nh, sps, pps, &sh)) return;
+    pthread_mutex_lock(&sp->mu);
+    sp->sps = *sps;
+    sp->pps = *pps;
+    sp->dpb = d->dpb;
+    sp->first = sh;
+    sp->nh = nh;
+    sp->w = d->pb.w; sp->h = d->pb.h; sp->cip = pps->cip;
+    sp->cur_slot = d->dpb.pic[d->dpb.size].slot;     /* what dpb_alloc_current will return */
+    sp->pic_ptr = buf;
+    queue_slices(sp, buf, 0, len, 1);
     pthread_cond_broadcast(&sp->cv_work);
     pthread_mutex_unlock(&sp->mu);
+}
+
+/* slices of the picture starting at buf are being parsed ahead */
+int spec_active_for(const SpecPool *sp, const uint8_t *buf)
+{
+    return sp && sp->njobs && sp->pic_ptr == buf;
 }
 
 static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
@@ -222,7 +301,8 @@ int spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes,
     for (int i = 0; i < sp->njobs; i++)
         if (sp->jobs[i].nal_ptr == buf && sp->jobs[i].read_bytes == read_bytes) { j = &sp->jobs[i]; break; }
     if (j) {
-        if (j - sp->jobs >= sp->next) {          /* not started: parse it here instead */
+        if (!j->started) {                        /* not started: parse it here instead */
+            j->started = 1;
             pthread_mutex_unlock(&sp->mu);
             return 0;
         }

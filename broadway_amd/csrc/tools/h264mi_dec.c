@@ -21,6 +21,8 @@ static double now_s(void)
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
+static double g_t[4];   /* parse, submit, wait, copy (H264SwDecGetTiming), summed over instances */
+
 static int decode_once(const uint8_t *stream, uint32_t len, uint8_t *work, int no_reorder, FILE *fo, int *errs)
 {
     H264SwDecInst inst;
@@ -62,6 +64,9 @@ static int decode_once(const uint8_t *stream, uint32_t len, uint8_t *work, int n
         *errs += (int)pic.nbrOfErrMBs;
         if (fo) fwrite(pic.pOutputPicture, 1, size, fo);
     }
+    double t[4];
+    if (H264SwDecGetTiming(inst, &t[0], &t[1], &t[2], &t[3], NULL) == H264SWDEC_OK)
+        for (int i = 0; i < 4; i++) g_t[i] += t[i];
     H264SwDecRelease(inst);
     return pics;
 }
@@ -103,7 +108,10 @@ int main(int argc, char **argv)
     const double t1 = now_s();
     if (fo) fclose(fo);
     printf("pictures %d errors %d\n", pics, errs);
-    if (timing) printf("decode_seconds %.6f fps %.2f\n", t1 - t0, pics / (t1 - t0));
+    if (timing) {
+        printf("decode_seconds %.6f fps %.2f\n", t1 - t0, pics / (t1 - t0));
+        printf("t_parse %.6f\nt_submit %.6f\nt_wait %.6f\nt_copy %.6f\n", g_t[0], g_t[1], g_t[2], g_t[3]);
+    }
     free(buf);
     free(work);
     return errs ? 1 : 0;

@@ -119,6 +119,13 @@ void  H264SwDecMemset(void *ptr, i32 value, u32 count);                         
  * picHeight * 4 bytes; pOutput->pOutputPicture = rgba.  No reference C
  * counterpart: the reference converts in JavaScript. */
 H264SwDecRet H264SwDecNextPictureRGBA(H264SwDecInst decInst, H264SwDecPicture *pOutput, u32 flushBuffer, u8 *rgba);
+/* Extension (no reference counterpart): where an instance's time went, in
+ * seconds since H264SwDecInit -- host parse (NAL extraction, headers, CAVLC /
+ * MB layer, DPB, concealment), record upload + kernel launch, waiting for the
+ * device in NextPicture, and the output copy -- plus pictures output.  Any
+ * pointer may be NULL. */
+H264SwDecRet H264SwDecGetTiming(H264SwDecInst decInst, double *parse_s, double *submit_s, double *wait_s,
+                                double *copy_s, u32 *pictures);
 
 /* ---------------------------------------------------------------------- */
 /* 2. Broadway glue (reference Decoder/src/Decoder.c:44-185, make.py:39)   */

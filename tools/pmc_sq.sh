@@ -11,6 +11,6 @@ P2="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INS
 i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/p$i -o sq -- python3 bench.py --no-cpu-baseline --no-verify --no-e2e --steps 8 --warmup 2 "$@" > $OUT/p$i.log 2>&1 || { tail -20 $OUT/p$i.log; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/p$i -o sq -- python3 bench.py --no-cpu-baseline --no-verify --no-e2e --no-legs --steps 8 --warmup 2 "$@" > $OUT/p$i.log 2>&1 || { tail -20 $OUT/p$i.log; exit 1; }
 done
 python3 tools/pmc_sq_report.py $OUT
