@@ -987,6 +987,19 @@ __device__ __forceinline__ void st_gran(unsigned long long *p, uint32_t v, uint3
 {
     __hip_atomic_store((g_u64 *)p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// the same granules in LDS, between the two rows of one workgroup (k_wgpp
+// RPW = 2): one 8-B LDS access each, no L2 round trip
+typedef __attribute__((address_space(3))) unsigned long long l_u64;
+template <bool LDSM> __device__ __forceinline__ unsigned long long ld_granT(const unsigned long long *p)
+{
+    if (LDSM) return __hip_atomic_load((const l_u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return ld_gran(p);
+}
+template <bool LDSM> __device__ __forceinline__ void st_granT(unsigned long long *p, uint32_t v, uint32_t tag)
+{
+    if (LDSM) __hip_atomic_store((l_u64 *)p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else st_gran(p, v, tag);
+}
 
 // LDS hand-off ring between the MC waves of a row workgroup and its row
 // unit: slot c % RING_K holds MB c's MC samples, residual and deblocking
@@ -1017,6 +1030,7 @@ __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v,
 // (out of line to keep the kernel's VGPR count for 3 workgroups per CU; the
 // arguments are plain values: a reference to the kernel's ReconArgs would
 // force the whole argument block into private memory)
+template <bool UPL>
 __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const unsigned long long *mbx_up, unsigned *perr,
                                                    int W, int c, uint32_t tag, bool has_up, int lane, McScratch &M,
                                                    MbRing &R, const uint32_t *i4tab)
@@ -1043,12 +1057,12 @@ __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const uns
         const int ce = min(max(c + dsel, 0), W - 1);
         const unsigned long long *g = mbx_up + ce * 32 + dw;
         const bool mine = (lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD);
-        unsigned long long gr = ld_gran(g);
+        unsigned long long gr = ld_granT<UPL>(g);
         unsigned spins = 0;
         while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-            if (mine) gr = ld_gran(g);
+            if (mine) gr = ld_granT<UPL>(g);
         }
         top = (uint32_t)gr;
     }
@@ -1125,8 +1139,12 @@ struct __attribute__((aligned(16))) PPLds {
     unsigned long long ptw1[8];     // PROF: wave 1's phase sums, added by wave 0
 };
 
-template <bool PROF>
-__device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing *R)
+// UPL / MEL: the row above's mailbox (mbx_up) / this row's (mbx_me) is the
+// workgroup's LDS one (k_wgpp RPW = 2: the upper row of the pair publishes to
+// LDS, the lower one reads from there)
+template <bool PROF, bool UPL, bool MEL>
+__device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing *R,
+                       const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
     const int W = a.w, H = a.h;
     const PicDesc *pdp = a.pics + p;
@@ -1138,8 +1156,6 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     unsigned *perr = a.err + p;
     const uint32_t tag = a.epoch;
     const bool has_up = r > 0, has_down = r + 1 < H;
-    const unsigned long long *mbx_up = a.mbx + ((size_t)p * H + (has_up ? r - 1 : r)) * W * 32;
-    unsigned long long *mbx_me = a.mbx + ((size_t)p * H + r) * W * 32;
     const bool last_row = r == H - 1;
     typedef const __attribute__((address_space(4))) uint32_t *cu32p;
     const cu32p recw = (cu32p)(const void *)(a.rec + rec_base + r * W);   // 24 dwords per record
@@ -1273,7 +1289,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         const bool dbf = avail & DB_INNER;
         // speculative read of the row above's entry c (lanes 0..23 used)
         const unsigned long long *tga = mbx_up + c * 32 + (lane < 24 ? lane : (lane & 15));
-        unsigned long long gr = ld_gran(tga);
+        unsigned long long gr = ld_granT<UPL>(tga);
         // ---- off the chain: my region is free once MB c-1's wave read MB c-2's
         {
             unsigned spins = 0;
@@ -1338,7 +1354,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }
-                if (mine) gr = ld_gran(tga);
+                if (mine) gr = ld_granT<UPL>(tga);
             }
             *(uint32_t *)(Lb + top_lds) = (uint32_t)gr;
             wave_sync();
@@ -1390,7 +1406,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                 const uint32_t newp = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
                 if (is_patch) ent = newp;
             }
-            st_gran(mbx_me + (size_t)c * 32 + gi, ent, tag);
+            st_granT<MEL>(mbx_me + (size_t)c * 32 + gi, ent, tag);
             if (prof && lane == 0) pmb[2] = (wall_clock64() & 0xFFFFFFFFull) | (tvd << 32);
         }
         // ---- off the chain again: frame stores, once per sample
@@ -1629,11 +1645,11 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
 // beside live row chains would lengthen the chains' L2 hand-offs).  Tail
 // workgroups come after every row workgroup in dispatch order, so no row
 // ever waits for them; the poll is bounded.
-template <int NMC>
-__device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRing &R)
+template <int NW>
+__device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRing &R, int row_wgs)
 {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wid >= NMC) return;
+    if (wid >= NW) return;
     unsigned spins = 0;
     while (__hip_atomic_load(a.rows_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.prep_target) {
         __builtin_amdgcn_s_sleep(64);
@@ -1643,43 +1659,20 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
     pa.rec = a.n_rec; pa.coef = a.n_coef; pa.pics = a.n_pics; pa.dbrec = a.n_dbrec; pa.res = a.n_res;
     pa.nmbs_total = a.n_nmbs_total; pa.w = a.w; pa.h = a.h;
     const Tabs T = load_tabs(lane);
-    const int t = blockIdx.x - a.S * a.h;
-    for (int g = t * NMC + wid; g < pa.nmbs_total; g += a.prep_wgs * NMC)
+    const int t = blockIdx.x - row_wgs;
+    for (int g = t * NW + wid; g < pa.nmbs_total; g += a.prep_wgs * NW)
         prep_mb(pa, g, lane, M[wid], R.db[wid], T);
 }
 
-template <int NMC, bool PROF, bool PREP>
-__global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(NMC == 3 ? 4 : 3))) void k_wgpp(ReconArgs a)
+// MC waves of one row (picture p, MB row r): walk the row's MBs c0, c0 + NMC,
+// ... into the row's LDS ring.  UPL / MEL as row_pp: where the row above's
+// unfiltered bottom rows come from (intra) / where this row's go.
+template <int NMC, bool PROF, bool UPL, bool MEL>
+__device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing &R,
+                                       const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
-    __shared__ PPLds L;
-    __shared__ McScratch M[NMC];
-    __shared__ MbRing R;
-    const int S = a.S;
-    // blockIdx = r * S + s: the S pictures' row r are dispatched together,
-    // rows in order, so a row's workgroup only waits on earlier ones
-    if (blockIdx.x >= S * a.h) {        // tail workgroup: the next batch's k_prep
-        prep_tail<NMC>(a, M, R);
-        return;
-    }
-    const int r = blockIdx.x / S, p = blockIdx.x - r * S;
-    if (threadIdx.x < RING_K) R.flag[threadIdx.x] = 0;
-    if (threadIdx.x == 0) { R.consumed = 0; L.hdone = 0; L.copied = 0; L.pdone = 0; }
-    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2)) L.i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
-    __syncthreads();
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wid < 2) {
-        __builtin_amdgcn_s_setprio(3);
-        row_pp<PROF>(a, p, r, L, wid, lane, &R);
-        // row finished: progress for the tail workgroups' start
-        if (wid == 0 && lane == 0 && a.rows_done)
-            __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
-    McScratch &Mw = M[wid - 2];
     const PicDesc pd = a.pics[p];
     const uint32_t *recrow = (const uint32_t *)(a.rec + pd.rec_base + r * a.w);
-    const int c0 = wid - 2;
     // MB c0's record (lane i < 24: dword i) and loads; then one MB ahead
     uint32_t v0 = c0 < a.w ? recrow[(size_t)c0 * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
@@ -1699,22 +1692,18 @@ __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(
         const unsigned long long t0 = PROF ? clock64() : 0;
         const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], R.res[slot], R.db[slot]);
         if (type == MBT_IPCM) {
-            const PicDesc &pd = a.pics[p];
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
             ((uint32_t *)R.px[slot])[lane] = src[lane];
             if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
         } else if (type >= MBT_I4x4) {
-            const PicDesc &pd = a.pics[p];
-            mc_intra(a.rec + pd.rec_base + r * a.w + c, a.mbx + ((size_t)p * a.h + (r > 0 ? r - 1 : 0)) * a.w * 32,
-                     a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, L.i4tab);
+            mc_intra<UPL>(a.rec + pd.rec_base + r * a.w + c, mbx_up, a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, i4tab);
         }
         wave_sync();
         {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
             const int kk = lane & 7;
             const uint8_t *px = R.px[slot];
             const uint32_t v = *(const uint32_t *)&px[kk < 4 ? 240 + kk * 4 : kk < 6 ? 312 + (kk - 4) * 4 : 376 + (kk - 6) * 4];
-            if (r + 1 < a.h)
-                st_gran(a.mbx + ((size_t)p * a.h + r) * a.w * 32 + c * 32 + 24 + kk, v, a.epoch);
+            if (r + 1 < a.h) st_granT<MEL>(mbx_me + c * 32 + 24 + kk, v, a.epoch);
         }
         if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
@@ -1722,7 +1711,68 @@ __global__ __launch_bounds__(64 * (NMC + 2)) __attribute__((amdgpu_waves_per_eu(
         if (more) mc_issue(a, pd, r * a.w + c + NMC, v0, lane, ld);
     }
 }
-template __global__ void k_wgpp<3, false, true>(ReconArgs);
-template __global__ void k_wgpp<3, true, true>(ReconArgs);
 
-
+// RPW MB rows per workgroup (1..3), each with its own NMC MC waves, two row
+// waves, ring and region LDS.  Inside the group a row hands its bottom rows
+// to the next one through an LDS mailbox (dynamic shared memory, w * 256 B
+// per inner boundary) instead of an L2 round trip: (RPW - 1) / RPW of the
+// picture's row-to-row hand-offs become LDS ones.
+template <int NMC, bool PROF, bool PREP, int RPW>
+__global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_per_eu(NMC == 3 || RPW > 1 ? 4 : 3))) void k_wgpp(ReconArgs a)
+{
+    __shared__ PPLds L[RPW];
+    __shared__ McScratch M[RPW * NMC];
+    __shared__ MbRing R[RPW];
+    extern __shared__ unsigned long long lmbx[];
+    const int S = a.S;
+    const int hg = (a.h + RPW - 1) / RPW;
+    // blockIdx = g * S + s: the S pictures' row group g are dispatched
+    // together, groups in order, so a row's workgroup only waits on earlier ones
+    if (blockIdx.x >= S * hg) {        // tail workgroup: the next batch's k_prep
+        prep_tail<NMC * RPW>(a, M, R[0], S * hg);
+        return;
+    }
+    const int g = blockIdx.x / S, p = blockIdx.x - g * S;
+    for (int q = 0; q < RPW; q++) {
+        if (threadIdx.x < RING_K) R[q].flag[threadIdx.x] = 0;
+        if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; }
+    }
+    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2) * RPW) L[0].i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
+    if (RPW > 1)        // granule tags from an earlier workgroup on this CU must not match
+        for (int e = threadIdx.x; e < (RPW - 1) * a.w * 32; e += 64 * (NMC + 2) * RPW) lmbx[e] = 0;
+    __syncthreads();
+    const int wid0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int q = RPW == 1 ? 0 : wid0 / (NMC + 2), wid = wid0 - q * (NMC + 2);
+    const int r = g * RPW + q;
+    if (r >= a.h) return;
+    const size_t W32 = (size_t)a.w * 32;
+    // mailboxes: the group's first row reads the row above from L2, its last
+    // row publishes there; inner boundaries use lmbx[(q - 1) * W32 ..]
+    const bool upl = q > 0, mel = q < RPW - 1;
+    unsigned long long *const up = upl ? lmbx + (q - 1) * W32 : a.mbx + ((size_t)p * a.h + (r > 0 ? r - 1 : 0)) * W32;
+    unsigned long long *const me = mel ? lmbx + q * W32 : a.mbx + ((size_t)p * a.h + r) * W32;
+    if (wid < 2) {
+        __builtin_amdgcn_s_setprio(3);
+        if (!upl && !mel) row_pp<PROF, false, false>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else if (!upl) row_pp<PROF, false, true>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else if (mel) row_pp<PROF, true, true>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else row_pp<PROF, true, false>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        // row finished: progress for the tail workgroups' start
+        if (wid == 0 && lane == 0 && a.rows_done)
+            __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
+    McScratch &Mw = M[q * NMC + wid - 2];
+    if (!upl && !mel) mc_row<NMC, PROF, false, false>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (!upl) mc_row<NMC, PROF, false, true>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (mel) mc_row<NMC, PROF, true, true>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else mc_row<NMC, PROF, true, false>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+}
+template __global__ void k_wgpp<3, false, true, 1>(ReconArgs);
+template __global__ void k_wgpp<3, true, true, 1>(ReconArgs);
+template __global__ void k_wgpp<3, false, true, 2>(ReconArgs);
+template __global__ void k_wgpp<3, true, true, 2>(ReconArgs);
+template __global__ void k_wgpp<3, false, true, 3>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 2>(ReconArgs);
+template __global__ void k_wgpp<3, true, true, 3>(ReconArgs);

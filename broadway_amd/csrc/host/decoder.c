@@ -367,7 +367,10 @@ static int finish_picture(H264Dec *d, int concealed_mbs)
 {
     const Sps *sps = &d->sps[d->active_sps];
     const double t0 = h264dec_now();
-    const int rc = d->be.decode(d->be.ctx, &d->pb, d->cur_slot);
+    int rc = d->be.decode(d->be.ctx, &d->pb, d->cur_slot);
+    /* the picture's output copy starts now, behind its reconstruction */
+    if (!rc && d->be.prefetch && d->out_frames)
+        rc = d->be.prefetch(d->be.ctx, d->cur_slot, d->out_frames + d->frame_bytes * (size_t)d->cur_slot);
     d->t_submit += h264dec_now() - t0;
     if (rc) return DEC_FAIL(DEC_ERROR);
     d->pics_decoded++;

@@ -38,6 +38,10 @@ typedef struct H264Backend {
     /* optional: wait for the reconstructions issued so far (timing split of
      * the output path into device wait and copy) */
     int  (*sync)(void *ctx);
+    /* optional: start copying slot to dst (host memory) behind the
+     * reconstructions issued so far; a later read of the same slot into the
+     * same dst then only waits for that copy (the D2H overlaps host work) */
+    int  (*prefetch)(void *ctx, int slot, uint8_t *dst);
     void (*destroy)(void *ctx);
 } H264Backend;
 

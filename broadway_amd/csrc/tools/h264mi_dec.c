@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/resource.h>
 
 static double now_s(void)
 {
@@ -99,6 +100,8 @@ int main(int argc, char **argv)
         H264SwDecRelease(warm);
     }
     int pics = 0, errs = 0;
+    struct rusage ru0, ru1;
+    getrusage(RUSAGE_SELF, &ru0);
     const double t0 = now_s();
     for (int k = 0; k < reps; k++) {
         const int n = decode_once(buf, (uint32_t)len, work, no_reorder, k == 0 ? fo : NULL, &errs);
@@ -106,11 +109,16 @@ int main(int argc, char **argv)
         pics += n;
     }
     const double t1 = now_s();
+    getrusage(RUSAGE_SELF, &ru1);
     if (fo) fclose(fo);
     printf("pictures %d errors %d\n", pics, errs);
     if (timing) {
         printf("decode_seconds %.6f fps %.2f\n", t1 - t0, pics / (t1 - t0));
         printf("t_parse %.6f\nt_submit %.6f\nt_wait %.6f\nt_copy %.6f\n", g_t[0], g_t[1], g_t[2], g_t[3]);
+        /* host CPU time of the whole process over the timed loop (all threads) */
+        const double cpu = (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) + 1e-6 * (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) +
+                           (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec);
+        printf("cpu_seconds %.6f\n", cpu);
     }
     free(buf);
     free(work);

@@ -81,8 +81,14 @@ def test_decoder_js_api_holds_reordered_pictures():
     assert 0 < len(got) < len(c["frames"]) and got == c["frames"][:len(got)]
 
 
-def test_engine_multistream_batch_vs_oracle_replay():
-    streams = [gen.generate(2, 40 + i, nframes=6, w_mbs=10, h_mbs=6, crop_bottom=0, slices=2, gop=4)
+@pytest.mark.parametrize("rpw", [None, "1", "2", "3"])
+def test_engine_multistream_batch_vs_oracle_replay(rpw, monkeypatch):
+    """4 streams per launch vs the oracle replay; rpw: k_wgpp rows per
+    workgroup forced (H264MI_RPW; 7 rows leave a partial last group), None =
+    the engine's choice by batch size."""
+    if rpw:
+        monkeypatch.setenv("H264MI_RPW", rpw)
+    streams = [gen.generate(2, 40 + i, nframes=6, w_mbs=10, h_mbs=7, crop_bottom=0, slices=2, gop=4)
                for i in range(4)]
     caps = [Capture(s) for s in streams]
     w, h = caps[0].w_mbs, caps[0].h_mbs
@@ -101,9 +107,13 @@ def test_engine_multistream_batch_vs_oracle_replay():
     assert eng.errors() == 0
 
 
-def test_engine_bench_streams_vs_reference():
+@pytest.mark.parametrize("rpw", [None, "3"])
+def test_engine_bench_streams_vs_reference(rpw, monkeypatch):
     """The bench workload (configs[3]: 8 concurrent 1080p streams, one picture
-    of each per launch), 12 pictures, every frame vs the reference MD5s."""
+    of each per launch), 12 pictures, every frame vs the reference MD5s; also
+    with three MB rows per k_wgpp workgroup (the large-batch layout)."""
+    if rpw:
+        monkeypatch.setenv("H264MI_RPW", rpw)
     names = [f"bench_1080p_s{s}" for s in range(100, 108)]
     caps = []
     for n in names:
