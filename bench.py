@@ -80,6 +80,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-rgba", action="store_true", help="skip the RGBA output leg")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the SURVEY §8d config 2 (720p I-only) / config 5 (2160p) legs")
+    ap.add_argument("--pipe", type=int, default=int(os.environ.get("BENCH_PIPE", "1")),
+                    help="steps per launch (1 or 2): with 2, a launch reconstructs two consecutive pictures of "
+                         "every stream and the second's rows start as the reference rows they read are final")
     ap.add_argument("--dry-run", action="store_true",
                     help="no device calls: sharding, host parse, step loop and reductions only (CPU tests)")
     return ap.parse_args(argv)
@@ -175,10 +178,10 @@ def pack(caps, npics):
     return recs, coefs, pics, rec_bytes * S, nslots
 
 
-def upload(L, caps, npics):
+def upload(L, caps, npics, packed=None):
     """pack() into HBM; returns (d_recs, d_coef, d_pics, step_rec_bytes,
     nslots, resident bytes)."""
-    recs, coefs, pics, step_rec_bytes, nslots = pack(caps, npics)
+    recs, coefs, pics, step_rec_bytes, nslots = packed or pack(caps, npics)
     d_recs = L.h264mi_device_alloc(len(recs))
     d_coef = L.h264mi_device_alloc(len(coefs))
     d_pics = L.h264mi_device_alloc(pics.nbytes)
@@ -189,6 +192,78 @@ def upload(L, caps, npics):
     assert L.h264mi_copy_h2d(d_coef, coefs, len(coefs)) == 0
     assert L.h264mi_copy_h2d(d_pics, pics.ctypes.data, pics.nbytes) == 0
     return d_recs, d_coef, d_pics, step_rec_bytes, nslots, len(recs) + len(coefs)
+
+
+def slots_read(recs, nmbs, i):
+    """DPB slots the inter MBs of packed picture i read (MbRec.ref, bytes
+    24..27 of each 96-B record; MBT_INTER = 0, MBT_SKIP = 1)."""
+    r = np.frombuffer(recs, dtype=np.uint8, count=nmbs * MBREC, offset=i * nmbs * MBREC).reshape(nmbs, MBREC)
+    inter = r[:, 0] <= 1
+    return set(np.unique(r[inter, 24:28]).tolist())
+
+
+def rename_slots(recs, pics, S, nmbs, nslots):
+    """Physical frame slots for frame-pipelined launches: the host parser's
+    DPB slot d of a stream maps to one of nslots + 1 physical slots, and a
+    picture decoded into d gets the physical slot released longest ago --
+    never the one d held before (which the previous picture may still be
+    reading, e.g. the reference the sliding window just dropped).  The
+    mapping is a bijection at every picture, so the records' reference-slot
+    comparisons (bS) are unchanged; MbRec.ref and PicDesc cur_slot /
+    frame_base are rewritten in place.  Returns the physical slot count."""
+    nphys = nslots + 1
+    n = len(pics) // S
+    arr = np.frombuffer(recs, dtype=np.uint8).reshape(-1, MBREC)
+    for s in range(S):
+        cur = {}                              # DPB slot -> physical slot
+        free = list(range(nphys))             # released order, oldest first
+        for k in range(n):
+            i = k * S + s
+            lut = np.arange(256, dtype=np.uint8)
+            for d, ph in cur.items():
+                lut[d] = ph
+            r = arr[i * nmbs:(i + 1) * nmbs]
+            inter = r[:, 0] <= 1
+            r[inter, 24:28] = lut[r[inter, 24:28]]
+            d = int(pics[i][2])
+            old = cur.get(d)
+            ph = next(x for x in free if x != old)
+            free.remove(ph)
+            if old is not None:
+                free.append(old)
+            cur[d] = ph
+            pics[i][1] = s * nphys
+            pics[i][2] = ph
+    return nphys
+
+
+def schedule(recs, pics, S, nmbs, warmup, steps, P):
+    """Launches as (first step, steps in it).  P = 2 pairs steps (2i, 2i+1)
+    when, for every stream, the pair's pictures write different slots and
+    the first does not read the slot the second writes (the engine's
+    frame-pipelined batch contract); otherwise, or when warmup / steps are
+    odd, every launch is one step."""
+    n = warmup + steps
+    if P > 1 and warmup % P == 0 and steps % P == 0:
+        ok = True
+        for k0 in range(0, n, P):
+            for s in range(S):
+                a, b = k0 * S + s, (k0 + 1) * S + s
+                if pics[a][2] == pics[b][2] or pics[b][2] in slots_read(recs, nmbs, a):
+                    ok = False
+        if ok:
+            return [(k, P) for k in range(0, n, P)]
+    return [(k, 1) for k in range(n)]
+
+
+def pack_steps(pics, S, nmbs, P):
+    """PicDesc array for P-step launches: picture j * S + s of the launch at
+    step k0 has rec_base relative to step k0's records."""
+    out = pics.copy()
+    for i in range(len(pics)):
+        k, s = divmod(i, S)
+        out[i][0] = ((k % P) * S + s) * nmbs
+    return out
 
 
 def golden_frames(config, seed, overrides):
@@ -345,25 +420,28 @@ def end_to_end(streams, nframes, reps=3):
         shutil.rmtree(td, ignore_errors=True)
 
 
-def verify_all(eng, step, caps, seeds, config, overrides, nsteps):
-    """Untimed verification pass: decode steps [0, nsteps) again and compare
-    every picture of every stream with the reference decoder's MD5s (POC
-    type 2: output order == decode order, frame k = picture k).  Returns
-    (ok, frames checked, frames without a fixture)."""
+def verify_all(eng, launch, sched, caps, seeds, config, overrides, cur_slots=None):
+    """Untimed verification pass: run every launch of the schedule again and
+    compare every picture of every stream with the reference decoder's MD5s
+    (POC type 2: output order == decode order, frame k = picture k) right
+    after its launch (the pictures of one launch write distinct slots).
+    Returns (ok, frames checked, frames without a fixture)."""
     refs = [golden_frames(config, sd, overrides) for sd in seeds]
     ok, n, missing = True, 0, 0
-    for k in range(nsteps):
-        step(k)
+    for i, (k0, P) in enumerate(sched):
+        launch(i)
         eng.sync()
-        for s, c in enumerate(caps):
-            ref = refs[s]
-            if ref is None or k >= len(ref):
-                missing += 1
-                continue
-            got = hashlib.md5(eng.read(s, c.pictures[k].cur_slot).tobytes()).hexdigest()
-            n += 1
-            if got != ref[k]:
-                ok = False
+        for k in range(k0, k0 + P):
+            for s, c in enumerate(caps):
+                ref = refs[s]
+                if ref is None or k >= len(ref):
+                    missing += 1
+                    continue
+                slot = c.pictures[k].cur_slot if cur_slots is None else int(cur_slots[k][s])
+                got = hashlib.md5(eng.read(s, slot).tobytes()).hexdigest()
+                n += 1
+                if got != ref[k]:
+                    ok = False
     return ok, n, missing
 
 
@@ -391,6 +469,12 @@ class _DryEngine:
     def decode_device_next(self, *a):
         self.launches += 1
 
+    def decode_device_steps(self, *a):
+        self.launches += 1
+
+    def set_steps(self, *a):
+        pass
+
     def sync(self):
         pass
 
@@ -408,6 +492,71 @@ class _DryEngine:
 
     def close(self):
         pass
+
+
+class DeviceRun:
+    """The bench's device-resident path for one rank: records, coefficient
+    blocks and descriptors of pictures [0, warmup + steps) of every stream in
+    HBM, an engine for the S streams, and the launch schedule (P steps per
+    launch when the streams allow it, physical slots renamed for it; the next
+    launch's k_prep in each launch's tail).  dry: no device calls."""
+
+    def __init__(self, L, caps, warmup, steps, pipe, device=0, dry=False):
+        self.L, self.S = L, len(caps)
+        S, nframes = self.S, warmup + steps
+        w, h = caps[0].w_mbs, caps[0].h_mbs
+        nmbs = w * h
+        packed = pack(caps, nframes)
+        recs_h, _, pics_h, self.srb, nslots = packed
+        if pipe > 1:
+            nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots)
+            packed = packed[:4] + (nslots,)
+        self.sched = schedule(recs_h, pics_h, S, nmbs, warmup, steps, pipe)
+        self.P = self.sched[0][1]
+        self.cur_slots = pics_h[:, 2].reshape(nframes, S).copy()
+        self.bufs = []
+        if dry:
+            self.d_recs = self.d_coef = self.pics_base = 0
+            self.resident = 0
+            self.eng = _DryEngine()
+            return
+        from broadway_amd.engine import Engine
+        self.d_recs, self.d_coef, d_pics, _, nslots, self.resident = upload(L, caps, nframes, packed)
+        self.bufs = [self.d_recs, self.d_coef, d_pics]
+        self.pics_base = d_pics
+        if self.P > 1:
+            ps = pack_steps(pics_h, S, nmbs, self.P)
+            d = L.h264mi_device_alloc(ps.nbytes)
+            assert d and L.h264mi_copy_h2d(d, ps.ctypes.data, ps.nbytes) == 0
+            self.bufs.append(d)
+            self.pics_base = d
+        self.eng = Engine(w, h, S, nslots, device=device)
+        if self.P > 1:
+            self.eng.set_steps(self.P)
+
+    def launch(self, i):
+        """Launch i of the schedule: P steps; the next launch's k_prep runs
+        in its tail workgroups."""
+        S, srb = self.S, self.srb
+        k0, p = self.sched[i]
+        args = (self.d_recs + k0 * srb, self.d_coef, self.pics_base + k0 * S * 32)
+        if i + 1 < len(self.sched):
+            k1 = self.sched[i + 1][0]
+            self.eng.decode_device_steps(S, p, *args, self.d_recs + k1 * srb, self.d_coef,
+                                         self.pics_base + k1 * S * 32)
+        else:
+            self.eng.decode_device_steps(S, p, *args)
+
+    def close_engine(self):
+        if self.eng is not None:
+            self.eng.close()
+            self.eng = None
+
+    def free(self):
+        self.close_engine()
+        for p in self.bufs:
+            self.L.h264mi_device_free(p)
+        self.bufs = []
 
 
 def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3):
@@ -449,7 +598,7 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3):
         launch_us = us / max(nb, 1)
         r_alg = sum(c.pictures[k].alg_ref_bytes + 32 * c.pictures[k].n_coded + MBREC * w * h
                     for c in caps for k in range(warmup, nframes)) / steps
-        ok, n, missing = verify_all(eng, step, caps, seeds, config, {}, nframes)
+        ok, n, missing = verify_all(eng, step, [(k, 1) for k in range(nframes)], caps, seeds, config, {})
         gbs = r_alg / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
         return {"size": f"{w * 16}x{h * 16}", "streams": S, "seeds": seeds, "steps": steps,
                 "mc_waves_per_row_workgroup": mc_waves,
@@ -495,29 +644,16 @@ def main(argv=None):
     streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= nframes for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    if a.dry_run:
-        d_recs = d_coef = d_pics = 0
-        _, _, _, step_rec_bytes, nslots = pack(caps, nframes)
-        resident = 0
-        eng = _DryEngine()
-    else:
-        from broadway_amd.engine import Engine
-        d_recs, d_coef, d_pics, step_rec_bytes, nslots, resident = upload(L, caps, nframes)
-        eng = Engine(w, h, S, nslots, device=local)
+    run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run)
+    if not a.dry_run:
         torch.cuda.set_device(local)
+    eng, sched, launch, P, resident = run.eng, run.sched, run.launch, run.P, run.resident
     t_prep = time.perf_counter() - t_prep
     sync = (lambda: None) if a.dry_run else torch.cuda.synchronize
 
-    def step(k):
-        # the next step's k_prep runs in this launch's tail workgroups
-        if k + 1 < nframes:
-            eng.decode_device_next(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32,
-                                   d_recs + (k + 1) * step_rec_bytes, d_coef, d_pics + (k + 1) * S * 32)
-        else:
-            eng.decode_device(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32)
-
-    for k in range(a.warmup):
-        step(k)
+    nwarm = sum(1 for k0, _ in sched if k0 < a.warmup)
+    for i in range(nwarm):
+        launch(i)
     eng.sync()
     sync()
     # HIP events around every 4th launch, carried by k_wgpp's own dispatch
@@ -528,8 +664,8 @@ def main(argv=None):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
-    for k in range(a.warmup, a.warmup + a.steps):
-        step(k)
+    for i in range(nwarm, len(sched)):
+        launch(i)
     eng.sync()
     sync()
     if dist:
@@ -549,7 +685,7 @@ def main(argv=None):
         for k in range(a.warmup, a.warmup + a.steps):
             p = c.pictures[k]
             r_alg += p.alg_ref_bytes + 32 * p.n_coded + MBREC * c.w_mbs * c.h_mbs
-    launch_bytes = r_alg / a.steps
+    launch_bytes = r_alg / (len(sched) - nwarm)
     step_us = rows_us / max(nb, 1)
     achieved = launch_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
     traffic = load_traffic()
@@ -557,7 +693,7 @@ def main(argv=None):
 
     ok, n_checked, n_missing = None, 0, 0
     if not a.no_verify and not a.dry_run:
-        ok, n_checked, n_missing = verify_all(eng, step, caps, seeds, a.config, overrides, nframes)
+        ok, n_checked, n_missing = verify_all(eng, launch, sched, caps, seeds, a.config, overrides, run.cur_slots)
     n_checked_all = int(reduce_over_ranks(dist, torch, n_checked, "sum"))
     n_missing_all = int(reduce_over_ranks(dist, torch, n_missing, "sum"))
     ok_all = None if ok is None else reduce_over_ranks(dist, torch, 0.0 if ok else 1.0, "max") == 0.0
@@ -567,7 +703,7 @@ def main(argv=None):
     cpu = None
     if rank == 0 and not a.no_cpu_baseline and not a.dry_run:
         cpu = cpu_baseline(streams, nframes)
-    eng.close()
+    run.close_engine()
     legs = None
     if rank == 0 and world == 1 and not a.no_legs and not a.dry_run:
         legs = config_legs(L, torch)
@@ -596,8 +732,8 @@ def main(argv=None):
                        "frames_per_stream_timed": a.steps,
                        "seeds": f"100..{100 + S * world - 1}",
                        "parallelism": f"streams sharded {S}/GPU over {world} rank(s), no collective; "
-                                      f"one picture of each stream per launch"},
-            "roofline": {"kernel": "k_wgpp (one launch = one step; k_prep of the next step runs beside it)",
+                                      f"{P} consecutive picture(s) of each stream per launch"},
+            "roofline": {"kernel": f"k_wgpp (one launch = {P} step(s); k_prep of the next launch runs in its tail)",
                          # what limits the kernel: the MB-row deblocking dependency chain
                          # (SQ counters profiles/r19_sq_s8.json), not HBM;
                          # `frac` is still quoted against the HBM peak, the metric's axis
@@ -611,7 +747,8 @@ def main(argv=None):
                          "avg_launch_kernel_us": round(step_us, 2),
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
-            "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S,
+            "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S * P,
+                                   "steps_per_launch": P,
                                    "timed_launches": nb,
                                    "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}},
             "wall_read_GBs": round(frame_read_gbs, 2),
@@ -630,9 +767,7 @@ def main(argv=None):
         if a.dry_run:
             line["dry_run"] = {"launches": eng.launches, "seeds": seeds}
         print(json.dumps(line), flush=True)
-    if not a.dry_run:
-        for p in (d_recs, d_coef, d_pics):
-            L.h264mi_device_free(p)
+    run.free()
     if dist:
         dist.destroy_process_group()
 

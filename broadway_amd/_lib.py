@@ -142,6 +142,10 @@ def mi() -> C.CDLL:
     L.h264mi_engine_decode_device.restype = i32
     L.h264mi_engine_decode_device_next.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.h264mi_engine_decode_device_next.restype = i32
+    L.h264mi_engine_decode_device_steps.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp]
+    L.h264mi_engine_decode_device_steps.restype = i32
+    L.h264mi_engine_set_steps.argtypes = [vp, i32]
+    L.h264mi_engine_set_steps.restype = i32
     L.h264mi_engine_read.argtypes = [vp, i32, i32, vp]
     L.h264mi_engine_read.restype = i32
     L.h264mi_engine_read_rgba.argtypes = [vp, i32, i32, vp]

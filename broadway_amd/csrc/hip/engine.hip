@@ -65,6 +65,8 @@ struct h264mi_engine {
     int tev_cap, tev_n;
     int tev_stride, tev_seq;  // record every tev_stride-th launch (h264mi_engine_set_timing_stride)
     uint8_t *d_rgba;          // h264mi_engine_read_rgba staging (w*h*4 B, allocated on first use)
+    int steps;                // pictures per stream per launch (h264mi_engine_set_steps)
+    unsigned *d_done;         // per picture row of a launch: epoch tag once the row is final in its slot
 };
 
 // per-picture buffers of one launch (deblocking records, residuals, row
@@ -72,8 +74,9 @@ struct h264mi_engine {
 static void free_pic_buffers(h264mi_engine *e)
 {
     (void)hipFree(e->d_mbx); (void)hipFree(e->d_dbrec); (void)hipFree(e->d_res); (void)hipFree(e->d_err);
+    (void)hipFree(e->d_done);
     (void)hipHostFree(e->h_err);
-    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL;
+    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL; e->d_done = NULL;
     e->h_err = NULL;
     e->pipe_cap = 0;
 }
@@ -85,11 +88,13 @@ static int alloc_pic_buffers(h264mi_engine *e, int cap)
               hipMalloc(&e->d_dbrec, 2 * mbs * 64) == hipSuccess &&
               hipMalloc(&e->d_res, 2 * mbs * 768) == hipSuccess &&
               hipMalloc(&e->d_err, sizeof(unsigned) * np) == hipSuccess &&
+              hipMalloc(&e->d_done, sizeof(unsigned) * np * e->h) == hipSuccess &&
               hipHostMalloc(&e->h_err, sizeof(unsigned) * np, hipHostMallocDefault) == hipSuccess;
     if (!ok) { free_pic_buffers(e); return -1; }
     // cleared granules carry epoch 0, which no launch uses
     (void)hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st);
     (void)hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * np, e->st);
+    (void)hipMemsetAsync(e->d_done, 0, sizeof(unsigned) * np * e->h, e->st);
     memset(e->h_err, 0, sizeof(unsigned) * np);
     e->pipe_cap = cap;
     return 0;
@@ -113,6 +118,7 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->dev = device;
     e->w = w_mbs; e->h = h_mbs; e->nmbs = w_mbs * h_mbs;
     e->nstreams = nstreams; e->nslots = nslots;
+    e->steps = 1;
     e->frame_bytes = (size_t)e->nmbs * 384;
     e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
     e->h_coef_cap = e->coef_cap;
@@ -207,10 +213,11 @@ static int launch_prep(h264mi_engine *e, int npics, const MbRec *d_rec, const in
 // known (next_rec != NULL), tail workgroups that run the next batch's k_prep
 // as this launch's rows drain.  k_prep outputs alternate between two buffer
 // halves; stream order separates writer and reader.
-static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const int16_t *d_coef,
+static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, const int16_t *d_coef,
                         const PicDesc *d_pics, const MbRec *next_rec, const int16_t *next_coef,
                         const PicDesc *next_pics)
 {
+    const int npics = S * P;
     const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
     const int hb = e->prep_parity;
     if (!(e->prepped_rec && e->prepped_rec == (const void *)d_rec && e->prepped_pics == (const void *)d_pics))
@@ -226,6 +233,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     if (++e->epoch >= (1u << 20)) {           // granule tags: epoch in the high dword
         if (h264mi_engine_sync(e)) return -1;
         HIPCHECK(hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_done, 0, sizeof(unsigned) * e->pipe_cap * e->h, e->st));
         e->epoch = 1;
     }
     a.epoch = e->epoch;
@@ -234,7 +242,9 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     a.npics = npics;
     a.w = e->w; a.h = e->h;
     a.err = e->d_err;
-    a.S = npics;
+    a.S = S;
+    a.P = P;
+    a.done = e->d_done;
     a.dbrec = e->d_dbrec + hb * mbs * 64;
     a.res = e->d_res + hb * mbs * 384;
     const int rows = npics * e->h;
@@ -263,7 +273,7 @@ static int launch_batch(h264mi_engine *e, int npics, const MbRec *d_rec, const i
     // bound and three chains on one CU contend; beyond that, three rows per
     // workgroup with LDS hand-offs inside (measured, 1080p: S = 8 410 vs
     // 440 us per launch; S = 32 1368 vs 1113 us)
-    int rpw = e->rpw_env ? e->rpw_env : (rows > 3 * e->ncu ? 3 : 1);
+    int rpw = e->rpw_env ? e->rpw_env : (S * e->h > 3 * e->ncu ? 3 : 1);
     if (rpw > e->rpw_max) rpw = e->rpw_max;
     if (e->mc_waves == 2 && rpw > 2) rpw = 2;
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
@@ -309,7 +319,6 @@ extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stre
     HIPCHECK(hipSetDevice(e->dev));
     // staging buffers are reused: wait until the previous upload consumed them
     HIPCHECK(hipEventSynchronize(e->ev_staged));
-    for (int i = 0; i < npics; i++) e->err_accum += 0;
     size_t total = 0;
     for (int i = 0; i < npics; i++) total += ncoef[i];
     if (total + 16 > e->coef_cap) {
@@ -338,7 +347,7 @@ extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stre
     if (cbase) HIPCHECK(hipMemcpyAsync(e->d_coef, e->h_coef, cbase * 32, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipMemcpyAsync(e->d_pics, e->h_pics, sizeof(PicDesc) * npics, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipEventRecord(e->ev_staged, e->st));
-    return launch_batch(e, npics, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
+    return launch_batch(e, npics, 1, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
 }
 
 extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
@@ -354,8 +363,37 @@ extern "C" int h264mi_engine_decode_device_next(h264mi_engine *e, int npics, con
     if (!e || npics < 1 || npics > e->nstreams || !d_recs || !d_pics) return -1;
     if (next_recs && !next_pics) return -1;
     HIPCHECK(hipSetDevice(e->dev));
-    return launch_batch(e, npics, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
+    return launch_batch(e, npics, 1, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
                         next_coef, (const PicDesc *)next_pics);
+}
+
+// frame-pipelined batches: P (<= the engine's steps) consecutive pictures of
+// each of S streams in one launch, step-major (descriptor j * S + s), every
+// PicDesc.rec_base relative to d_recs; the caller guarantees that no picture
+// of the batch writes a slot an earlier picture of the batch reads or writes
+extern "C" int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P, const void *d_recs,
+                                                 const int16_t *d_coef, const void *d_pics, const void *next_recs,
+                                                 const int16_t *next_coef, const void *next_pics)
+{
+    if (!e || S < 1 || S > e->nstreams || P < 1 || P > e->steps || !d_recs || !d_pics) return -1;
+    if (next_recs && !next_pics) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    return launch_batch(e, S, P, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
+                        next_coef, (const PicDesc *)next_pics);
+}
+
+extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)
+{
+    if (!e || steps < 1 || steps > 2) return -1;
+    if (steps == e->steps) return 0;
+    if (h264mi_engine_sync(e)) return -1;
+    free_pic_buffers(e);
+    if (alloc_pic_buffers(e, e->nstreams * steps)) return -1;
+    e->steps = steps;
+    e->prepped_rec = NULL; e->prepped_pics = NULL;
+    e->prep_parity = 0;
+    HIPCHECK(hipStreamSynchronize(e->st));
+    return 0;
 }
 
 extern "C" const char *h264mi_engine_kernel(h264mi_engine *e)
@@ -451,7 +489,7 @@ extern "C" int h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long
                            hipMemcpyDeviceToHost));
     }
     if (enable && !e->d_prof) {
-        e->prof_cap = (size_t)e->nstreams * e->h * 16 + (size_t)e->nstreams * e->nmbs * 4;
+        e->prof_cap = (size_t)e->pipe_cap * e->h * 16 + (size_t)e->pipe_cap * e->nmbs * 4;
         HIPCHECK(hipMalloc(&e->d_prof, sizeof(unsigned long long) * e->prof_cap));
         HIPCHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * e->prof_cap));
     } else if (!enable && e->d_prof) {

@@ -50,6 +50,13 @@ struct ReconArgs {
     uint8_t *n_dbrec;
     int16_t *n_res;
     int n_nmbs_total;
+    // frame-pipelined launches (P > 1): the launch holds P consecutive
+    // pictures of each of the S streams, step-major (picture p = j * S + s);
+    // step j's MC reads of a slot written by step j - k of the same launch
+    // wait for that picture's rows (done[(p - k * S) * h + r] == epoch, set
+    // by row r's workgroup after its frame stores and an agent release)
+    int P;
+    unsigned int *done;
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -1134,7 +1141,7 @@ struct __attribute__((aligned(16))) PPRegion {
 struct __attribute__((aligned(16))) PPLds {
     PPRegion G[2];
     uint8_t junk[2][256];
-    int hdone, copied, pdone;
+    int hdone, copied, pdone, fin;
     uint32_t i4tab[9 * 16];
     unsigned long long ptw1[8];     // PROF: wave 1's phase sums, added by wave 0
 };
@@ -1638,6 +1645,63 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     return rtype;
 }
 
+// Frame-pipelined launches (a.P > 1): before MB mb's reference loads are
+// issued, wait until every 128-B line they touch is final in the slots that
+// earlier steps of this launch reconstruct.  Row r of a picture is final in
+// memory once row workgroups 0..r+1 are done (row r+1 stores row r's rows
+// 12..15 after its top-edge filter; the last row stores its own).  A line
+// is only read once all of its bytes are final, so no CU's L1 and no XCD's
+// L2 ever holds a stale copy of it (the producer's release writes its L2
+// back; lines from earlier launches were dropped at kernel start), and the
+// loads themselves stay plain.  known[k]: leading row workgroups of the
+// step j - k picture seen done by this wave.
+// in-launch producers a picture can wait on: one (steps per launch <= 2);
+// with more, the MC waves' state spills past their 128 VGPRs
+#define DEP_MAX 1
+struct DepState {
+    int n;                 // in-launch producers of this picture: steps j-1 .. j-n
+    uint32_t slot[DEP_MAX];  // their target slots
+    int pic[DEP_MAX];        // their picture indices
+    int known[DEP_MAX];
+};
+
+__device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0, int lane, DepState &D)
+{
+    // the record's dwords 4..6 (wave-uniform): per 8x8 partition the last MB
+    // row of its reference slot that its MC lines touch (MbRec.i4 of an
+    // inter MB, filled by the host) and the slot
+    const uint32_t d0 = rec_dw(v0, 0);
+    if ((d0 & 255) >= MBT_I4x4) return;
+    const uint32_t rw01 = rec_dw(v0, 4), rw23 = rec_dw(v0, 5), refs = rec_dw(v0, 6);
+#pragma unroll
+    for (int k = 0; k < DEP_MAX; k++) {
+        if (k >= D.n) break;
+        // leading row workgroups of producer k this MB needs done
+        int need = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t row = ((q < 2 ? rw01 : rw23) >> ((q & 1) * 16)) & 0xFFFF;
+            if (((refs >> (q * 8)) & 255) == D.slot[k]) need = max(need, (int)row + 2);
+        }
+        need = min(need, a.h);
+        unsigned spins = 0;
+        while (need > D.known[k]) {
+            const int idx = D.known[k] + lane;
+            const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic[k] * a.h + idx) == a.epoch;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+            const int adv = __builtin_amdgcn_readfirstlane(~m ? __builtin_ctzll(~m) : 64);
+            D.known[k] = min(D.known[k] + adv, a.h);
+            if (adv == 0) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known[k] = a.h; }
+            }
+        }
+    }
+    // order the reference loads after the polls (compiler: the polls are
+    // relaxed atomics; hardware: the wave issues in order)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // k_wgpp tail workgroup: waves 0..NMC-1 run the next batch's k_prep over a
 // grid-stride share of its MBs, in the LDS of the MC scratch and ring (unused
 // by a tail workgroup), once enough row workgroups of this and earlier
@@ -1673,9 +1737,23 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
 {
     const PicDesc pd = a.pics[p];
     const uint32_t *recrow = (const uint32_t *)(a.rec + pd.rec_base + r * a.w);
+    DepState D;
+    D.n = 0;
+    if (a.P > 1) {
+        const int S = a.S, j = p / S;
+#pragma unroll
+        for (int k = 1; k <= DEP_MAX; k++) {
+            if (k > j) break;
+            D.pic[D.n] = p - k * S;
+            D.slot[D.n] = __builtin_amdgcn_readfirstlane(a.pics[p - k * S].cur_slot);
+            D.known[D.n] = 0;
+            D.n++;
+        }
+    }
     // MB c0's record (lane i < 24: dword i) and loads; then one MB ahead
     uint32_t v0 = c0 < a.w ? recrow[(size_t)c0 * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
+    if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
     if (c0 < a.w) mc_issue(a, pd, r * a.w + c0, v0, lane, ld);
     for (int c = c0; c < a.w; c += NMC) {
         const int slot = c & (RING_K - 1);
@@ -1708,6 +1786,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
         v0 = nv0;
+        if (more && D.n) dep_wait(a, p, v0, lane, D);
         if (more) mc_issue(a, pd, r * a.w + c + NMC, v0, lane, ld);
     }
 }
@@ -1726,16 +1805,19 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     extern __shared__ unsigned long long lmbx[];
     const int S = a.S;
     const int hg = (a.h + RPW - 1) / RPW;
-    // blockIdx = g * S + s: the S pictures' row group g are dispatched
-    // together, groups in order, so a row's workgroup only waits on earlier ones
-    if (blockIdx.x >= S * hg) {        // tail workgroup: the next batch's k_prep
-        prep_tail<NMC * RPW>(a, M, R[0], S * hg);
+    // blockIdx = (j * hg + g) * S + s: step j's pictures (one per stream)
+    // come before step j + 1's, and within a step the S pictures' row group
+    // g are dispatched together, groups in order -- so a row's workgroup
+    // only waits on earlier ones (the row above, an earlier step's rows)
+    if (blockIdx.x >= a.npics * hg) {  // tail workgroup: the next batch's k_prep
+        prep_tail<NMC * RPW>(a, M, R[0], a.npics * hg);
         return;
     }
-    const int g = blockIdx.x / S, p = blockIdx.x - g * S;
+    const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
+    const int j = jg / hg, g = jg - j * hg, p = j * S + s;
     for (int q = 0; q < RPW; q++) {
         if (threadIdx.x < RING_K) R[q].flag[threadIdx.x] = 0;
-        if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; }
+        if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
     for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2) * RPW) L[0].i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
     if (RPW > 1)        // granule tags from an earlier workgroup on this CU must not match
@@ -1760,6 +1842,20 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
         // row finished: progress for the tail workgroups' start
         if (wid == 0 && lane == 0 && a.rows_done)
             __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (j + 1 < a.P) {
+            // a later step of this launch may read this picture: once both
+            // row waves' frame stores have completed, the second wave writes
+            // the XCD's L2 back and tags the row done
+            drain_vm();
+            int last = 0;
+            if (lane == 0) last = __hip_atomic_fetch_add(&L[q].fin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            last = __builtin_amdgcn_readfirstlane(last);
+            if (last == 1 && lane == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_sc1_u32(a.done + (size_t)p * a.h + r, a.epoch);
+            }
+        }
         return;
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");

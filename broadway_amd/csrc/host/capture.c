@@ -39,6 +39,61 @@ static int cap_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
     return 0;
 }
 
+/* Last MB row of a w x h-MB I420 slot that the 128-B lines holding bytes
+ * [first, last] of the slot touch.  Lines run in address order, so that is
+ * the row at the end of the last byte's line -- except for a line that
+ * crosses the Cb/Cr boundary (w * h odd), which holds Cb's last row even
+ * where the bytes read are Cr's top row.  The kernel's frame-pipelined
+ * dependency wait relies on it (a line is read only once all its rows are
+ * final). */
+static int line_rows(long long first, long long last, int W16, int H16, int h)
+{
+    const long long ysz = (long long)W16 * H16, csz = ysz >> 2, bnd = ysz + csz;
+    const long long le = last | 127;
+    int r;
+    if ((bnd & 127) && (first & ~127ll) <= (bnd & ~127ll) && le >= bnd) return h - 1;
+    if (le < ysz) return (int)(le / W16) >> 4;
+    r = (int)((le < bnd ? le - ysz : le - bnd) / (W16 / 2)) >> 3;
+    return r < h - 1 ? r : h - 1;
+}
+
+static int clampi(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* per inter MB and 8x8 partition: the last reference-slot MB row its MC
+ * reads (luma 9 rows x 12 bytes per 4x4 block, chroma 3 rows x 8 bytes per
+ * 2x2 block and plane, windows clamped as in the kernel's mc_issue) */
+static void set_ref_rows(MbRec *recs, int w, int h)
+{
+    static const int bx[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
+    static const int by[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
+    const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2;
+    for (int mb = 0; mb < w * h; mb++) {
+        MbRec *r = &recs[mb];
+        if (r->type != MBT_INTER && r->type != MBT_SKIP) continue;
+        const int mbx = mb % w, mby = mb / w;
+        uint16_t rows[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 16; b++) {
+            const int mvx = r->mv[b][0], mvy = r->mv[b][1];
+            const int lx0 = mbx * 16 + bx[b] * 4 + (mvx >> 2) - 2;
+            const int lax = clampi(0, W16 - 12, lx0 & ~3);
+            const int ly = clampi(0, H16 - 1, mby * 16 + by[b] * 4 + (mvy >> 2) - 2 + 8);
+            int n = line_rows((long long)ly * W16 + lax, (long long)ly * W16 + lax + 11, W16, H16, h);
+            const int cx0 = mbx * 8 + bx[b] * 2 + (mvx >> 3);
+            const int cax = clampi(0, CW - 8, cx0 & ~3);
+            const int cy0 = mby * 8 + by[b] * 2 + (mvy >> 3);
+            for (int comp = 0; comp < 2; comp++)
+                for (int wy = 0; wy < 3; wy++) {
+                    const long long o = (long long)W16 * H16 + (long long)comp * CW * CH +
+                                        (long long)clampi(0, CH - 1, cy0 + wy) * CW + cax;
+                    const int nc = line_rows(o, o + 7, W16, H16, h);
+                    if (nc > n) n = nc;
+                }
+            if (n > rows[b >> 2]) rows[b >> 2] = (uint16_t)n;
+        }
+        memcpy(r->i4, rows, 8);
+    }
+}
+
 static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
 {
     struct h264mi_capture *c = (struct h264mi_capture *)vctx;
@@ -75,6 +130,7 @@ static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
     p->n_intra = pb->n_intra;
     p->n_coded = pb->n_coded_blocks;
     memcpy(c->recs + c->nrec, pb->rec, sizeof(MbRec) * nmbs);
+    set_ref_rows(c->recs + c->nrec, c->w, c->h);
     if (pb->ncoef) memcpy(c->coefs + c->ncoef * 16, pb->coef, (size_t)pb->ncoef * 32);
     c->nrec += nmbs;
     c->ncoef += pb->ncoef;

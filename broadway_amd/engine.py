@@ -107,6 +107,20 @@ class Engine:
                                                     n_recs, n_coef, n_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device_next failed")
 
+    def set_steps(self, steps: int) -> None:
+        """Pictures per stream per launch for decode_device_steps (1..2)."""
+        if self._L.h264mi_engine_set_steps(self._h, steps) != 0:
+            raise RuntimeError("h264mi_engine_set_steps failed")
+
+    def decode_device_steps(self, S: int, P: int, d_recs: int, d_coef: int, d_pics: int,
+                            n_recs: int = 0, n_coef: int = 0, n_pics: int = 0) -> None:
+        """P consecutive pictures of each of S streams in one launch
+        (descriptors step-major, rec_base relative to d_recs); the next
+        batch's k_prep in this launch's tail when n_recs is given."""
+        if self._L.h264mi_engine_decode_device_steps(self._h, S, P, d_recs, d_coef, d_pics,
+                                                     n_recs or None, n_coef or None, n_pics or None) != 0:
+            raise RuntimeError("h264mi_engine_decode_device_steps failed")
+
     def read(self, stream: int, slot: int) -> np.ndarray:
         out = np.empty(self.frame_bytes, dtype=np.uint8)
         if self._L.h264mi_engine_read(self._h, stream, slot, out.ctypes.data) != 0:

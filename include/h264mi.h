@@ -168,6 +168,18 @@ int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs,
 int h264mi_engine_decode_device_next(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
                                      const void *d_pics, const void *next_recs, const int16_t *next_coef,
                                      const void *next_pics);
+/* Frame-pipelined batch: P consecutive pictures of each of S streams in one
+ * launch, descriptors step-major (j * S + s), every PicDesc.rec_base relative
+ * to d_recs.  A picture reading a slot that an earlier picture of the batch
+ * reconstructs waits, per 128-B line of its reference windows, for those rows
+ * to be final (device row tags), so the later picture's top rows overlap the
+ * earlier one's bottom rows.  The caller guarantees that no picture of the
+ * batch writes a slot an earlier picture of the batch reads or writes.
+ * P <= the engine's steps (h264mi_engine_set_steps, 1..2; default 1). */
+int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P, const void *d_recs, const int16_t *d_coef,
+                                      const void *d_pics, const void *next_recs, const int16_t *next_coef,
+                                      const void *next_pics);
+int h264mi_engine_set_steps(h264mi_engine *e, int steps);
 
 int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */
 /* D2H of a slot as RGBA (w*16 * h*16 * 4 bytes), converted on the GPU

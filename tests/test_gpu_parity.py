@@ -132,34 +132,55 @@ def test_engine_bench_streams_vs_reference(rpw, monkeypatch):
     assert eng.errors() == 0
 
 
-@pytest.mark.parametrize("rank", range(8))
-def test_configs3_shard_vs_reference(rank):
+@pytest.mark.parametrize("rank,pipe", [(r, 2) for r in range(8)] + [(0, 1)])
+def test_configs3_shard_vs_reference(rank, pipe):
     """configs[3]: 64 streams, 8 per GPU.  Rank r's shard (seeds 100+8r ..
     100+8r+7, bench.shard_seeds) through bench.py's own device-resident path
-    (records in HBM, one k_prep + k_wgpp launch pair per step) and its
-    verification pass: all 60 pictures of all 8 streams vs the reference
-    decoder's MD5s."""
+    (bench.DeviceRun: records in HBM, `pipe` pictures of every stream per
+    launch -- 1 is the bench default, 2 the frame-pipelined batches -- with
+    the next launch's k_prep in its tail) and its verification pass: all 60
+    pictures of all 8 streams vs the reference decoder's MD5s."""
     import bench
     seeds = bench.shard_seeds(rank, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
-    L = _lib.mi()
-    d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, n)
+    run = bench.DeviceRun(_lib.mi(), caps, 4, n - 4, pipe)
     try:
-        eng = Engine(caps[0].w_mbs, caps[0].h_mbs, 8, nslots)
-        def step(k):   # bench.py's step: the next step's k_prep in this launch's tail
-            if k + 1 < n:
-                eng.decode_device_next(8, d_recs + k * step_rec_bytes, d_coef, d_pics + k * 8 * 32,
-                                       d_recs + (k + 1) * step_rec_bytes, d_coef, d_pics + (k + 1) * 8 * 32)
-            else:
-                eng.decode_device(8, d_recs + k * step_rec_bytes, d_coef, d_pics + k * 8 * 32)
-        ok, checked, missing = bench.verify_all(eng, step, caps, seeds, 3, {}, n)
+        assert run.P == pipe and len(run.sched) == n // pipe
+        ok, checked, missing = bench.verify_all(run.eng, run.launch, run.sched, caps, seeds, 3, {}, run.cur_slots)
         assert (ok, checked, missing) == (True, 8 * n, 0)
-        assert eng.errors() == 0
-        eng.close()
+        assert run.eng.errors() == 0
     finally:
-        for p in (d_recs, d_coef, d_pics):
-            L.h264mi_device_free(p)
+        run.free()
+
+
+@pytest.mark.parametrize("wh", [(13, 7), (12, 9), (20, 11)])
+def test_engine_pipelined_steps_vs_oracle(wh):
+    """Frame-pipelined launches (two consecutive pictures of each of 3
+    streams per launch, physical slots renamed) on sizes whose chroma rows
+    and Cb/Cr planes do not end on 128-B lines (odd w*h: a line straddles
+    the Cb/Cr boundary), every picture vs the oracle's decode of the stream."""
+    import bench
+    w, h = wh
+    streams = [gen.generate(2, 70 + i, nframes=10, w_mbs=w, h_mbs=h, crop_bottom=0, slices=2, gop=5)
+               for i in range(3)]
+    caps = [Capture(s) for s in streams]
+    refs = [O.decode(s)[0] for s in streams]
+    n = min(c.npics for c in caps)
+    n -= n % 2
+    run = bench.DeviceRun(_lib.mi(), caps, 0, n, 2)
+    try:
+        assert run.P == 2
+        for i, (k0, P) in enumerate(run.sched):
+            run.launch(i)
+            run.eng.sync()
+            for k in range(k0, k0 + P):
+                for s in range(len(caps)):
+                    got = run.eng.read(s, int(run.cur_slots[k][s])).tobytes()
+                    assert got == refs[s][k], f"stream {s} picture {k}"
+        assert run.eng.errors() == 0
+    finally:
+        run.free()
 
 
 def test_2160p_vs_reference():
