@@ -3,7 +3,7 @@
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats of the bench command
   profiles/<tag>_pmc.json           FETCH_SIZE / WRITE_SIZE per launch (separate passes)
-  profiles/traffic.json             HBM bytes per reconstruction step (k_wg, or k_mb + k_rows),
+  profiles/traffic.json             HBM bytes per reconstruction step (k_wgpp + k_prep),
                                     read by bench.py for roofline.traffic
 
 Units and corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE / WRITE_SIZE are
@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kname(full):
-    """'void k_wg<false, 3, false>(ReconArgs)' -> 'k_wg'"""
+    """'void k_wgpp<3, false, true, 1>(ReconArgs)' -> 'k_wgpp'"""
     n = full.split("(")[0].split("<")[0]
     return n.split()[-1]
 
@@ -42,8 +42,7 @@ def main(tag):
     write = per_launch(os.path.join(src, "pmc_write", "bench_counter_collection.csv"), "WRITE_SIZE")
     kernels = {}
     step = 0.0
-    main_k = next((k for k in ("k_wgpp", "k_wg") if k in fetch), None)
-    step_kernels = ((main_k,) if main_k else ("k_mb", "k_rows")) + (("k_prep",) if "k_prep" in fetch else ())
+    step_kernels = ("k_wgpp",) + (("k_prep",) if "k_prep" in fetch else ())
     for k in step_kernels:
         f_kib, n = fetch[k]
         w_kib, _ = write[k]
