@@ -415,6 +415,26 @@ def end_to_end(streams, nframes, reps=3):
             # cores that keeps busy at the measured rate
             res["host_cpu_ms_per_picture"] = round(cpu_s * 1e3 / pics, 3)
             res["host_cores_busy"] = round(cpu_s / t, 2)
+        # the same streams in ONE process, one thread (H264SwDec instance) per
+        # stream, sharing one batched engine (h264mi_set_share, -S)
+        paths = [os.path.join(td, f"s{i}.h264") for i in range(len(streams))]
+        o = subprocess.run([exe, "-Onone", f"-r{reps}", "-T", f"-S{len(streams)}"] + paths, capture_output=True,
+                           text=True, timeout=600)
+        if o.returncode == 0:
+            d = {}
+            for line in o.stdout.splitlines():
+                f = line.split()
+                if len(f) >= 2:
+                    try:
+                        d[f[0]] = float(f[1])
+                    except ValueError:
+                        pass
+            if d.get("pictures") and d.get("decode_seconds"):
+                res["one_process_shared_engine"] = {
+                    "value": round(d["pictures"] / d["decode_seconds"], 2), "unit": "frames/s",
+                    "threads": len(streams),
+                    "pictures_per_launch": round(d.get("share_pictures", 0) / max(d.get("share_batches", 1), 1), 2),
+                    "host_cpu_ms_per_picture": round(d.get("cpu_seconds", 0) * 1e3 / d["pictures"], 3)}
         return res
     finally:
         shutil.rmtree(td, ignore_errors=True)

@@ -561,36 +561,226 @@ extern "C" int h264mi_copy_h2d(void *dst, const void *src, size_t bytes)
 
 // -------- H264Backend adapter for the single-stream host decoder ----------
 #include "../host/decoder.h"
+#include <mutex>
+#include <condition_variable>
+#include <chrono>
+#include <atomic>
+
+// Per-GPU shared engines (H264MI_SHARE=N, or h264mi_set_share): the decoder
+// instances of a process that decode pictures of the same size on the same
+// device share one engine of N lanes (one engine per picture size) (a lane = a stream index of the frame
+// pool).  Each instance's H264SwDecDecode hands its picture's records to the
+// batch being collected and returns once a launch has taken it: the batch
+// launches when every attached instance has submitted, or SHARE_WAIT_US
+// after its first picture -- one k_prep + k_wgpp launch for the pictures of
+// up to N concurrent instances (threads) instead of one launch each.  The
+// reference's multi-instance model is N independent instances
+// (TestBenchMultipleInstance.c:134-305); each instance here still sees only
+// its own pictures, in its own order.
+#define SHARE_MAX 32
+#define SHARE_SLOTS 17                    // MaxDpbFrames (16) + the current picture
+#define SHARE_WAIT_US 1000                // default batch wait (H264MI_SHARE_WAIT_US)
+#define SHARE_FLAG_RING 256
+
+struct HipBackendCtx;
+struct SharedEng {
+    std::mutex mu;
+    std::condition_variable cv;
+    int device, w, h, lanes;
+    h264mi_engine *e;
+    uint32_t used;                        // attached lanes
+    int active;
+    // the batch being collected
+    int np;
+    int stream[SHARE_MAX], slot[SHARE_MAX];
+    const void *recs[SHARE_MAX];
+    const int16_t *coefs[SHARE_MAX];
+    uint32_t nc[SHARE_MAX];
+    HipBackendCtx *who[SHARE_MAX];
+    unsigned long long collecting, launched;   // batch ids: collecting > launched while np > 0
+    int rc;                               // result of the last launch
+    unsigned *h_flags;                    // pinned: per batch (ring of SHARE_FLAG_RING) the pictures' device flags
+};
+static std::mutex g_share_mu;
+#define SHARE_SIZES 4                     // shared engines per device, one per picture size
+static SharedEng *g_share[16][SHARE_SIZES];
+// totals per device; atomics, since share_launch runs under an engine's
+// lock and the lock order is g_share_mu before SharedEng::mu
+static std::atomic<unsigned long long> g_share_batches[16], g_share_pictures[16];
+static int g_share_lanes = -1;            // -1: H264MI_SHARE from the environment
+static int g_share_wait_us = SHARE_WAIT_US;
 
 struct HipBackendCtx {
     int device;
-    h264mi_engine *e;
+    h264mi_engine *e;   // private engine, or the shared one's
+    SharedEng *sh;      // shared engine (NULL: private)
+    int lane;           // stream index in e
+    hipEvent_t ev_last; // shared: after this instance's latest work on the engine stream
+    uint8_t *d_rgba;    // shared: RGBA staging
+    unsigned long long fbatch;   // shared: batch of this instance's latest picture, and its index there
+    int fidx;
     uint8_t **pref;     // per slot: host buffer a D2H copy of the slot's current picture was queued into
     int nslots;
     unsigned enq, synced;   // work items queued on the engine's stream / of those, waited for by hb_sync
 };
 
+extern "C" int h264mi_set_share(int lanes)
+{
+    if (lanes < 0 || lanes > SHARE_MAX) return -1;
+    std::lock_guard<std::mutex> g(g_share_mu);
+    g_share_lanes = lanes;
+    return 0;
+}
+
+static int share_lanes()
+{
+    std::lock_guard<std::mutex> g(g_share_mu);
+    if (g_share_lanes < 0) {
+        const char *v = getenv("H264MI_SHARE");
+        const int n = v ? atoi(v) : 0;
+        g_share_lanes = n > 1 && n <= SHARE_MAX ? n : 0;
+        const char *w = getenv("H264MI_SHARE_WAIT_US");
+        if (w && atoi(w) > 0) g_share_wait_us = atoi(w);
+    }
+    return g_share_lanes;
+}
+
+// caller holds sh->mu
+static void share_launch(SharedEng *sh)
+{
+    if (sh->np == 0) return;
+    h264mi_engine *e = sh->e;
+    sh->rc = h264mi_engine_decode(e, sh->np, sh->stream, sh->slot, sh->recs, sh->coefs, sh->nc);
+    // this batch's device flags (ReconArgs::err, one word per picture) into
+    // its ring entry, then cleared for the next batch
+    unsigned *hf = sh->h_flags + (size_t)(sh->collecting % SHARE_FLAG_RING) * SHARE_MAX;
+    if (hipMemcpyAsync(hf, e->d_err, sizeof(unsigned) * sh->np, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+        hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * sh->np, e->st) != hipSuccess)
+        sh->rc = -1;
+    for (int i = 0; i < sh->np; i++) {
+        HipBackendCtx *c = sh->who[i];
+        c->fbatch = sh->collecting;
+        c->fidx = i;
+        (void)hipEventRecord(c->ev_last, e->st);
+    }
+    g_share_batches[sh->device] += 1;
+    g_share_pictures[sh->device] += (unsigned long long)sh->np;
+    sh->np = 0;
+    sh->launched = sh->collecting;
+    sh->collecting++;
+    sh->cv.notify_all();
+}
+
+static void share_detach(HipBackendCtx *c)
+{
+    SharedEng *sh = c->sh;
+    if (!sh) return;
+    std::lock_guard<std::mutex> g(g_share_mu);
+    bool last;
+    {
+        std::unique_lock<std::mutex> l(sh->mu);
+        sh->used &= ~(1u << c->lane);
+        sh->active--;
+        if (sh->np > 0 && sh->np >= sh->active) share_launch(sh);      // the others need not wait for us
+        last = sh->active == 0;
+        if (last) (void)hipStreamSynchronize(sh->e->st);
+    }
+    (void)hipEventDestroy(c->ev_last);
+    (void)hipFree(c->d_rgba);
+    c->ev_last = NULL; c->d_rgba = NULL;
+    if (last) {
+        for (int k = 0; k < SHARE_SIZES; k++)
+            if (g_share[sh->device][k] == sh) g_share[sh->device][k] = NULL;
+        h264mi_engine_destroy(sh->e);
+        (void)hipHostFree(sh->h_flags);
+        delete sh;
+    }
+    c->sh = NULL; c->e = NULL;
+}
+
+// attach to the device's shared engine for a w x h stream; 0 = attached
+static int share_attach(HipBackendCtx *c, int w_mbs, int h_mbs, int nslots)
+{
+    const int lanes = share_lanes();
+    if (lanes < 2 || nslots > SHARE_SLOTS || c->device < 0 || c->device >= 16) return -1;
+    std::lock_guard<std::mutex> g(g_share_mu);
+    SharedEng *sh = NULL;
+    int free_k = -1;
+    for (int k = 0; k < SHARE_SIZES; k++) {
+        SharedEng *x = g_share[c->device][k];
+        if (x && x->w == w_mbs && x->h == h_mbs) sh = x;
+        else if (!x && free_k < 0) free_k = k;
+    }
+    if (!sh) {
+        if (free_k < 0) return -1;                          // SHARE_SIZES sizes in use: a private engine
+        h264mi_engine *e = h264mi_engine_create(c->device, w_mbs, h_mbs, lanes, SHARE_SLOTS);
+        if (!e) return -1;
+        sh = new SharedEng();
+        if (hipHostMalloc(&sh->h_flags, sizeof(unsigned) * SHARE_FLAG_RING * SHARE_MAX, hipHostMallocDefault) != hipSuccess) {
+            h264mi_engine_destroy(e);
+            delete sh;
+            return -1;
+        }
+        memset(sh->h_flags, 0, sizeof(unsigned) * SHARE_FLAG_RING * SHARE_MAX);
+        sh->device = c->device; sh->w = w_mbs; sh->h = h_mbs; sh->lanes = lanes; sh->e = e;
+        sh->used = 0; sh->active = 0; sh->np = 0; sh->collecting = 1; sh->launched = 0; sh->rc = 0;
+        g_share[c->device][free_k] = sh;
+    }
+    std::lock_guard<std::mutex> l(sh->mu);
+    int lane = -1;
+    for (int i = 0; i < sh->lanes; i++)
+        if (!(sh->used & (1u << i))) { lane = i; break; }
+    if (lane < 0) return -1;                                // all lanes taken: a private engine
+    if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) return -1;
+    (void)hipEventRecord(c->ev_last, sh->e->st);
+    sh->used |= 1u << lane;
+    sh->active++;
+    c->sh = sh; c->lane = lane; c->e = sh->e;
+    c->fbatch = 0; c->fidx = 0;
+    return 0;
+}
+
 static int hb_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
-    if (c->e) h264mi_engine_destroy(c->e);
+    if (c->sh) share_detach(c);
+    else if (c->e) h264mi_engine_destroy(c->e);
+    c->e = NULL;
     free(c->pref);
     c->pref = (uint8_t **)calloc((size_t)nslots, sizeof(uint8_t *));
     c->nslots = c->pref ? nslots : 0;
-    c->e = h264mi_engine_create(c->device, w_mbs, h_mbs, 1, nslots);
+    if (share_attach(c, w_mbs, h_mbs, nslots) != 0) {
+        c->lane = 0;
+        c->e = h264mi_engine_create(c->device, w_mbs, h_mbs, 1, nslots);
+    }
     return c->e && c->pref ? 0 : -1;
 }
 
 static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
-    int stream = 0;
-    const void *recs[1] = {pb->rec};
-    const int16_t *coefs[1] = {pb->coef};
-    uint32_t nc[1] = {pb->ncoef};
     if (cur_slot >= 0 && cur_slot < c->nslots) c->pref[cur_slot] = NULL;
     c->enq++;
-    return h264mi_engine_decode(c->e, 1, &stream, &cur_slot, recs, coefs, nc);
+    if (!c->sh) {
+        int stream = 0;
+        const void *recs[1] = {pb->rec};
+        const int16_t *coefs[1] = {pb->coef};
+        uint32_t nc[1] = {pb->ncoef};
+        return h264mi_engine_decode(c->e, 1, &stream, &cur_slot, recs, coefs, nc);
+    }
+    SharedEng *sh = c->sh;
+    std::unique_lock<std::mutex> l(sh->mu);
+    const int i = sh->np++;
+    sh->stream[i] = c->lane; sh->slot[i] = cur_slot;
+    sh->recs[i] = pb->rec; sh->coefs[i] = pb->coef; sh->nc[i] = pb->ncoef;
+    sh->who[i] = c;
+    const unsigned long long mine = sh->collecting;
+    if (sh->np >= sh->active) {
+        share_launch(sh);
+    } else if (!sh->cv.wait_for(l, std::chrono::microseconds(g_share_wait_us), [&] { return sh->launched >= mine; })) {
+        share_launch(sh);                 // the others are late: launch what is there
+    }
+    return sh->rc;
 }
 
 static int hb_prefetch(void *vctx, int slot, uint8_t *dst)
@@ -599,7 +789,10 @@ static int hb_prefetch(void *vctx, int slot, uint8_t *dst)
     if (slot < 0 || slot >= c->nslots) return -1;
     h264mi_engine *e = c->e;
     HIPCHECK(hipSetDevice(e->dev));
-    HIPCHECK(hipMemcpyAsync(dst, h264mi_engine_frame_ptr(e, 0, slot), e->frame_bytes, hipMemcpyDeviceToHost, e->st));
+    std::unique_lock<std::mutex> l;
+    if (c->sh) l = std::unique_lock<std::mutex>(c->sh->mu);
+    HIPCHECK(hipMemcpyAsync(dst, h264mi_engine_frame_ptr(e, c->lane, slot), e->frame_bytes, hipMemcpyDeviceToHost, e->st));
+    if (c->sh) HIPCHECK(hipEventRecord(c->ev_last, e->st));
     c->pref[slot] = dst;
     c->enq++;
     return 0;
@@ -615,11 +808,27 @@ static int hb_flagged(h264mi_engine *e, bool wait = true)
     return n ? 1 : 0;
 }
 
+// shared engine: wait for this instance's own work only, then its latest
+// picture's device flags from its batch's ring entry
+static int share_flagged(HipBackendCtx *c)
+{
+    HIPCHECK(hipEventSynchronize(c->ev_last));
+    if (!c->fbatch) return 0;
+    const unsigned f = c->sh->h_flags[(size_t)(c->fbatch % SHARE_FLAG_RING) * SHARE_MAX + c->fidx];
+    c->fbatch = 0;
+    if (f) fprintf(stderr, "h264mi: device flagged a picture (flags %#x)\n", f);
+    return f ? 1 : 0;
+}
+
 static int hb_sync(void *vctx)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
     const unsigned n = c->enq;
-    if (h264mi_engine_sync(c->e)) return -1;
+    if (c->sh) {
+        HIPCHECK(hipEventSynchronize(c->ev_last));
+    } else if (h264mi_engine_sync(c->e)) {
+        return -1;
+    }
     c->synced = n;
     return 0;
 }
@@ -627,6 +836,16 @@ static int hb_sync(void *vctx)
 static int hb_read(void *vctx, int slot, uint8_t *dst)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
+    if (c->sh) {
+        if (slot < 0 || slot >= c->nslots) return -1;
+        if (c->pref[slot] != dst) {
+            std::lock_guard<std::mutex> l(c->sh->mu);
+            HIPCHECK(hipMemcpyAsync(dst, h264mi_engine_frame_ptr(c->e, c->lane, slot), c->e->frame_bytes,
+                                    hipMemcpyDeviceToHost, c->e->st));
+            HIPCHECK(hipEventRecord(c->ev_last, c->e->st));
+        }
+        return share_flagged(c);
+    }
     // copied there already (hb_prefetch): only wait for it
     if (slot >= 0 && slot < c->nslots && c->pref[slot] == dst) return hb_flagged(c->e, c->synced != c->enq);
     if (h264mi_engine_read(c->e, 0, slot, dst)) return -1;
@@ -636,6 +855,21 @@ static int hb_read(void *vctx, int slot, uint8_t *dst)
 static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
+    if (c->sh) {
+        h264mi_engine *e = c->e;
+        const size_t bytes = (size_t)e->nmbs * 256 * 4;
+        if (slot < 0 || slot >= c->nslots) return -1;
+        if (!c->d_rgba) HIPCHECK(hipMalloc(&c->d_rgba, bytes));
+        {
+            std::lock_guard<std::mutex> l(c->sh->mu);
+            if (h264mi_yuv2rgba_device(h264mi_engine_frame_ptr(e, c->lane, slot), c->d_rgba, e->w * 16, e->h * 16, 1, 0,
+                                       0, e->st))
+                return -1;
+            HIPCHECK(hipMemcpyAsync(dst, c->d_rgba, bytes, hipMemcpyDeviceToHost, e->st));
+            HIPCHECK(hipEventRecord(c->ev_last, e->st));
+        }
+        return share_flagged(c);
+    }
     if (h264mi_engine_read_rgba(c->e, 0, slot, dst)) return -1;
     return hb_flagged(c->e);
 }
@@ -651,8 +885,15 @@ static void hb_host_free(void *vctx, void *p) { (void)hipHostFree(p); }
 static int hb_copy(void *vctx, int dst, int src)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
-    if (h264mi_engine_sync(c->e)) return -1;
     if (dst >= 0 && dst < c->nslots) c->pref[dst] = NULL;
+    if (c->sh) {
+        std::lock_guard<std::mutex> l(c->sh->mu);
+        HIPCHECK(hipMemcpyAsync(h264mi_engine_frame_ptr(c->e, c->lane, dst), h264mi_engine_frame_ptr(c->e, c->lane, src),
+                                c->e->frame_bytes, hipMemcpyDeviceToDevice, c->e->st));
+        HIPCHECK(hipEventRecord(c->ev_last, c->e->st));
+        return 0;
+    }
+    if (h264mi_engine_sync(c->e)) return -1;
     HIPCHECK(hipMemcpy(h264mi_engine_frame_ptr(c->e, 0, dst), h264mi_engine_frame_ptr(c->e, 0, src),
                        h264mi_engine_frame_bytes(c->e), hipMemcpyDeviceToDevice));
     return 0;
@@ -661,9 +902,28 @@ static int hb_copy(void *vctx, int dst, int src)
 static void hb_destroy(void *vctx)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
-    if (c->e) h264mi_engine_destroy(c->e);
+    if (c->sh) share_detach(c);
+    else if (c->e) h264mi_engine_destroy(c->e);
     free(c->pref);
     free(c);
+}
+
+// batches / pictures the device's shared engines launched since the process
+// started; returns the instances attached now
+extern "C" int h264mi_share_stats(int device, unsigned long long *batches, unsigned long long *pictures)
+{
+    if (device < 0 || device >= 16) return -1;
+    std::lock_guard<std::mutex> g(g_share_mu);
+    if (batches) *batches = g_share_batches[device].load();
+    if (pictures) *pictures = g_share_pictures[device].load();
+    int n = 0;
+    for (int k = 0; k < SHARE_SIZES; k++) {
+        SharedEng *sh = g_share[device][k];
+        if (!sh) continue;
+        std::lock_guard<std::mutex> l(sh->mu);
+        n += sh->active;
+    }
+    return n;
 }
 
 extern "C" H264Backend h264mi_hip_backend_create(int device)

@@ -4,11 +4,16 @@
  * D2H of every output picture.  Call protocol of the reference testbench
  * (Decoder/src/DecTestBench.c:230-410): decode, drain NextPicture after each
  * PIC_RDY, flush at end of stream.
- *   h264mi_dec [-R] [-Oout.yuv|-Onone] [-rN] [-T] in.h264
+ *   h264mi_dec [-R] [-Oout.yuv|-Onone] [-rN] [-T] [-SN] in.h264 [in2.h264 ...]
  * -rN decodes the stream N times (one instance each; HIP start-up is paid
- * once, before the timed loop); -T prints the wall time of the decode loops. */
+ * once, before the timed loop); -T prints the wall time of the decode loops.
+ * Several inputs: one thread per input, each with its own instances
+ * (TestBenchMultipleInstance.c's N instances, concurrently); -SN lets them
+ * share one N-lane engine per GPU (h264mi_set_share); -O applies to the
+ * first input. */
 #include "../../../include/h264mi.h"
 
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -23,6 +28,7 @@ static double now_s(void)
 }
 
 static double g_t[4];   /* parse, submit, wait, copy (H264SwDecGetTiming), summed over instances */
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 
 static int decode_once(const uint8_t *stream, uint32_t len, uint8_t *work, int no_reorder, FILE *fo, int *errs)
 {
@@ -66,33 +72,74 @@ static int decode_once(const uint8_t *stream, uint32_t len, uint8_t *work, int n
         if (fo) fwrite(pic.pOutputPicture, 1, size, fo);
     }
     double t[4];
-    if (H264SwDecGetTiming(inst, &t[0], &t[1], &t[2], &t[3], NULL) == H264SWDEC_OK)
+    if (H264SwDecGetTiming(inst, &t[0], &t[1], &t[2], &t[3], NULL) == H264SWDEC_OK) {
+        pthread_mutex_lock(&g_mu);
         for (int i = 0; i < 4; i++) g_t[i] += t[i];
+        pthread_mutex_unlock(&g_mu);
+    }
     H264SwDecRelease(inst);
     return pics;
 }
 
+typedef struct Job {
+    uint8_t *buf, *work;
+    uint32_t len;
+    int reps, no_reorder, pics, errs, fail;
+    FILE *fo;
+} Job;
+
+static void *run_job(void *arg)
+{
+    Job *j = (Job *)arg;
+    for (int k = 0; k < j->reps; k++) {
+        const int n = decode_once(j->buf, j->len, j->work, j->no_reorder, k == 0 ? j->fo : NULL, &j->errs);
+        if (n < 0) { j->fail = 1; break; }
+        j->pics += n;
+    }
+    return NULL;
+}
+
+static int load(const char *path, Job *j)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f) { perror(path); return -1; }
+    fseek(f, 0, SEEK_END);
+    long len = ftell(f);
+    rewind(f);
+    j->buf = (uint8_t *)malloc((size_t)len);
+    j->work = (uint8_t *)malloc((size_t)len);
+    if (!j->buf || !j->work || fread(j->buf, 1, (size_t)len, f) != (size_t)len) { fclose(f); return -1; }
+    fclose(f);
+    j->len = (uint32_t)len;
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
-    const char *out = NULL, *in = NULL;
-    int no_reorder = 0, timing = 0, reps = 1;
+    const char *out = NULL;
+    const char *ins[256];
+    int nin = 0, no_reorder = 0, timing = 0, reps = 1, share = 0;
     for (int i = 1; i < argc; i++) {
         if (!strncmp(argv[i], "-O", 2)) out = argv[i] + 2;
         else if (!strcmp(argv[i], "-R")) no_reorder = 1;
         else if (!strcmp(argv[i], "-T")) timing = 1;
         else if (!strncmp(argv[i], "-r", 2)) reps = atoi(argv[i] + 2);
-        else in = argv[i];
+        else if (!strncmp(argv[i], "-S", 2)) share = atoi(argv[i] + 2);
+        else if (nin < 256) ins[nin++] = argv[i];
     }
-    if (!in || reps < 1) { fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] in.h264\n"); return 2; }
-    FILE *f = fopen(in, "rb");
-    if (!f) { perror(in); return 2; }
-    fseek(f, 0, SEEK_END);
-    long len = ftell(f);
-    rewind(f);
-    uint8_t *buf = (uint8_t *)malloc((size_t)len), *work = (uint8_t *)malloc((size_t)len);
-    if (!buf || !work || fread(buf, 1, (size_t)len, f) != (size_t)len) { fclose(f); return 2; }
-    fclose(f);
+    if (!nin || reps < 1) {
+        fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] [-SN] in.h264 [in2.h264 ...]\n");
+        return 2;
+    }
+    Job *jobs = (Job *)calloc((size_t)nin, sizeof(Job));
+    for (int i = 0; i < nin; i++) {
+        if (load(ins[i], &jobs[i])) return 2;
+        jobs[i].reps = reps;
+        jobs[i].no_reorder = no_reorder;
+    }
     FILE *fo = (out && strcmp(out, "none")) ? fopen(out, "wb") : NULL;
+    jobs[0].fo = fo;
+    if (share && h264mi_set_share(share)) { fprintf(stderr, "bad -S\n"); return 2; }
     /* HIP start-up (device, code objects) outside the timed loop */
     {
         H264SwDecInst warm;
@@ -103,14 +150,22 @@ int main(int argc, char **argv)
     struct rusage ru0, ru1;
     getrusage(RUSAGE_SELF, &ru0);
     const double t0 = now_s();
-    for (int k = 0; k < reps; k++) {
-        const int n = decode_once(buf, (uint32_t)len, work, no_reorder, k == 0 ? fo : NULL, &errs);
-        if (n < 0) { fprintf(stderr, "DECODER INITIALIZATION FAILED\n"); return 1; }
-        pics += n;
+    if (nin == 1) {
+        run_job(&jobs[0]);
+    } else {
+        pthread_t *th = (pthread_t *)calloc((size_t)nin, sizeof(pthread_t));
+        for (int i = 0; i < nin; i++) pthread_create(&th[i], NULL, run_job, &jobs[i]);
+        for (int i = 0; i < nin; i++) pthread_join(th[i], NULL);
+        free(th);
     }
     const double t1 = now_s();
     getrusage(RUSAGE_SELF, &ru1);
     if (fo) fclose(fo);
+    for (int i = 0; i < nin; i++) {
+        if (jobs[i].fail) { fprintf(stderr, "DECODER INITIALIZATION FAILED\n"); return 1; }
+        pics += jobs[i].pics;
+        errs += jobs[i].errs;
+    }
     printf("pictures %d errors %d\n", pics, errs);
     if (timing) {
         printf("decode_seconds %.6f fps %.2f\n", t1 - t0, pics / (t1 - t0));
@@ -119,8 +174,11 @@ int main(int argc, char **argv)
         const double cpu = (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) + 1e-6 * (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) +
                            (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec);
         printf("cpu_seconds %.6f\n", cpu);
+        unsigned long long nb = 0, np = 0;
+        h264mi_share_stats(0, &nb, &np);
+        if (share) printf("share_batches %llu\nshare_pictures %llu\n", nb, np);
     }
-    free(buf);
-    free(work);
+    for (int i = 0; i < nin; i++) { free(jobs[i].buf); free(jobs[i].work); }
+    free(jobs);
     return errs ? 1 : 0;
 }

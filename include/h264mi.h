@@ -126,6 +126,20 @@ H264SwDecRet H264SwDecNextPictureRGBA(H264SwDecInst decInst, H264SwDecPicture *p
  * pointer may be NULL. */
 H264SwDecRet H264SwDecGetTiming(H264SwDecInst decInst, double *parse_s, double *submit_s, double *wait_s,
                                 double *copy_s, u32 *pictures);
+/* Extension: per-GPU shared engine for concurrent instances (threads) of one
+ * process.  With lanes >= 2 (or H264MI_SHARE=lanes in the environment), the
+ * instances decoding pictures of the same size on one device share one
+ * engine of `lanes` streams (one such engine per picture size): each H264SwDecDecode hands its picture to the
+ * batch being collected and returns once a launch took it; a batch launches
+ * when every attached instance has submitted or 1 ms (H264MI_SHARE_WAIT_US)
+ * after its first picture, as one k_prep + k_wgpp launch.  Set before the instances are
+ * configured (their first picture); 0 turns it off.  Outputs, order and
+ * error reporting per instance are unchanged.  The reference's model is N
+ * independent instances (TestBenchMultipleInstance.c:134-305). */
+int h264mi_set_share(int lanes);
+/* batches / pictures launched by device's shared engine; returns the
+ * instances attached (0: none) */
+int h264mi_share_stats(int device, unsigned long long *batches, unsigned long long *pictures);
 
 /* ---------------------------------------------------------------------- */
 /* 2. Broadway glue (reference Decoder/src/Decoder.c:44-185, make.py:39)   */

@@ -183,6 +183,58 @@ def test_engine_pipelined_steps_vs_oracle(wh):
         run.free()
 
 
+@pytest.mark.parametrize("share", [0, 4])
+def test_swdec_concurrent_instances_vs_reference(share):
+    """One H264SwDec instance per thread, decoding concurrently (the
+    reference's N-instance model, TestBenchMultipleInstance.c:134-305, on
+    threads): four 1080p streams -- a damaged one among them, with its
+    concealment and nbrOfErrMBs -- two 720p and a small damaged one.
+    share = 4: instances of one picture size share one batched engine
+    (h264mi_set_share; 1080p and 720p each get theirs, the small stream's
+    engine is shared by nobody else).  Every output picture, picture id and
+    error count equals the reference's, and the lock-step 1080p and 720p
+    instances put several pictures in one launch."""
+    import threading
+    L = _lib.mi()
+    names = ["bench_1080p_s100", "bench_1080p_s101", "bench_1080p_s102", "err_1080p_mixed",
+             "leg_cfg2_720p_s1", "leg_cfg2_720p_s2", "err_range_p_11x9"]
+    b0, p0 = C.c_ulonglong(), C.c_ulonglong()
+    L.h264mi_share_stats(0, C.byref(b0), C.byref(p0))
+    assert L.h264mi_set_share(share) == 0
+    results, errors = {}, []
+
+    def run(n):
+        try:
+            c = CASES[n]
+            results[n] = swdec_decode(stream(c), no_reorder=c["no_reorder"], info=True)
+        except Exception as ex:          # surfaced by the main thread
+            errors.append((n, ex))
+
+    try:
+        th = [threading.Thread(target=run, args=(n,)) for n in names]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=240)
+        assert not any(t.is_alive() for t in th), "decoder thread hung"
+    finally:
+        L.h264mi_set_share(0)
+    assert not errors, errors
+    for n in names:
+        c = CASES[n]
+        frames, _, pics = results[n]
+        assert md5s(frames) == c["frames"], n
+        if "pics" in c:
+            assert [list(p) for p in pics] == c["pics"], n
+    b1, p1 = C.c_ulonglong(), C.c_ulonglong()
+    L.h264mi_share_stats(0, C.byref(b1), C.byref(p1))
+    nb, npic = b1.value - b0.value, p1.value - p0.value
+    if share:
+        assert npic > 0 and nb < 0.75 * npic, (nb, npic)
+    else:
+        assert nb == npic == 0
+
+
 def test_2160p_vs_reference():
     c = CASES["cfg5_2160p_s200"]
     frames, errors = swdec_decode(stream(c))
