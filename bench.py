@@ -375,6 +375,10 @@ def end_to_end(streams, nframes, reps=3):
     if not os.path.exists(exe):
         return None
     streams = streams[:MAX_E2E_PROCS]
+    # a thread waiting for the GPU sleeps instead of spinning: the host cores
+    # are the bound on this path (tools/e2e_env_sweep.sh: 1.89k -> 2.08k fps)
+    env = dict(os.environ)
+    env.setdefault("H264MI_BLOCKING_SYNC", "1")
     td = tempfile.mkdtemp(prefix="h264e2e")
     try:
         procs = []
@@ -383,7 +387,7 @@ def end_to_end(streams, nframes, reps=3):
             with open(pth, "wb") as f:
                 f.write(s)
             procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T", pth], stdout=subprocess.PIPE,
-                                          stderr=subprocess.PIPE, text=True))
+                                          stderr=subprocess.PIPE, text=True, env=env))
         secs, pics, parts, cpu_s = [], 0, {}, 0.0
         for pr in procs:
             o, e = pr.communicate(timeout=600)
@@ -411,6 +415,7 @@ def end_to_end(streams, nframes, reps=3):
             # host parse / record upload + launch / wait for the GPU / D2H copy
             res["per_picture_ms"] = {k[2:]: round(v * 1e3 / pics, 3) for k, v in sorted(parts.items())}
             res["parse_threads_per_process"] = 1 + int(os.environ.get("H264MI_PARSE_THREADS", "3"))
+            res["host_sync"] = "blocking" if env["H264MI_BLOCKING_SYNC"] == "1" else "spin"
             # host CPU time (all threads of all processes) per picture, and the
             # cores that keeps busy at the measured rate
             res["host_cpu_ms_per_picture"] = round(cpu_s * 1e3 / pics, 3)
@@ -419,7 +424,7 @@ def end_to_end(streams, nframes, reps=3):
         # stream, sharing one batched engine (h264mi_set_share, -S)
         paths = [os.path.join(td, f"s{i}.h264") for i in range(len(streams))]
         o = subprocess.run([exe, "-Onone", f"-r{reps}", "-T", f"-S{len(streams)}"] + paths, capture_output=True,
-                           text=True, timeout=600)
+                           text=True, timeout=600, env=env)
         if o.returncode == 0:
             d = {}
             for line in o.stdout.splitlines():

@@ -731,7 +731,8 @@ static int share_attach(HipBackendCtx *c, int w_mbs, int h_mbs, int nslots)
     for (int i = 0; i < sh->lanes; i++)
         if (!(sh->used & (1u << i))) { lane = i; break; }
     if (lane < 0) return -1;                                // all lanes taken: a private engine
-    if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) return -1;
+    // a waiting instance sleeps (its core parses for another instance)
+    if (hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming | hipEventBlockingSync) != hipSuccess) return -1;
     (void)hipEventRecord(c->ev_last, sh->e->st);
     sh->used |= 1u << lane;
     sh->active++;
