@@ -128,6 +128,11 @@ def dist_setup(gpus: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    # BENCH_ONE_DEVICE=1: every rank on device 0 -- a rehearsal of the N-rank
+    # path (sharding, barriers, max-over-ranks timing, verification sums) on
+    # a one-GPU box; the value is then NOT a multi-GPU throughput
+    if os.environ.get("BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world != gpus:
         raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}")
     import torch
@@ -787,6 +792,8 @@ def main(argv=None):
                                          "stream of every rank vs reference-decoder MD5s",
                                "residual_range_errors": errors_all},
             "prep_seconds": round(t_prep, 1),
+            **({"one_device_rehearsal": f"{world} ranks shared device 0 (BENCH_ONE_DEVICE=1): not a multi-GPU rate"}
+               if os.environ.get("BENCH_ONE_DEVICE") == "1" else {}),
             "hbm_resident_input_MB": round(resident / 1e6, 1),
         }
         if a.dry_run:

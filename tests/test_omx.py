@@ -66,7 +66,9 @@ class Buf:
 
 def _both(libs, name, make_args):
     """Run primitive `name` of both libraries on identical copies; returns
-    (ret_ours, ret_ref, [(ours, ref) buffer pairs])."""
+    (ret_ours, ret_ref, [(ours, ref) buffer pairs]).  make_args returns the
+    call's arguments and EVERY buffer they point into (the buffers must
+    outlive the call)."""
     ours, ref = libs
     a_o, bufs_o = make_args()
     a_r, bufs_r = make_args()
@@ -93,7 +95,7 @@ def _intra_case(rng, size, mode, avail, step=64):
 
     def make():
         s, d = src.clone(), dst.clone()
-        return [s.p(base - 1), s.p(base - step), s.p(base - step - 1), d.p(), step, step, mode, avail], [d]
+        return [s.p(base - 1), s.p(base - step), s.p(base - step - 1), d.p(), step, step, mode, avail], [d, s]
     return make
 
 
@@ -187,12 +189,12 @@ def test_interpolate_luma_vs_reference(libs):
 
                     def make():
                         s, d = src.clone(), dst.clone()
-                        return [s.p(24 * step + 24), step, d.p(), step, dx, dy, Size(w, h)], [d]
+                        return [s.p(24 * step + 24), step, d.p(), step, dx, dy, Size(w, h)], [d, s]
                     if (dx, dy) in REF_SAFE:
                         r_o, r_r, pairs = _both(libs, "omxVCM4P10_InterpolateLuma", make)
                         _check(r_o, r_r, pairs, ("luma", w, h, dx, dy))
                     else:
-                        args, (d,) = make()
+                        args, (d, _s) = make()
                         r_o = ours.omxVCM4P10_InterpolateLuma(*args)
                         got = d.a.reshape(32, step)[:h, :w]
                         assert np.array_equal(got, _luma_spec(src.a, 24, 24, step, w, h, dx, dy)), (w, h, dx, dy)
@@ -212,7 +214,7 @@ def test_interpolate_chroma_vs_reference(libs):
 
                     def make():
                         s, d = src.clone(), dst.clone()
-                        return [s.p(8 * step + 8), step, d.p(), step, dx, dy, Size(w, h)], [d]
+                        return [s.p(8 * step + 8), step, d.p(), step, dx, dy, Size(w, h)], [d, s]
                     r_o, r_r, pairs = _both(libs, "omxVCM4P10_InterpolateChroma", make)
                     _check(r_o, r_r, pairs, ("chroma", w, h, dx, dy))
                     assert r_o == 0
