@@ -156,9 +156,11 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         e->rpw_env = rp ? atoi(rp) : 0;
         if (e->rpw_env < 0 || e->rpw_env > 3) e->rpw_env = 0;
         // the group's LDS mailboxes (w * 256 B per inner row boundary) beside
-        // the static LDS of its rows (24 KB per row) within the CU's 160 KB
+        // the static LDS of its rows (regions, MC scratch, a RINGG-slot ring)
+        // within the CU's 160 KB
+        const size_t row_lds = sizeof(PPLds) + (size_t)e->mc_waves * sizeof(McScratch) + sizeof(MbRing<RINGG>);
         e->rpw_max = e->mc_waves == 2 ? 2 : 3;
-        while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * w_mbs * 256 + (size_t)e->rpw_max * 24 * 1024 > 156 * 1024)
+        while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * w_mbs * 256 + (size_t)e->rpw_max * row_lds > 156 * 1024)
             e->rpw_max--;
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;

@@ -516,6 +516,7 @@ struct McScratch {
     int32_t dc[24];
     uint32_t srec[72];               // deblocking record inputs: this MB's, left and top records
     uint32_t coef[216];              // the MB's coded blocks (<= 27 x 32 B), staged by one coalesced load
+    int16_t res[384];                // k_wgpp MC waves: the MB's residual (luma 16x16, Cb 8x8, Cr 8x8)
     union {
         struct {                         // inter: reference windows
             uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
@@ -1009,19 +1010,27 @@ template <bool LDSM> __device__ __forceinline__ void st_granT(unsigned long long
 }
 
 // LDS hand-off ring between the MC waves of a row workgroup and its row
-// unit: slot c % RING_K holds MB c's MC samples, residual and deblocking
+// unit: slot c % RK holds MB c's MC samples (residual added) and deblocking
 // record; flag[slot] = c + 1 once filled, consumed = c + 1 once the row unit
 // no longer reads MB c's slot.  LDS instructions of one wave execute in
 // order, so a flag written after the data (compiler barrier between) is
 // seen after it by every other wave of the workgroup.
-#ifndef RING_K
-#define RING_K 8
+// ring slots per row: a single-row workgroup (RPW = 1) gets a deep ring, so
+// its MC waves run far ahead of the row's deblocking chain and their
+// reference loads are mostly done before the chain reaches the row (fewer
+// loads queued in front of the chain's mailbox polls); row groups keep a
+// small one (LDS)
+#ifndef RING1
+#define RING1 64
 #endif
+#ifndef RINGG
+#define RINGG 16
+#endif
+template <int RK>
 struct __attribute__((aligned(16))) MbRing {
-    uint8_t px[RING_K][384];
-    int16_t res[RING_K][384];
-    uint8_t db[RING_K][64];
-    int flag[RING_K];
+    uint8_t px[RK][384];
+    uint8_t db[RK][64];
+    int flag[RK];
     int consumed;
 };
 
@@ -1037,19 +1046,19 @@ __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v,
 // (out of line to keep the kernel's VGPR count for 3 workgroups per CU; the
 // arguments are plain values: a reference to the kernel's ReconArgs would
 // force the whole argument block into private memory)
-template <bool UPL>
+template <bool UPL, int RK>
 __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const unsigned long long *mbx_up, unsigned *perr,
                                                    int W, int c, uint32_t tag, bool has_up, int lane, McScratch &M,
-                                                   MbRing &R, const uint32_t *i4tab)
+                                                   MbRing<RK> &R, const uint32_t *i4tab)
 {
     const MbRec &rec = *mbrec;
     const int qtype = rec.type, avail = rec.avail, pred = rec.pred;
     const uint64_t i4 = *(const uint64_t *)rec.i4;
-    const int slot = c & (RING_K - 1);
+    const int slot = c & (RK - 1);
     const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
     if (aA) {
         unsigned spins = 0;
-        while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[(c - 1) & (RING_K - 1)])) != c) {
+        while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[(c - 1) & (RK - 1)])) != c) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
         }
@@ -1073,7 +1082,7 @@ __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const uns
         }
         top = (uint32_t)gr;
     }
-    const uint8_t *lp = R.px[(c - 1) & (RING_K - 1)];
+    const uint8_t *lp = R.px[(c - 1) & (RK - 1)];
     {   // tile halo: top row (incl. top-left / top-right), left column
         const uint32_t b0 = top & 255, b1 = (top >> 8) & 255, b2 = (top >> 16) & 255, b3 = top >> 24;
         if (lane >= 24 && lane < 32) {
@@ -1094,7 +1103,7 @@ __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const uns
         }
     }
     wave_sync();
-    intra_tile(qtype, avail, pred, i4, R.res[slot], rec.cbits != 0, M.ty, M.tu, M.tv, i4tab, M.sx, M.junk, lane);
+    intra_tile(qtype, avail, pred, i4, M.res, rec.cbits != 0, M.ty, M.tu, M.tv, i4tab, M.sx, M.junk, lane);
     uint8_t *px = R.px[slot];
     {   // tile -> slot (tile samples start at column 1: byte reads)
         const int orow = lane >> 2, oq = lane & 3;
@@ -1149,8 +1158,8 @@ struct __attribute__((aligned(16))) PPLds {
 // UPL / MEL: the row above's mailbox (mbx_up) / this row's (mbx_me) is the
 // workgroup's LDS one (k_wgpp RPW = 2: the upper row of the pair publishes to
 // LDS, the lower one reads from there)
-template <bool PROF, bool UPL, bool MEL>
-__device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing *R,
+template <bool PROF, bool UPL, bool MEL, int RK>
+__device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing<RK> *R,
                        const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
     const int W = a.w, H = a.h;
@@ -1306,7 +1315,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             }
         }
         PPT(6);
-        const int slot = c & (RING_K - 1);
+        const int slot = c & (RK - 1);
         {
             unsigned spins = 0;
             while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[slot])) != c + 1) {
@@ -1379,7 +1388,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             const bool more = c + 1 < W;
             uint32_t ent = *(const uint32_t *)(Lb + prov_off);
             if (more) {
-                const int s1 = (c + 1) & (RING_K - 1);
+                const int s1 = (c + 1) & (RK - 1);
                 // MB c+1's MC output (normally long done): its flag and the
                 // slot data in one LDS round trip.  LDS serves one wave's
                 // accesses in order and the MC wave writes the slot before
@@ -1709,8 +1718,8 @@ __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0,
 // beside live row chains would lengthen the chains' L2 hand-offs).  Tail
 // workgroups come after every row workgroup in dispatch order, so no row
 // ever waits for them; the poll is bounded.
-template <int NW>
-__device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRing &R, int row_wgs)
+template <int NW, int RK>
+__device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRing<RK> &R, int row_wgs)
 {
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (wid >= NW) return;
@@ -1731,8 +1740,8 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
 // MC waves of one row (picture p, MB row r): walk the row's MBs c0, c0 + NMC,
 // ... into the row's LDS ring.  UPL / MEL as row_pp: where the row above's
 // unfiltered bottom rows come from (intra) / where this row's go.
-template <int NMC, bool PROF, bool UPL, bool MEL>
-__device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing &R,
+template <int NMC, bool PROF, bool UPL, bool MEL, int RK>
+__device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing<RK> &R,
                                        const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
     const PicDesc pd = a.pics[p];
@@ -1756,25 +1765,25 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
     if (c0 < a.w) mc_issue(a, pd, r * a.w + c0, v0, lane, ld);
     for (int c = c0; c < a.w; c += NMC) {
-        const int slot = c & (RING_K - 1);
+        const int slot = c & (RK - 1);
         const bool more = c + NMC < a.w;
         const uint32_t nv0 = more ? recrow[(size_t)(c + NMC) * 24 + (lane < 24 ? lane : 0)] : 0;
-        if (c >= RING_K) {
+        if (c >= RK) {
             unsigned spins = 0;
-            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RING_K + 1) {
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RK + 1) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }
             }
             wave_sync();
         }
         const unsigned long long t0 = PROF ? clock64() : 0;
-        const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], R.res[slot], R.db[slot]);
+        const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], Mw.res, R.db[slot]);
         if (type == MBT_IPCM) {
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
             ((uint32_t *)R.px[slot])[lane] = src[lane];
             if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
         } else if (type >= MBT_I4x4) {
-            mc_intra<UPL>(a.rec + pd.rec_base + r * a.w + c, mbx_up, a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, i4tab);
+            mc_intra<UPL, RK>(a.rec + pd.rec_base + r * a.w + c, mbx_up, a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, i4tab);
         }
         wave_sync();
         {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
@@ -1801,7 +1810,9 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
 {
     __shared__ PPLds L[RPW];
     __shared__ McScratch M[RPW * NMC];
-    __shared__ MbRing R[RPW];
+    constexpr int RK = RPW == 1 ? RING1 : RINGG;
+    static_assert(RK >= NMC * RPW, "tail workgroups use one ring db entry per wave as k_prep scratch");
+    __shared__ MbRing<RK> R[RPW];
     extern __shared__ unsigned long long lmbx[];
     const int S = a.S;
     const int hg = (a.h + RPW - 1) / RPW;
@@ -1810,13 +1821,13 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     // g are dispatched together, groups in order -- so a row's workgroup
     // only waits on earlier ones (the row above, an earlier step's rows)
     if (blockIdx.x >= a.npics * hg) {  // tail workgroup: the next batch's k_prep
-        prep_tail<NMC * RPW>(a, M, R[0], a.npics * hg);
+        prep_tail<NMC * RPW, RK>(a, M, R[0], a.npics * hg);
         return;
     }
     const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
     const int j = jg / hg, g = jg - j * hg, p = j * S + s;
     for (int q = 0; q < RPW; q++) {
-        if (threadIdx.x < RING_K) R[q].flag[threadIdx.x] = 0;
+        if (threadIdx.x < RK) R[q].flag[threadIdx.x] = 0;
         if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
     for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2) * RPW) L[0].i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
@@ -1835,10 +1846,10 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     unsigned long long *const me = mel ? lmbx + q * W32 : a.mbx + ((size_t)p * a.h + r) * W32;
     if (wid < 2) {
         __builtin_amdgcn_s_setprio(3);
-        if (!upl && !mel) row_pp<PROF, false, false>(a, p, r, L[q], wid, lane, &R[q], up, me);
-        else if (!upl) row_pp<PROF, false, true>(a, p, r, L[q], wid, lane, &R[q], up, me);
-        else if (mel) row_pp<PROF, true, true>(a, p, r, L[q], wid, lane, &R[q], up, me);
-        else row_pp<PROF, true, false>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        if (!upl && !mel) row_pp<PROF, false, false, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else if (!upl) row_pp<PROF, false, true, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else if (mel) row_pp<PROF, true, true, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else row_pp<PROF, true, false, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         // row finished: progress for the tail workgroups' start
         if (wid == 0 && lane == 0 && a.rows_done)
             __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1860,10 +1871,10 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
     McScratch &Mw = M[q * NMC + wid - 2];
-    if (!upl && !mel) mc_row<NMC, PROF, false, false>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (!upl) mc_row<NMC, PROF, false, true>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (mel) mc_row<NMC, PROF, true, true>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else mc_row<NMC, PROF, true, false>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (!upl) mc_row<NMC, PROF, false, true, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (mel) mc_row<NMC, PROF, true, true, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else mc_row<NMC, PROF, true, false, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
 }
 template __global__ void k_wgpp<3, false, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 1>(ReconArgs);
