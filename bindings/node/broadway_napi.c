@@ -29,6 +29,10 @@ typedef struct {
     H264SwDecInfo info;
     u32 pic_decode;
     u32 rgb;
+    /* rgb mode: the RGBA Buffer the last drain iteration allocated but found
+     * no picture for, kept for the next picture instead of thrown away */
+    napi_ref spare;
+    size_t spare_len;
 } JsDec;
 
 #define CHECK(env, call)                                                  \
@@ -42,6 +46,7 @@ typedef struct {
 static void finalize_dec(napi_env env, void *data, void *hint)
 {
     JsDec *d = (JsDec *)data;
+    if (d->spare) napi_delete_reference(env, d->spare);
     if (d->inst) H264SwDecRelease(d->inst);
     free(d);
 }
@@ -124,12 +129,24 @@ static napi_value js_decode(napi_env env, napi_callback_info cbi)
                     /* RGBA straight into a new JS Buffer (DecoderPost.js hands
                      * onPictureDecoded a fresh copy, :89-95) */
                     void *dst = NULL;
-                    if (napi_create_buffer(env, px * 4, &dst, &view) != napi_ok) {
+                    napi_status st = napi_generic_failure;
+                    if (d->spare) {
+                        if (d->spare_len == px * 4 && napi_get_reference_value(env, d->spare, &view) == napi_ok && view)
+                            st = napi_get_buffer_info(env, view, &dst, NULL);
+                        napi_delete_reference(env, d->spare);
+                        d->spare = NULL;
+                    }
+                    if (st != napi_ok && napi_create_buffer(env, px * 4, &dst, &view) != napi_ok) {
                         free(buf);
                         napi_throw_error(env, NULL, "cannot allocate picture buffer");
                         return NULL;
                     }
-                    if (H264SwDecNextPictureRGBA(d->inst, &pic, 0, (u8 *)dst) != H264SWDEC_PIC_RDY) break;
+                    if (H264SwDecNextPictureRGBA(d->inst, &pic, 0, (u8 *)dst) != H264SWDEC_PIC_RDY) {
+                        /* no picture: keep the Buffer for the next one */
+                        if (napi_create_reference(env, view, 1, &d->spare) == napi_ok) d->spare_len = px * 4;
+                        else d->spare = NULL;
+                        break;
+                    }
                 } else {
                     if (H264SwDecNextPicture(d->inst, &pic, 0) != H264SWDEC_PIC_RDY) break;
                     /* the picture is borrowed DPB memory (dpb.c:1443): hand JS a
