@@ -589,7 +589,7 @@ class DeviceRun:
         self.bufs = []
 
 
-def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3):
+def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0):
     """One single-GPU measurement of another SURVEY §8d config with the same
     step structure (records resident in HBM, one k_wgpp launch per step,
     HIP events on every launch) and the same untimed verification against
@@ -601,11 +601,15 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3):
     S = len(caps)
     w, h = caps[0].w_mbs, caps[0].h_mbs
     d_recs, d_coef, d_pics, srb, nslots, _ = upload(L, caps, nframes)
+    # both knobs are read once, when the engine is created
     os.environ["H264MI_MC_WAVES"] = str(mc_waves)
+    if rpw:
+        os.environ["H264MI_RPW"] = str(rpw)
     try:
         eng = Engine(w, h, S, nslots, device=torch.cuda.current_device())
     finally:
         os.environ.pop("H264MI_MC_WAVES", None)
+        os.environ.pop("H264MI_RPW", None)
     try:
         def step(k):
             if k + 1 < nframes:
@@ -632,6 +636,7 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3):
         gbs = r_alg / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
         return {"size": f"{w * 16}x{h * 16}", "streams": S, "seeds": seeds, "steps": steps,
                 "mc_waves_per_row_workgroup": mc_waves,
+                "rows_per_workgroup": eng.rows_per_workgroup(S),
                 "frames_per_s": round(S * steps / dt, 1), "avg_launch_us": round(launch_us, 2),
                 "picture_latency_ms": round(launch_us / 1e3, 3),
                 "alg_bytes_per_launch": int(r_alg), "achieved_GBs": round(gbs, 1),
@@ -654,6 +659,8 @@ def config_legs(L, torch):
         "cfg2_720p_ionly_1stream": run_leg(L, torch, 1, [1], 20, 4),
         "cfg5_2160p_1stream": run_leg(L, torch, 4, [100], 20, 4),
         "cfg5_2160p_1stream_2mc": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2),
+        "cfg5_2160p_1stream_2rows": run_leg(L, torch, 4, [100], 20, 4, rpw=2),
+        "cfg5_2160p_1stream_2mc_2rows": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2, rpw=2),
     }
 
 

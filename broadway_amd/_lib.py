@@ -164,6 +164,8 @@ def mi() -> C.CDLL:
     L.h264mi_engine_kernel.restype = C.c_char_p
     L.h264mi_engine_errors.argtypes = [vp]
     L.h264mi_engine_errors.restype = u32
+    L.h264mi_engine_rows_per_workgroup.argtypes = [vp, C.c_int]
+    L.h264mi_engine_rows_per_workgroup.restype = C.c_int
     L.h264mi_engine_last_timing.argtypes = [vp, C.POINTER(C.c_float)]
     L.h264mi_engine_last_timing.restype = i32
     L.h264mi_engine_set_timing.argtypes = [vp, i32]

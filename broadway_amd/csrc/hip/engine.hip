@@ -215,6 +215,20 @@ static int launch_prep(h264mi_engine *e, int npics, const MbRec *d_rec, const in
 // known (next_rec != NULL), tail workgroups that run the next batch's k_prep
 // as this launch's rows drain.  k_prep outputs alternate between two buffer
 // halves; stream order separates writer and reader.
+// rows per workgroup: while the batch's rows fit the chip as single-row
+// workgroups (three per CU), one row each -- a picture's latency is the
+// bound and three chains on one CU contend; beyond that, three rows per
+// workgroup with LDS hand-offs inside (measured, 1080p: S = 8 410 vs 440 us
+// per launch; S = 32 1368 vs 1113 us).  H264MI_RPW fixes it; the LDS budget
+// (rpw_max) and the 2-MC-wave builds cap it.
+static int rows_per_wg(const h264mi_engine *e, int S)
+{
+    int rpw = e->rpw_env ? e->rpw_env : (S * e->h > 3 * e->ncu ? 3 : 1);
+    if (rpw > e->rpw_max) rpw = e->rpw_max;
+    if (e->mc_waves == 2 && rpw > 2) rpw = 2;
+    return rpw;
+}
+
 static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, const int16_t *d_coef,
                         const PicDesc *d_pics, const MbRec *next_rec, const int16_t *next_coef,
                         const PicDesc *next_pics)
@@ -270,14 +284,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     }
     const bool rec = e->timing || rec_tev;
     e->last_kernel = "k_wgpp";
-    // rows per workgroup: while the batch's rows fit the chip as single-row
-    // workgroups (three per CU), one row each -- a picture's latency is the
-    // bound and three chains on one CU contend; beyond that, three rows per
-    // workgroup with LDS hand-offs inside (measured, 1080p: S = 8 410 vs
-    // 440 us per launch; S = 32 1368 vs 1113 us)
-    int rpw = e->rpw_env ? e->rpw_env : (S * e->h > 3 * e->ncu ? 3 : 1);
-    if (rpw > e->rpw_max) rpw = e->rpw_max;
-    if (e->mc_waves == 2 && rpw > 2) rpw = 2;
+    const int rpw = rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
     const size_t lmbx = (size_t)(rpw - 1) * e->w * 256;
     if (a.prof) {
@@ -416,6 +423,11 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     HIPCHECK(hipStreamSynchronize(e->st));
     for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
     return 0;
+}
+
+extern "C" int h264mi_engine_rows_per_workgroup(h264mi_engine *e, int npics)
+{
+    return e && npics > 0 ? rows_per_wg(e, npics) : 0;
 }
 
 extern "C" uint32_t h264mi_engine_errors(h264mi_engine *e)

@@ -149,6 +149,10 @@ class Engine:
     def errors(self) -> int:
         return int(self._L.h264mi_engine_errors(self._h))
 
+    def rows_per_workgroup(self, npics: int) -> int:
+        """MB rows per k_wgpp workgroup for a batch of npics pictures."""
+        return int(self._L.h264mi_engine_rows_per_workgroup(self._h, npics))
+
     def last_timing_us(self):
         v = (C.c_float * 2)()
         if self._L.h264mi_engine_last_timing(self._h, v) != 0:

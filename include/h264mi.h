@@ -209,6 +209,9 @@ int  h264mi_engine_sync(h264mi_engine *e);
  * range errors (reference transform.c:181) or a bounded wait that expired;
  * flags accumulate over every launch and are collected by h264mi_engine_sync */
 uint32_t h264mi_engine_errors(h264mi_engine *e);
+/* MB rows per k_wgpp workgroup the engine launches for a batch of npics
+ * pictures (1..3: by batch size, H264MI_RPW, the LDS budget) */
+int  h264mi_engine_rows_per_workgroup(h264mi_engine *e, int npics);
 /* duration (us) of the last batch's k_wgpp launch: us2[1] (us2[0] = 0);
  * needs H264MI_TIMING in the environment */
 int  h264mi_engine_last_timing(h264mi_engine *e, float *us2);
