@@ -90,6 +90,23 @@ REF_CASES = {
     "ref_all_1080p": (3, 400, dict(nframes=16, ref_mod_pct=50, mmco_pct=40, lt_idr_pct=50, nonref_pct=20), False),
 }
 CASES.update(REF_CASES)
+# Degenerate picture shapes (one MB, one MB row, one MB column, thin strips):
+# every neighbour-availability, ring, row-hand-off and edge-clamp corner of
+# the row workgroups, with heavy off-picture MVs, intra-heavy P pictures,
+# constrained intra and one slice per MB
+_E = dict(nframes=8, crop_bottom=0, gop=5, offpic_pct=25, mv_jitter=8)
+EDGE_CASES = {
+    "edge_1x1_i": (1, 901, dict(_E, w_mbs=1, h_mbs=1, slices=1, im_pcm=20), False),
+    "edge_1x1_ip": (2, 902, dict(_E, w_mbs=1, h_mbs=1, slices=1), False),
+    "edge_1x9_ip": (2, 903, dict(_E, w_mbs=1, h_mbs=9, slices=3, pm_intra=30), False),
+    "edge_9x1_ip": (2, 904, dict(_E, w_mbs=9, h_mbs=1, slices=2, dbf_idc2_pct=50), False),
+    "edge_2x2_ip_mbslices": (2, 905, dict(_E, w_mbs=2, h_mbs=2, slices=4, cip=1, pm_intra=40), False),
+    "edge_2x13_ip": (2, 906, dict(_E, w_mbs=2, h_mbs=13, slices=2, num_ref_frames=4), False),
+    "edge_17x2_ip": (2, 907, dict(_E, w_mbs=17, h_mbs=2, slices=3, chroma_qp_offset=9), False),
+    "edge_31x1_i": (1, 908, dict(_E, w_mbs=31, h_mbs=1, slices=1), False),
+    "edge_3x23_ip_idc1": (2, 909, dict(_E, w_mbs=3, h_mbs=23, slices=2, dbf_idc1_pct=40), False),
+}
+CASES.update(EDGE_CASES)
 # bench.py config legs: 24 pictures each
 for s in (1, 2, 3, 4):
     CASES[f"leg_cfg2_720p_s{s}"] = (1, s, dict(nframes=24), False)

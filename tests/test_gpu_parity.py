@@ -54,6 +54,26 @@ def test_swdec_api_vs_reference(name):
     assert md5s(frames) == c["frames"]
 
 
+EDGE = sorted(n for n in CASES if n.startswith("edge_"))
+
+
+@pytest.mark.parametrize("rpw", [None, "2", "3"])
+def test_swdec_degenerate_shapes_vs_reference(rpw, monkeypatch):
+    """One-MB, one-row, one-column and thin-strip pictures through H264SwDec*
+    (25 % off-picture MVs, intra-heavy P pictures, constrained intra, a slice
+    per MB): the row workgroup's first/last-MB, ring, hand-off and clamp
+    corners; rpw forces 2 or 3 MB rows per k_wgpp workgroup (LDS hand-offs
+    inside the group, partial last groups)."""
+    if rpw:
+        monkeypatch.setenv("H264MI_RPW", rpw)
+    assert len(EDGE) >= 9
+    for name in EDGE:
+        c = CASES[name]
+        frames, errors = swdec_decode(stream(c), no_reorder=c["no_reorder"])
+        assert errors == 0, name
+        assert md5s(frames) == c["frames"], name
+
+
 PICS = [n for n in CASES if "pics" in CASES[n]]
 
 
