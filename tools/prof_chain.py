@@ -76,3 +76,27 @@ st("delta", delta)
 print(f"  H start gated by the row above: {gated_top.mean() * 100:.1f} % of MBs")
 per = np.diff(Cst[:, rows, :], axis=2)[:, :, 2:w - 3]
 st("period", per)
+
+# where the hand-off tail and the period come from: by row band and by column band
+print("by row band (all columns 2..w-3):")
+for r0, r1 in ((1, 4), (4, 8), (8, 24), (24, 48), (48, h - 1)):
+    if r1 <= r0:
+        continue
+    pr = np.diff(Cst[:, r0:r1, :], axis=2)[:, :, 2:w - 3]
+    tp = (Cst[:, r0:r1, cols] - B[:, r0:r1, cols])
+    g = tp > 0.05
+    dl = (Cst[:, r0:r1, cols] - E[:, r0 - 1:r1 - 1, cols])[g]
+    print(f"  rows {r0:2d}..{r1 - 1:2d}: period mean {pr.mean():.3f} p50 {np.percentile(pr, 50):.3f}"
+          f" | top mean {tp.mean():.3f} | delta mean {dl.mean() if dl.size else 0:.3f}"
+          f" p90 {np.percentile(dl, 90) if dl.size else 0:.3f} | gated {g.mean() * 100:.0f} %")
+print("deep rows by column band:")
+for c0, c1 in ((2, 16), (16, 40), (40, 64), (64, 88), (88, w - 2)):
+    tp = Cst[:, rows, c0:c1] - B[:, rows, c0:c1]
+    g = tp > 0.05
+    dl = (Cst[:, 8:h - 1, c0:c1] - E[:, 7:h - 2, c0:c1])[g]
+    pr = np.diff(Cst[:, rows, c0 - 1:c1], axis=2)
+    print(f"  cols {c0:3d}..{c1 - 1:3d}: period mean {pr.mean():.3f} | top mean {tp.mean():.3f}"
+          f" | delta mean {dl.mean():.3f} p50 {np.percentile(dl, 50):.3f} p90 {np.percentile(dl, 90):.3f}")
+# row 0's end and the second-to-last row's (the last row publishes nothing,
+# so its H end is not stamped)
+print(f"  row 0 end (us, mean over pictures): {D[:, 0, w - 1].mean():.1f}; row {h - 2} end: {D[:, h - 2, w - 1].mean():.1f}")
