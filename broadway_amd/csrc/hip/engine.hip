@@ -40,6 +40,7 @@ struct h264mi_engine {
     int prep_parity;
     const void *prepped_rec, *prepped_pics;
     unsigned long long *d_rows_done;   // row workgroups finished, all launches (tail-prep trigger)
+    int prep_wgs;                      // tail workgroups per launch (H264MI_PREP_WGS, default 2048)
     unsigned long long rows_launched;
     int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
     int mc_waves;                      // MC waves per row workgroup: 3, or 2 (H264MI_MC_WAVES, sizing study)
@@ -148,6 +149,8 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * nslots * nstreams, e->st);
     (void)hipMemsetAsync(e->d_rows_done, 0, sizeof(unsigned long long), e->st);
     {
+        const char *pw = getenv("H264MI_PREP_WGS");
+        e->prep_wgs = pw && atoi(pw) > 0 ? atoi(pw) : 2048;
         const char *pa = getenv("H264MI_PREP_AT");
         e->prep_at_pct = pa ? atoi(pa) : 0;
         const char *mw = getenv("H264MI_MC_WAVES");
@@ -265,7 +268,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     a.res = e->d_res + hb * mbs * 384;
     const int rows = npics * e->h;
     if (next_rec) {
-        a.prep_wgs = 2048;
+        a.prep_wgs = e->prep_wgs;
         a.rows_done = e->d_rows_done;
         a.prep_target = e->rows_launched + (unsigned long long)((long long)rows * e->prep_at_pct / 100);
         a.n_rec = next_rec; a.n_coef = next_coef; a.n_pics = next_pics;
