@@ -1718,11 +1718,19 @@ __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0,
 // beside live row chains would lengthen the chains' L2 hand-offs).  Tail
 // workgroups come after every row workgroup in dispatch order, so no row
 // ever waits for them; the poll is bounded.
-template <int NW, int RK>
+// NW waves take MBs: the NM of them with a McScratch of M, the others
+// (single-row layout: the two row waves' slots) one carved from the unused
+// ring samples.  The extra waves only for batches of 4 and more pictures:
+// measured, 1080p S = 8 +0.5 % frames/s, 2160p S = 1 658 vs 646 us
+// (profiles/r31_*)
+template <int NW, int NM, int RK>
 __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRing<RK> &R, int row_wgs)
 {
+    static_assert(NW <= RK && (NW - NM) * sizeof(McScratch) <= sizeof(R.px), "tail scratch");
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (wid >= NW) return;
+    const int nw = a.S >= 4 ? NW : NM;
+    if (wid >= nw) return;
+    McScratch *const Mx = (McScratch *)(void *)R.px;
     unsigned spins = 0;
     while (__hip_atomic_load(a.rows_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.prep_target) {
         __builtin_amdgcn_s_sleep(64);
@@ -1733,8 +1741,8 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
     pa.nmbs_total = a.n_nmbs_total; pa.w = a.w; pa.h = a.h;
     const Tabs T = load_tabs(lane);
     const int t = blockIdx.x - row_wgs;
-    for (int g = t * NW + wid; g < pa.nmbs_total; g += a.prep_wgs * NW)
-        prep_mb(pa, g, lane, M[wid], R.db[wid], T);
+    for (int g = t * nw + wid; g < pa.nmbs_total; g += a.prep_wgs * nw)
+        prep_mb(pa, g, lane, wid < NM ? M[wid] : Mx[wid - NM], R.db[wid], T);
 }
 
 // MC waves of one row (picture p, MB row r): walk the row's MBs c0, c0 + NMC,
@@ -1821,7 +1829,7 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     // g are dispatched together, groups in order -- so a row's workgroup
     // only waits on earlier ones (the row above, an earlier step's rows)
     if (blockIdx.x >= a.npics * hg) {  // tail workgroup: the next batch's k_prep
-        prep_tail<NMC * RPW, RK>(a, M, R[0], a.npics * hg);
+        prep_tail<RPW == 1 ? NMC + 2 : NMC * RPW, NMC * RPW, RK>(a, M, R[0], a.npics * hg);
         return;
     }
     const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
