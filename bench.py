@@ -83,6 +83,9 @@ def parse_args(argv=None):
     ap.add_argument("--pipe", type=int, default=int(os.environ.get("BENCH_PIPE", "1")),
                     help="steps per launch (1 or 2): with 2, a launch reconstructs two consecutive pictures of "
                          "every stream and the second's rows start as the reference rows they read are final")
+    ap.add_argument("--aligned", action="store_true",
+                    help="all streams' GOPs aligned, pictures W .. W+K-1 timed (no IDR in short windows); "
+                         "default: GOP phases staggered over the streams")
     ap.add_argument("--dry-run", action="store_true",
                     help="no device calls: sharding, host parse, step loop and reductions only (CPU tests)")
     return ap.parse_args(argv)
@@ -159,9 +162,10 @@ def prepare(config, seeds, nframes, overrides=None):
 
 def pack(caps, npics):
     """Host image of every record batch / coefficient block / picture
-    descriptor of pictures [0, npics) of every stream.  Step k's records are
-    contiguous, picture-major (stream s at k*S + s); PicDesc.rec_base is
-    relative to the step's records, coef_base to the whole coefficient pool."""
+    descriptor of pictures [0, npics) of every stream.  Picture k of stream s
+    is record batch k*S + s; its PicDesc (row k*S + s) has rec_base relative
+    to the whole record pool and coef_base to the whole coefficient pool, so
+    a launch may take any picture of any stream (DeviceRun's plans)."""
     S = len(caps)
     nmbs = caps[0].w_mbs * caps[0].h_mbs
     nslots = max(c.nslots for c in caps)
@@ -177,26 +181,23 @@ def pack(caps, npics):
             recs[off:off + rec_bytes] = C.string_at(p.rec, rec_bytes)
             if p.ncoef:
                 coef_parts.append(C.string_at(p.coef, p.ncoef * 32))
-            pics[j * S + s] = (s * nmbs, s * nslots, p.cur_slot, 0, cbase, 0, 0, 0)
+            pics[j * S + s] = ((j * S + s) * nmbs, s * nslots, p.cur_slot, 0, cbase, 0, 0, 0)
             cbase += p.ncoef
     coefs = b"".join(coef_parts) + b"\0" * 64
     return recs, coefs, pics, rec_bytes * S, nslots
 
 
-def upload(L, caps, npics, packed=None):
-    """pack() into HBM; returns (d_recs, d_coef, d_pics, step_rec_bytes,
-    nslots, resident bytes)."""
-    recs, coefs, pics, step_rec_bytes, nslots = packed or pack(caps, npics)
-    d_recs = L.h264mi_device_alloc(len(recs))
-    d_coef = L.h264mi_device_alloc(len(coefs))
-    d_pics = L.h264mi_device_alloc(pics.nbytes)
-    if not (d_recs and d_coef and d_pics):
-        raise RuntimeError("device allocation failed")
+def upload(eng, packed):
+    """pack() output into HBM of the engine's GPU (engine-scoped allocations:
+    a rank's buffers live on its own device whatever the thread's current
+    HIP device is); returns (d_recs, d_coef, resident bytes)."""
+    recs, coefs = packed[0], packed[1]
+    d_recs = eng.alloc(len(recs))
+    d_coef = eng.alloc(len(coefs))
     rb = (C.c_char * len(recs)).from_buffer(recs)
-    assert L.h264mi_copy_h2d(d_recs, rb, len(recs)) == 0
-    assert L.h264mi_copy_h2d(d_coef, coefs, len(coefs)) == 0
-    assert L.h264mi_copy_h2d(d_pics, pics.ctypes.data, pics.nbytes) == 0
-    return d_recs, d_coef, d_pics, step_rec_bytes, nslots, len(recs) + len(coefs)
+    eng.upload(d_recs, rb, len(recs))
+    eng.upload(d_coef, coefs, len(coefs))
+    return d_recs, d_coef, len(recs) + len(coefs)
 
 
 def slots_read(recs, nmbs, i):
@@ -259,16 +260,6 @@ def schedule(recs, pics, S, nmbs, warmup, steps, P):
         if ok:
             return [(k, P) for k in range(0, n, P)]
     return [(k, 1) for k in range(n)]
-
-
-def pack_steps(pics, S, nmbs, P):
-    """PicDesc array for P-step launches: picture j * S + s of the launch at
-    step k0 has rec_base relative to step k0's records."""
-    out = pics.copy()
-    for i in range(len(pics)):
-        k, s = divmod(i, S)
-        out[i][0] = ((k % P) * S + s) * nmbs
-    return out
 
 
 def golden_frames(config, seed, overrides):
@@ -450,31 +441,6 @@ def end_to_end(streams, nframes, reps=3):
         shutil.rmtree(td, ignore_errors=True)
 
 
-def verify_all(eng, launch, sched, caps, seeds, config, overrides, cur_slots=None):
-    """Untimed verification pass: run every launch of the schedule again and
-    compare every picture of every stream with the reference decoder's MD5s
-    (POC type 2: output order == decode order, frame k = picture k) right
-    after its launch (the pictures of one launch write distinct slots).
-    Returns (ok, frames checked, frames without a fixture)."""
-    refs = [golden_frames(config, sd, overrides) for sd in seeds]
-    ok, n, missing = True, 0, 0
-    for i, (k0, P) in enumerate(sched):
-        launch(i)
-        eng.sync()
-        for k in range(k0, k0 + P):
-            for s, c in enumerate(caps):
-                ref = refs[s]
-                if ref is None or k >= len(ref):
-                    missing += 1
-                    continue
-                slot = c.pictures[k].cur_slot if cur_slots is None else int(cur_slots[k][s])
-                got = hashlib.md5(eng.read(s, slot).tobytes()).hexdigest()
-                n += 1
-                if got != ref[k]:
-                    ok = False
-    return ok, n, missing
-
-
 def load_traffic():
     """HBM bytes per step from the committed rocprofv3 PMC passes
     (tools/pmc_traffic.py -> profiles/traffic.json), or None."""
@@ -487,17 +453,65 @@ def load_traffic():
         return None
 
 
+GOP = 60                   # configs[3]: 1 I + 59 P per GOP; the bench streams are one GOP long
+
+
+def gop_phases(S: int, gop: int = GOP):
+    """GOP phase of each stream: stream s is s*gop/S pictures into its GOP
+    when the first warmup step starts, so the S streams' IDR pictures are
+    spread evenly over the steps (independent streams that did not start
+    together) and every window of `gop` steps reconstructs S I pictures out
+    of S*gop -- the configs[3] mix of 1 I per 60 in every step window, not
+    only in the one step that happens to hold picture 0."""
+    return [(s * gop) // S for s in range(S)]
+
+
+def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None):
+    """Per launch, per step of the launch, the picture index of each stream;
+    returns (launches, pre-roll launch count).
+
+    phases None: launches follow `sched` ((first step, steps) pairs), stream
+    s decodes picture k at step k.  Otherwise warmup step v (then timed step
+    v - warmup) decodes picture (v + phases[s]) % N of stream s: a stream of
+    N pictures starting with its IDR is decoded cyclically -- after picture
+    N-1 comes picture 0 again, an IDR (no reference is read across it), so
+    the pictures and MD5s are the stream's own.  An untimed pre-roll of
+    max(phases) launches first brings stream s to picture phases[s]: its
+    pictures 0 .. phases[s]-1 in order, preceded by repeats of the IDR
+    picture 0 (which reads no reference, so repeating it is idempotent)."""
+    if phases is None:
+        return [[[k] * S for k in range(k0, k0 + P)] for k0, P in sched], 0
+    R = max(phases)
+    pre = [[[max(0, u - R + ph) for ph in phases]] for u in range(R)]
+    main = [[[(v + ph) % N for ph in phases]] for v in range(warmup + steps)]
+    return pre + main, R
+
+
 class _DryEngine:
-    """--dry-run stand-in for broadway_amd.engine.Engine: no device calls."""
+    """--dry-run stand-in for broadway_amd.engine.Engine: no device calls;
+    allocations are fake addresses that remember the device they were asked
+    for (the gloo test checks every rank's buffers name its own GPU)."""
 
-    def __init__(self, *a, **k):
+    def __init__(self, w=0, h=0, S=0, nslots=0, device=0):
         self.launches = 0
+        self.device = device
+        self._next = 1 << 40
+        self.alloc_dev = {}
 
-    def decode_device(self, *a):
-        self.launches += 1
+    def alloc(self, n):
+        p = self._next
+        self._next += (int(n) + 4095) & ~4095
+        self.alloc_dev[p] = self.device
+        return p
 
-    def decode_device_next(self, *a):
-        self.launches += 1
+    def free(self, p):
+        self.alloc_dev.pop(p, None)
+
+    def upload(self, *a):
+        pass
+
+    def pointer_device(self, p):
+        return self.alloc_dev.get(p, -1)
 
     def decode_device_steps(self, *a):
         self.launches += 1
@@ -520,73 +534,188 @@ class _DryEngine:
     def kernel_name(self):
         return "dry-run"
 
+    def read(self, *a):
+        return np.zeros(1, np.uint8)
+
     def close(self):
         pass
 
 
 class DeviceRun:
-    """The bench's device-resident path for one rank: records, coefficient
-    blocks and descriptors of pictures [0, warmup + steps) of every stream in
-    HBM, an engine for the S streams, and the launch schedule (P steps per
-    launch when the streams allow it, physical slots renamed for it; the next
-    launch's k_prep in each launch's tail).  dry: no device calls."""
+    """The bench's device-resident path for one rank: the engine for its S
+    streams on its own GPU (`device`), every picture's records, coefficient
+    blocks and descriptors in that GPU's HBM (engine-scoped allocations,
+    placement asserted per buffer), and a launch plan (launch_plan: GOP
+    phases, or P steps per launch with physical slots renamed for P = 2; the
+    next launch's k_prep runs in each launch's tail).  dry: no device calls."""
 
-    def __init__(self, L, caps, warmup, steps, pipe, device=0, dry=False):
-        self.L, self.S = L, len(caps)
-        S, nframes = self.S, warmup + steps
-        w, h = caps[0].w_mbs, caps[0].h_mbs
-        nmbs = w * h
-        packed = pack(caps, nframes)
-        recs_h, _, pics_h, self.srb, nslots = packed
-        if pipe > 1:
-            nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots)
-            packed = packed[:4] + (nslots,)
-        self.sched = schedule(recs_h, pics_h, S, nmbs, warmup, steps, pipe)
-        self.P = self.sched[0][1]
-        self.cur_slots = pics_h[:, 2].reshape(nframes, S).copy()
-        self.bufs = []
-        if dry:
-            self.d_recs = self.d_coef = self.pics_base = 0
-            self.resident = 0
-            self.eng = _DryEngine()
-            return
+    def __init__(self, L, caps, warmup, steps, pipe=1, device=0, dry=False, phases=None):
         from broadway_amd.engine import Engine
-        self.d_recs, self.d_coef, d_pics, _, nslots, self.resident = upload(L, caps, nframes, packed)
-        self.bufs = [self.d_recs, self.d_coef, d_pics]
-        self.pics_base = d_pics
-        if self.P > 1:
-            ps = pack_steps(pics_h, S, nmbs, self.P)
-            d = L.h264mi_device_alloc(ps.nbytes)
-            assert d and L.h264mi_copy_h2d(d, ps.ctypes.data, ps.nbytes) == 0
-            self.bufs.append(d)
-            self.pics_base = d
-        self.eng = Engine(w, h, S, nslots, device=device)
+        self.L, self.S, self.caps = L, len(caps), caps
+        S = self.S
+        w, h = caps[0].w_mbs, caps[0].h_mbs
+        self.nmbs = nmbs = w * h
+        self.N = N = min(c.npics for c in caps)
+        self.device = device
+        packed = pack(caps, N)
+        recs_h, _, pics_h, _, nslots = packed
+        if phases is not None:
+            pipe = 1
+        self.sched = None
+        if phases is None:
+            if warmup + steps > N:
+                raise ValueError(f"{warmup}+{steps} steps but the streams hold {N} pictures")
+            if pipe > 1:
+                nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots)
+            self.sched = schedule(recs_h, pics_h, S, nmbs, warmup, steps, pipe)
+        self.P = self.sched[0][1] if self.sched else 1
+        self.nslots = nslots
+        self.pics_h = pics_h
+        self.slot_of = pics_h[:, 2].reshape(N, S).copy()
+        self.is_i = [[c.pictures[k].n_inter == 0 for c in caps] for k in range(N)]
+        self.eng = _DryEngine(device=device) if dry else Engine(w, h, S, nslots, device=device)
         if self.P > 1:
             self.eng.set_steps(self.P)
+        self.d_recs, self.d_coef, self.resident = upload(self.eng, packed)
+        self.bufs = [self.d_recs, self.d_coef]
+        self.d_desc = 0
+        self.set_plan(warmup, steps, phases)
+
+    def set_plan(self, warmup, steps, phases=None):
+        """(Re)build the launch plan and its descriptor table in HBM."""
+        S, P = self.S, self.P
+        self.warmup, self.steps, self.phases = warmup, steps, phases
+        self.launches, self.n_pre = launch_plan(self.N, S, warmup, steps, phases, self.sched)
+        self.n_warm = self.n_pre + sum(1 for k0, _ in self.sched if k0 < warmup) if self.sched else self.n_pre + warmup
+        d = np.zeros((len(self.launches) * P * S, 8), dtype=np.uint32)
+        for i, launch in enumerate(self.launches):
+            for j, step in enumerate(launch):
+                for s, k in enumerate(step):
+                    d[(i * P + j) * S + s] = self.pics_h[k * S + s]
+        if self.d_desc:
+            self.eng.free(self.d_desc)
+            self.bufs.remove(self.d_desc)
+        self.d_desc = self.eng.alloc(d.nbytes)
+        self.bufs.append(self.d_desc)
+        self.eng.upload(self.d_desc, d.ctypes.data, d.nbytes)
+
+    def placement(self):
+        """Device of every HBM buffer of this run: [(name, device)]."""
+        names = ["records", "coefficients", "descriptors"]
+        return [(n, self.eng.pointer_device(p)) for n, p in zip(names, self.bufs)]
 
     def launch(self, i):
-        """Launch i of the schedule: P steps; the next launch's k_prep runs
-        in its tail workgroups."""
-        S, srb = self.S, self.srb
-        k0, p = self.sched[i]
-        args = (self.d_recs + k0 * srb, self.d_coef, self.pics_base + k0 * S * 32)
-        if i + 1 < len(self.sched):
-            k1 = self.sched[i + 1][0]
-            self.eng.decode_device_steps(S, p, *args, self.d_recs + k1 * srb, self.d_coef,
-                                         self.pics_base + k1 * S * 32)
+        """Launch i of the plan: P steps of the S streams; the next launch's
+        k_prep runs in its tail workgroups."""
+        S, P = self.S, self.P
+        desc = self.d_desc + i * P * S * 32
+        if i + 1 < len(self.launches):
+            self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc,
+                                         self.d_recs, self.d_coef, desc + P * S * 32)
         else:
-            self.eng.decode_device_steps(S, p, *args)
+            self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc)
+
+    def timed_pictures(self):
+        """(stream, picture) of every picture the timed launches decode."""
+        return [(s, k) for launch in self.launches[self.n_warm:] for step in launch for s, k in enumerate(step)]
+
+    def verify(self, refs):
+        """Untimed re-run of the whole plan, every picture compared with the
+        reference decoder's MD5 (refs[s][k]; POC type 2: output order ==
+        decode order) right after its launch (the pictures of one launch
+        write distinct slots).  Pre-roll repeats of the IDR are checked once.
+        Returns (ok, frames checked in warmup + timed, frames without a
+        fixture, pre-roll frames checked)."""
+        ok, n, missing, n_pre = True, 0, 0, 0
+        last = [None] * self.S
+        for i, launch in enumerate(self.launches):
+            self.launch(i)
+            self.eng.sync()
+            for step in launch:
+                for s, k in enumerate(step):
+                    pre = i < self.n_pre
+                    if pre and last[s] == k:
+                        continue
+                    last[s] = k
+                    if refs[s] is None or k >= len(refs[s]):
+                        missing += 0 if pre else 1
+                        continue
+                    got = hashlib.md5(self.eng.read(s, int(self.slot_of[k][s])).tobytes()).hexdigest()
+                    if pre:
+                        n_pre += 1
+                    else:
+                        n += 1
+                    ok &= got == refs[s][k]
+        return ok, n, missing, n_pre
+
+    def check_resident(self, refs):
+        """After the plan ran: every frame slot still holds the last picture
+        the plan decoded into it -- compare those (the timed launches' own
+        output, not a re-run) with the reference MD5s.  Returns (ok, n)."""
+        last = {}
+        for launch in self.launches:
+            for step in launch:
+                for s, k in enumerate(step):
+                    last[(s, int(self.slot_of[k][s]))] = k
+        ok, n = True, 0
+        for (s, slot), k in sorted(last.items()):
+            if refs[s] is None or k >= len(refs[s]):
+                continue
+            ok &= hashlib.md5(self.eng.read(s, slot).tobytes()).hexdigest() == refs[s][k]
+            n += 1
+        return ok, n
 
     def close_engine(self):
         if self.eng is not None:
+            for p in self.bufs:
+                self.eng.free(p)
+            self.bufs = []
             self.eng.close()
             self.eng = None
 
     def free(self):
         self.close_engine()
-        for p in self.bufs:
-            self.L.h264mi_device_free(p)
-        self.bufs = []
+
+
+def timed_run(run, dist, torch, sync, stride):
+    """Pre-roll + warmup launches untimed, then the timed launches bracketed
+    by a barrier and device syncs; HIP events on every stride-th timed
+    launch, carried by k_wgpp's own dispatch packet.  Returns (wall seconds
+    max over ranks, avg k_wgpp us of the sampled launches, sampled launch
+    indices)."""
+    for i in range(run.n_warm):
+        run.launch(i)
+    run.eng.sync()
+    sync()
+    ntimed = len(run.launches) - run.n_warm
+    run.eng.set_timing(ntimed, stride=stride)
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(run.n_warm, len(run.launches)):
+        run.launch(i)
+    run.eng.sync()
+    sync()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    dt = max_over_ranks(dist, torch, t1 - t0)
+    _, us, nb = run.eng.timing_report()
+    sampled = [run.n_warm + j for j in range(0, ntimed, stride)][:nb]
+    return dt, us / max(nb, 1), sampled
+
+
+def alg_bytes(run, launch_ids):
+    """SURVEY §8d R_alg of the listed launches: MC reference footprint +
+    32 B per coded 4x4 block + 96-B MB record, per picture."""
+    tot = 0
+    for i in launch_ids:
+        for step in run.launches[i]:
+            for s, k in enumerate(step):
+                p = run.caps[s].pictures[k]
+                tot += p.alg_ref_bytes + 32 * p.n_coded + MBREC * run.nmbs
+    return tot
 
 
 def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0):
@@ -594,59 +723,37 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0):
     step structure (records resident in HBM, one k_wgpp launch per step,
     HIP events on every launch) and the same untimed verification against
     the reference MD5s.  Returns a dict for the bench line."""
-    from broadway_amd.engine import Engine
     nframes = warmup + steps
     streams, caps = prepare(config, seeds, nframes)
     assert all(c.errors == 0 and c.npics >= nframes for c in caps), "leg stream preparation failed"
     S = len(caps)
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    d_recs, d_coef, d_pics, srb, nslots, _ = upload(L, caps, nframes)
     # both knobs are read once, when the engine is created
     os.environ["H264MI_MC_WAVES"] = str(mc_waves)
     if rpw:
         os.environ["H264MI_RPW"] = str(rpw)
     try:
-        eng = Engine(w, h, S, nslots, device=torch.cuda.current_device())
+        run = DeviceRun(L, caps, warmup, steps, 1, device=torch.cuda.current_device())
     finally:
         os.environ.pop("H264MI_MC_WAVES", None)
         os.environ.pop("H264MI_RPW", None)
     try:
-        def step(k):
-            if k + 1 < nframes:
-                eng.decode_device_next(S, d_recs + k * srb, d_coef, d_pics + k * S * 32,
-                                       d_recs + (k + 1) * srb, d_coef, d_pics + (k + 1) * S * 32)
-            else:
-                eng.decode_device(S, d_recs + k * srb, d_coef, d_pics + k * S * 32)
-        for k in range(warmup):
-            step(k)
-        eng.sync()
-        eng.set_timing(steps, stride=1)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for k in range(warmup, nframes):
-            step(k)
-        eng.sync()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        _, us, nb = eng.timing_report()
-        launch_us = us / max(nb, 1)
-        r_alg = sum(c.pictures[k].alg_ref_bytes + 32 * c.pictures[k].n_coded + MBREC * w * h
-                    for c in caps for k in range(warmup, nframes)) / steps
-        ok, n, missing = verify_all(eng, step, [(k, 1) for k in range(nframes)], caps, seeds, config, {})
+        dt, launch_us, sampled = timed_run(run, None, torch, torch.cuda.synchronize, 1)
+        r_alg = alg_bytes(run, sampled) / max(len(sampled), 1)
+        refs = [golden_frames(config, sd, {}) for sd in seeds]
+        ok, n, missing, _ = run.verify(refs)
         gbs = r_alg / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
         return {"size": f"{w * 16}x{h * 16}", "streams": S, "seeds": seeds, "steps": steps,
                 "mc_waves_per_row_workgroup": mc_waves,
-                "rows_per_workgroup": eng.rows_per_workgroup(S),
+                "rows_per_workgroup": run.eng.rows_per_workgroup(S),
                 "frames_per_s": round(S * steps / dt, 1), "avg_launch_us": round(launch_us, 2),
                 "picture_latency_ms": round(launch_us / 1e3, 3),
                 "alg_bytes_per_launch": int(r_alg), "achieved_GBs": round(gbs, 1),
                 "frac_hbm": round(gbs / HBM_PEAK_GBS, 5),
                 "bitexact": {"ok": ok, "frames_checked": n, "frames_without_fixture": missing},
-                "device_errors": eng.errors()}
+                "device_errors": run.eng.errors()}
     finally:
-        eng.close()
-        for p in (d_recs, d_coef, d_pics):
-            L.h264mi_device_free(p)
+        run.free()
 
 
 def config_legs(L, torch):
@@ -670,71 +777,81 @@ def main(argv=None):
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(a.gpus, argv))
     torch, dist, rank, local, world = dist_setup(a.gpus)
+    if not a.dry_run:
+        # the rank's GPU is the current device from here on (torch and the
+        # HIP runtime libh264mi.so shares with it); the engine and every
+        # buffer of the run are bound to it explicitly as well
+        torch.cuda.set_device(local)
     from broadway_amd import _lib
     L = _lib.mi()
 
     S = a.streams
     seeds = shard_seeds(rank, S)
-    nframes = a.warmup + a.steps
-    t_prep = time.perf_counter()
     overrides = dict((kv.split("=")[0], int(kv.split("=")[1])) for kv in a.gen.split(",") if kv)
+    # GOP phases (the default): every stream is one 60-picture GOP decoded
+    # cyclically, IDRs staggered over the steps; --aligned / --pipe 2: the
+    # round-2 layout (pictures W .. W+K-1 of every stream, decode order)
+    staggered = not a.aligned and a.pipe == 1
+    nframes = GOP if staggered and not overrides else max(GOP, a.warmup + a.steps)
+    t_prep = time.perf_counter()
     streams, caps = prepare(a.config, seeds, nframes, overrides)
-    assert all(c.errors == 0 and c.npics >= nframes for c in caps), "stream preparation failed"
+    assert all(c.errors == 0 and c.npics >= min(nframes, GOP) for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run)
-    if not a.dry_run:
-        torch.cuda.set_device(local)
-    eng, sched, launch, P, resident = run.eng, run.sched, run.launch, run.P, run.resident
+    phases = gop_phases(S, min(c.npics for c in caps)) if staggered else None
+    run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run, phases=phases)
+    placement = run.placement()
+    assert all(d == local for _, d in placement), f"rank {rank}: buffers not on device {local}: {placement}"
+    eng, P, resident = run.eng, run.P, run.resident
     t_prep = time.perf_counter() - t_prep
     sync = (lambda: None) if a.dry_run else torch.cuda.synchronize
+    stride = int(os.environ.get("BENCH_TIMING_STRIDE", "4"))
 
-    nwarm = sum(1 for k0, _ in sched if k0 < a.warmup)
-    for i in range(nwarm):
-        launch(i)
-    eng.sync()
-    sync()
-    # HIP events around every 4th launch, carried by k_wgpp's own dispatch
-    # packet (hipExtLaunchKernelGGL: no marker packets between launches); a
-    # profiled dispatch still costs the stream a little, hence the stride
-    eng.set_timing(a.steps, stride=int(os.environ.get("BENCH_TIMING_STRIDE", "4")))
-    if dist:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(nwarm, len(sched)):
-        launch(i)
-    eng.sync()
-    sync()
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    dt = max_over_ranks(dist, torch, t1 - t0)
-    _, rows_us, nb = eng.timing_report()
+    dt, step_us, sampled = timed_run(run, dist, torch, sync, stride)
+    launches_timed = len(run.launches) - run.n_warm
     errors = eng.errors()
+    timed = run.timed_pictures()
+    n_i = sum(1 for s, k in timed if run.is_i[k][s])
+    refs = [golden_frames(a.config, sd, overrides) for sd in seeds]
+    res_ok, res_n = (None, 0) if a.dry_run or a.no_verify else run.check_resident(refs)
 
     frames_total = S * a.steps * world
     fps = frames_total / dt
-    # roofline: R_alg per frame = MC reference footprint + coded
-    # 4x4 blocks x 32 B + 96-B MB records; one step = one picture of each of
-    # the S streams, reconstructed by one k_prep + k_wgpp launch pair
-    r_alg = 0
-    for c in caps:
-        for k in range(a.warmup, a.warmup + a.steps):
-            p = c.pictures[k]
-            r_alg += p.alg_ref_bytes + 32 * p.n_coded + MBREC * c.w_mbs * c.h_mbs
-    launch_bytes = r_alg / (len(sched) - nwarm)
-    step_us = rows_us / max(nb, 1)
+    # roofline: R_alg of the launches the HIP events sampled
+    # (per picture: MC reference footprint + coded 4x4 blocks x 32 B + 96-B
+    # MB records) / their average k_wgpp duration
+    launch_bytes = alg_bytes(run, sampled) / max(len(sampled), 1)
     achieved = launch_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
     traffic = load_traffic()
-    frame_read_gbs = r_alg * world / dt / 1e9
+    frame_read_gbs = alg_bytes(run, range(run.n_warm, len(run.launches))) * world / dt / 1e9
 
-    ok, n_checked, n_missing = None, 0, 0
+    # the same streams with aligned GOPs, timed window P pictures only (the
+    # round-2 headline's mix), beside the configs[3] mix -- not instead
+    p_only = None
+    if staggered:
+        run.set_plan(a.warmup, a.steps, [1] * S)
+        dt_p, us_p, _ = timed_run(run, dist, torch, sync, stride)
+        tp = run.timed_pictures()
+        p_only = {"value": round(S * a.steps * world / dt_p, 2), "unit": "frames/s",
+                  "avg_launch_kernel_us": round(us_p, 2),
+                  "i_pictures_timed": sum(1 for s, k in tp if run.is_i[k][s]),
+                  "window": f"pictures 1+{a.warmup} .. of every stream (GOP phase 1, aligned)"}
+        run.set_plan(a.warmup, a.steps, phases)
+
+    ok, n_checked, n_missing, n_pre = None, 0, 0, 0
     if not a.no_verify and not a.dry_run:
-        ok, n_checked, n_missing = verify_all(eng, launch, sched, caps, seeds, a.config, overrides, run.cur_slots)
+        ok, n_checked, n_missing, n_pre = run.verify(refs)
+        ok = ok and res_ok
     n_checked_all = int(reduce_over_ranks(dist, torch, n_checked, "sum"))
     n_missing_all = int(reduce_over_ranks(dist, torch, n_missing, "sum"))
+    res_n_all = int(reduce_over_ranks(dist, torch, res_n, "sum"))
+    n_i_all = int(reduce_over_ranks(dist, torch, n_i, "sum"))
     ok_all = None if ok is None else reduce_over_ranks(dist, torch, 0.0 if ok else 1.0, "max") == 0.0
     errors_all = int(reduce_over_ranks(dist, torch, errors, "sum"))
+    if dist:
+        allp = [None] * world
+        dist.all_gather_object(allp, {"rank": rank, "device": local, "buffers": placement})
+    else:
+        allp = [{"rank": rank, "device": local, "buffers": placement}]
     rgba = rgba_leg(torch, L, eng, S, w, h) if rank == 0 and not a.dry_run and not a.no_rgba else None
 
     cpu = None
@@ -749,6 +866,9 @@ def main(argv=None):
         e2e = end_to_end(streams, nframes)
 
     if rank == 0:
+        mix = (f"IDRs staggered: stream s enters the timed window s*{run.N}/{S} pictures into its GOP "
+               f"(pre-roll + warmup untimed), 1 I per {run.N} in every {run.N}-step window"
+               if staggered else "decode order from picture 0 (aligned GOPs)")
         line = {
             "metric": "1080p Baseline frames/s per GPU; bit-exact YUV; % HBM-read roofline",
             "value": round(fps, 2),
@@ -768,12 +888,15 @@ def main(argv=None):
                        "streams_per_gpu": S, "total_streams": S * world,
                        "frames_per_stream_timed": a.steps,
                        "seeds": f"100..{100 + S * world - 1}",
+                       "gop_mix": mix,
+                       "i_pictures_timed": n_i_all,
+                       "i_share_timed": round(n_i_all / max(frames_total, 1), 5),
                        "parallelism": f"streams sharded {S}/GPU over {world} rank(s), no collective; "
                                       f"{P} consecutive picture(s) of each stream per launch"},
             "roofline": {"kernel": f"k_wgpp (one launch = {P} step(s); k_prep of the next launch runs in its tail)",
                          # what limits the kernel: the MB-row deblocking dependency chain
-                         # (SQ counters profiles/r19_sq_s8.json), not HBM;
-                         # `frac` is still quoted against the HBM peak, the metric's axis
+                         # (DESIGN.md §3), not HBM; `frac` is still quoted against the HBM
+                         # peak, the metric's axis
                          "bound": "latency",
                          "frac_axis": "hbm",
                          "limiter": "latency: the MB-row deblocking dependency chain (DESIGN.md §3), not HBM",
@@ -782,29 +905,37 @@ def main(argv=None):
                          "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
                          "alg_bytes_per_launch": int(launch_bytes),
                          "avg_launch_kernel_us": round(step_us, 2),
+                         "timed_launches_sampled": len(sampled),
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
             "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S * P,
                                    "steps_per_launch": P,
-                                   "timed_launches": nb,
+                                   "timed_launches": launches_timed,
                                    "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}},
+            "p_only": p_only,
             "wall_read_GBs": round(frame_read_gbs, 2),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "rgba_output": rgba,
             "config_legs": legs,
             "bitexact_check": {"ok": ok_all, "frames_checked": n_checked_all,
-                               "frames_expected": S * world * nframes, "frames_without_fixture": n_missing_all,
-                               "method": "untimed re-decode of all warmup+timed steps, every picture of every "
-                                         "stream of every rank vs reference-decoder MD5s",
+                               "frames_expected": S * world * (a.warmup + a.steps),
+                               "frames_without_fixture": n_missing_all,
+                               "timed_run_resident_frames_checked": res_n_all,
+                               "preroll_frames_checked": n_pre,
+                               "method": "(1) after the timed loop, every frame slot's last picture -- the timed "
+                                         "launches' own output -- vs reference-decoder MD5s; (2) untimed re-run "
+                                         "of the whole plan, every warmup + timed picture of every stream of "
+                                         "every rank vs the MD5s right after its launch",
                                "residual_range_errors": errors_all},
+            "device_placement": allp,
             "prep_seconds": round(t_prep, 1),
             **({"one_device_rehearsal": f"{world} ranks shared device 0 (BENCH_ONE_DEVICE=1): not a multi-GPU rate"}
                if os.environ.get("BENCH_ONE_DEVICE") == "1" else {}),
             "hbm_resident_input_MB": round(resident / 1e6, 1),
         }
         if a.dry_run:
-            line["dry_run"] = {"launches": eng.launches, "seeds": seeds}
+            line["dry_run"] = {"launches": eng.launches, "seeds": seeds, "preroll_launches": run.n_pre}
         print(json.dumps(line), flush=True)
     run.free()
     if dist:

@@ -197,6 +197,16 @@ def mi() -> C.CDLL:
     L.h264mi_device_free.restype = i32
     L.h264mi_copy_h2d.argtypes = [vp, vp, sz]
     L.h264mi_copy_h2d.restype = i32
+    L.h264mi_engine_device.argtypes = [vp]
+    L.h264mi_engine_device.restype = i32
+    L.h264mi_engine_alloc.argtypes = [vp, sz]
+    L.h264mi_engine_alloc.restype = vp
+    L.h264mi_engine_free.argtypes = [vp, vp]
+    L.h264mi_engine_free.restype = i32
+    L.h264mi_engine_copy_h2d.argtypes = [vp, vp, vp, sz]
+    L.h264mi_engine_copy_h2d.restype = i32
+    L.h264mi_pointer_device.argtypes = [vp]
+    L.h264mi_pointer_device.restype = i32
     _mi = L
     return L
 

@@ -576,6 +576,46 @@ extern "C" int h264mi_copy_h2d(void *dst, const void *src, size_t bytes)
     return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 
+// engine-scoped device memory: on the engine's GPU whatever the calling
+// thread's current device is (one process per GPU: rank r's record batches
+// must live on GPU r, next to its frame slots and launches)
+extern "C" int h264mi_engine_device(const h264mi_engine *e) { return e ? e->dev : -1; }
+
+extern "C" void *h264mi_engine_alloc(h264mi_engine *e, size_t bytes)
+{
+    if (!e || !bytes || hipSetDevice(e->dev) != hipSuccess) return NULL;
+    void *p = NULL;
+    if (hipMalloc(&p, bytes) != hipSuccess) return NULL;
+    return p;
+}
+
+extern "C" int h264mi_engine_free(h264mi_engine *e, void *p)
+{
+    if (!e || hipSetDevice(e->dev) != hipSuccess) return -1;
+    return hipFree(p) == hipSuccess ? 0 : -1;
+}
+
+extern "C" int h264mi_engine_copy_h2d(h264mi_engine *e, void *dst, const void *src, size_t bytes)
+{
+    if (!e || h264mi_pointer_device(dst) != e->dev) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, e->st));
+    HIPCHECK(hipStreamSynchronize(e->st));
+    return 0;
+}
+
+extern "C" int h264mi_pointer_device(const void *p)
+{
+    if (!p) return -1;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    if (at.type != hipMemoryTypeDevice) return -1;
+    return at.device;
+}
+
 // -------- H264Backend adapter for the single-stream host decoder ----------
 #include "../host/decoder.h"
 #include <mutex>

@@ -587,14 +587,14 @@ __device__ __forceinline__ void prep_mb(const PrepArgs &a, int gidx, int lane, M
         if (lane + 128 < ncw) Mw.coef[lane + 128] = cq2;
         if (lane + 192 < ncw) Mw.coef[lane + 192] = cq3;
         wave_sync();
-        mb_residual(r, (const int16_t *)Mw.coef, a.res + (size_t)gmb * 384, Mw.dc, lane, &e, T.ls,
+        mb_residual(r, (const int16_t *)Mw.coef, a.res + (size_t)gidx * 384, Mw.dc, lane, &e, T.ls,
                     res_mask(rtype, rcbits));
     }
     const int any_e = __builtin_amdgcn_ballot_w64(e != 0) != 0;
     if (lane < 16) {
         uint32_t w = ((const uint32_t *)s_db)[lane];
         if (lane == 15) w = (w & 0x00FFFFFFu) | (any_e ? 0x01000000u : 0u);
-        ((uint32_t *)(a.dbrec + (size_t)gmb * 64))[lane] = w;
+        ((uint32_t *)(a.dbrec + (size_t)gidx * 64))[lane] = w;     // batch position, not rec_base
     }
     wave_sync();
 }
@@ -1503,9 +1503,13 @@ struct McLoad {
 
 __device__ __forceinline__ uint32_t rec_dw(uint32_t v0, int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v0, i); }
 
-__device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, int mb, uint32_t v0, int lane, McLoad &L)
+__device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, int p, int mb, uint32_t v0, int lane,
+                                         McLoad &L)
 {
-    const int gmb = pd.rec_base + mb;
+    // k_prep outputs are indexed by the MB's position in the batch (picture p
+    // of the launch), not by PicDesc.rec_base: records may sit anywhere in
+    // the record pool
+    const int gmb = p * (a.w * a.h) + mb;
     const uint32_t d0 = rec_dw(v0, 0), cbits = rec_dw(v0, 2), refs = rec_dw(v0, 6);
     const int rtype = d0 & 255;
     const bool has_res = rtype != MBT_IPCM && cbits != 0;
@@ -1771,7 +1775,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     uint32_t v0 = c0 < a.w ? recrow[(size_t)c0 * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
     if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
-    if (c0 < a.w) mc_issue(a, pd, r * a.w + c0, v0, lane, ld);
+    if (c0 < a.w) mc_issue(a, pd, p, r * a.w + c0, v0, lane, ld);
     for (int c = c0; c < a.w; c += NMC) {
         const int slot = c & (RK - 1);
         const bool more = c + NMC < a.w;
@@ -1804,7 +1808,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
         v0 = nv0;
         if (more && D.n) dep_wait(a, p, v0, lane, D);
-        if (more) mc_issue(a, pd, r * a.w + c + NMC, v0, lane, ld);
+        if (more) mc_issue(a, pd, p, r * a.w + c + NMC, v0, lane, ld);
     }
 }
 

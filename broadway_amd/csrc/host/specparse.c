@@ -68,9 +68,11 @@ struct SpecPool {
 static void run_job(SpecPool *sp, SpecJob *j)
 {
     j->ok = 0;
-    uint32_t init, size;
+    uint32_t init, size, rb;
     int emul;
-    if (nal_scan(j->raw, j->read_bytes, &init, &size, &j->read_bytes, &emul)) return;
+    /* j->read_bytes is the caller's (spec_take matches jobs by it under the
+     * lock): scan into a local, never write the shared field here */
+    if (nal_scan(j->raw, j->read_bytes, &init, &size, &rb, &emul) || rb != j->read_bytes) return;
     if (j->rbsp_cap < size + 8) {
         free(j->rbsp);
         j->rbsp_cap = size + 64 + size / 2;

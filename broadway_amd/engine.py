@@ -134,6 +134,29 @@ class Engine:
             raise RuntimeError("h264mi_engine_read_rgba failed")
         return out
 
+    @property
+    def device(self) -> int:
+        return int(self._L.h264mi_engine_device(self._h))
+
+    def alloc(self, nbytes: int) -> int:
+        """Device memory on the engine's GPU (whatever the caller's current
+        HIP device is)."""
+        p = self._L.h264mi_engine_alloc(self._h, int(nbytes))
+        if not p:
+            raise RuntimeError(f"h264mi_engine_alloc({nbytes}) failed on device {self.device}")
+        return int(p)
+
+    def free(self, p: int) -> None:
+        self._L.h264mi_engine_free(self._h, p)
+
+    def upload(self, dst: int, src, nbytes: int) -> None:
+        """H2D into memory of this engine's GPU (refused for another GPU's)."""
+        if self._L.h264mi_engine_copy_h2d(self._h, dst, src, int(nbytes)) != 0:
+            raise RuntimeError("h264mi_engine_copy_h2d failed (destination not on the engine's device?)")
+
+    def pointer_device(self, p: int) -> int:
+        return int(self._L.h264mi_pointer_device(p))
+
     def frame_ptr(self, stream: int, slot: int) -> int:
         """Device address of a frame slot (I420, frame_bytes)."""
         return int(self._L.h264mi_engine_frame_ptr(self._h, stream, slot))

@@ -244,10 +244,21 @@ int  h264mi_capture_picture(const h264mi_capture *c, int i, const void **rec, co
 int  h264mi_capture_stats(const h264mi_capture *c, int i, uint32_t *n_inter, uint32_t *n_intra, uint32_t *n_coded);
 void h264mi_capture_free(h264mi_capture *c);
 
-/* Device memory helpers for the device-resident path (HIP device pointers) */
+/* Device memory helpers for the device-resident path (HIP device pointers).
+ * h264mi_device_alloc allocates on the calling thread's CURRENT HIP device;
+ * a multi-GPU caller uses the engine-scoped forms below instead. */
 void *h264mi_device_alloc(size_t bytes);
 int   h264mi_device_free(void *p);
 int   h264mi_copy_h2d(void *dst, const void *src, size_t bytes);
+/* Engine-scoped: memory on the engine's own GPU whatever the caller's current
+ * device (one process per GPU, TestBenchMultipleInstance.c:134-305 style
+ * independent instances); copy_h2d refuses a destination on another GPU. */
+int   h264mi_engine_device(const h264mi_engine *e);
+void *h264mi_engine_alloc(h264mi_engine *e, size_t bytes);
+int   h264mi_engine_free(h264mi_engine *e, void *p);
+int   h264mi_engine_copy_h2d(h264mi_engine *e, void *dst, const void *src, size_t bytes);
+/* HIP device ordinal a device pointer lives on, -1 for host / unknown memory */
+int   h264mi_pointer_device(const void *p);
 
 #ifdef __cplusplus
 }

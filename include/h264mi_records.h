@@ -91,7 +91,9 @@ _Static_assert(sizeof(MbRec) == 96, "MbRec must stay 96 bytes");
 
 /* Per-picture descriptor, one per picture in a launch batch */
 typedef struct PicDesc {
-    uint32_t rec_base;      /* first MbRec index of this picture in the batch */
+    uint32_t rec_base;      /* first MbRec index of this picture, relative to the launch's record
+                               pointer (any offset: the pictures of a launch need not be
+                               contiguous; k_prep outputs are indexed by batch position) */
     uint32_t frame_base;    /* index of this stream's slot 0 in the frame pool */
     uint32_t cur_slot;      /* slot being reconstructed */
     uint32_t flags;         /* bit0: picture has intra MBs, bit1: deblocking on */

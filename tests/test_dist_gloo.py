@@ -93,9 +93,20 @@ def test_bench_dry_run_two_ranks():
     line = json.loads(res[0].strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["steps"] == 3 and line["warmup"] == 1
     assert line["config"]["total_streams"] == 4 and line["config"]["seeds"] == "100..103"
-    assert line["dry_run"]["launches"] == 4 and line["dry_run"]["seeds"] == [100, 101]
+    # GOP phases 0 and 30 of the 60-picture streams: 30 pre-roll launches +
+    # 1 warmup + 3 timed, then the aligned P-only leg (1 pre-roll + 4)
+    assert line["dry_run"]["preroll_launches"] == 30 and line["dry_run"]["seeds"] == [100, 101]
+    assert line["dry_run"]["launches"] == 30 + 4 + 1 + 4
     assert line["value"] > 0 and line["scaling"] == "weak"
     assert line["bitexact_check"]["frames_expected"] == 2 * 2 * 4
+    assert line["p_only"]["i_pictures_timed"] == 0
+    # every rank's record, coefficient and descriptor buffers on its own GPU
+    # (rank r -> LOCAL_RANK r), allocated through its engine
+    place = {p["rank"]: p for p in line["device_placement"]}
+    assert sorted(place) == [0, 1]
+    for r in (0, 1):
+        assert place[r]["device"] == r
+        assert [d for _, d in place[r]["buffers"]] == [r, r, r]
 
 
 def test_bench_gpus_mismatch_refused(monkeypatch):

@@ -152,23 +152,35 @@ def test_engine_bench_streams_vs_reference(rpw, monkeypatch):
     assert eng.errors() == 0
 
 
-@pytest.mark.parametrize("rank,pipe", [(r, 2) for r in range(8)] + [(0, 1)])
+@pytest.mark.parametrize("rank,pipe", [(r, 2) for r in range(8)] + [(0, 1), (1, 1)])
 def test_configs3_shard_vs_reference(rank, pipe):
     """configs[3]: 64 streams, 8 per GPU.  Rank r's shard (seeds 100+8r ..
     100+8r+7, bench.shard_seeds) through bench.py's own device-resident path
-    (bench.DeviceRun: records in HBM, `pipe` pictures of every stream per
-    launch -- 1 is the bench default, 2 the frame-pipelined batches -- with
-    the next launch's k_prep in its tail) and its verification pass: all 60
-    pictures of all 8 streams vs the reference decoder's MD5s."""
+    (bench.DeviceRun: records in HBM on the rank's engine, the next launch's
+    k_prep in each launch's tail) and its verification pass.  pipe 1: the
+    bench default -- GOP phases staggered over the streams, each 60-picture
+    stream decoded cyclically after an untimed pre-roll; pipe 2: two
+    consecutive pictures of every stream per launch (frame-pipelined
+    batches).  Every picture of every launch vs the reference MD5s, and after
+    the run every frame slot's last picture."""
     import bench
     seeds = bench.shard_seeds(rank, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
-    run = bench.DeviceRun(_lib.mi(), caps, 4, n - 4, pipe)
+    phases = bench.gop_phases(8, n) if pipe == 1 else None
+    run = bench.DeviceRun(_lib.mi(), caps, 4, n - 4, pipe, phases=phases)
     try:
-        assert run.P == pipe and len(run.sched) == n // pipe
-        ok, checked, missing = bench.verify_all(run.eng, run.launch, run.sched, caps, seeds, 3, {}, run.cur_slots)
+        assert run.P == pipe and all(d == 0 for _, d in run.placement())
+        if pipe == 1:
+            assert run.n_pre == max(phases) and len(run.launches) == run.n_pre + n
+            timed = run.timed_pictures()
+            assert sum(run.is_i[k][s] for s, k in timed) == 8 - 1     # stream 0's IDR falls in the warmup
+        else:
+            assert len(run.launches) == n // pipe
+        refs = [bench.golden_frames(3, sd, {}) for sd in seeds]
+        ok, checked, missing, _ = run.verify(refs)
         assert (ok, checked, missing) == (True, 8 * n, 0)
+        assert run.check_resident(refs)[0]
         assert run.eng.errors() == 0
     finally:
         run.free()
@@ -191,12 +203,12 @@ def test_engine_pipelined_steps_vs_oracle(wh):
     run = bench.DeviceRun(_lib.mi(), caps, 0, n, 2)
     try:
         assert run.P == 2
-        for i, (k0, P) in enumerate(run.sched):
+        for i, launch in enumerate(run.launches):
             run.launch(i)
             run.eng.sync()
-            for k in range(k0, k0 + P):
-                for s in range(len(caps)):
-                    got = run.eng.read(s, int(run.cur_slots[k][s])).tobytes()
+            for step in launch:
+                for s, k in enumerate(step):
+                    got = run.eng.read(s, int(run.slot_of[k][s])).tobytes()
                     assert got == refs[s][k], f"stream {s} picture {k}"
         assert run.eng.errors() == 0
     finally:

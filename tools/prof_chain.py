@@ -24,19 +24,23 @@ import ctypes as C  # noqa: E402
 
 import bench  # noqa: E402
 from broadway_amd import _lib  # noqa: E402
-from broadway_amd.engine import Engine  # noqa: E402
 
 L = _lib.mi()
 S = int(os.environ.get("PROF_S", "8"))
-streams, caps = bench.prepare(3, [100 + i for i in range(S)], 6)
+# PROF_CONFIG=3: the bench streams (1080p I+P; picture PROF_PIC, a P picture
+# by default); PROF_CONFIG=1: 720p I-only (config 2 of SURVEY §8d)
+CFG = int(os.environ.get("PROF_CONFIG", "3"))
+PIC = int(os.environ.get("PROF_PIC", "5"))
+seeds = [(100 if CFG == 3 else 1) + i for i in range(S)]
+streams, caps = bench.prepare(CFG, seeds, PIC + 1)
 w, h = caps[0].w_mbs, caps[0].h_mbs
-d_recs, d_coef, d_pics, step_rec_bytes, nslots, _ = bench.upload(L, caps, 6)
-eng = Engine(w, h, S, nslots)
-print("kernel", eng.kernel_name())
+run = bench.DeviceRun(L, caps, 0, PIC + 1, 1)
+eng = run.eng
 L.h264mi_engine_profile(eng._h, 1, None, 0)
-for k in range(6):
-    eng.decode_device(S, d_recs + k * step_rec_bytes, d_coef, d_pics + k * S * 32)
+for i in range(len(run.launches)):
+    run.launch(i)
     eng.sync()
+print("kernel", eng.kernel_name(), "config", CFG, "picture", PIC, "intra" if run.is_i[PIC][0] else "inter")
 n = S * h * 16 + S * w * h * 4
 buf = (C.c_uint64 * n)()
 L.h264mi_engine_profile(eng._h, 1, buf, n)
