@@ -506,7 +506,7 @@ extern "C" int h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long
                            hipMemcpyDeviceToHost));
     }
     if (enable && !e->d_prof) {
-        e->prof_cap = (size_t)e->pipe_cap * e->h * 16 + (size_t)e->pipe_cap * e->nmbs * 4;
+        e->prof_cap = (size_t)e->pipe_cap * e->h * 16 + (size_t)e->pipe_cap * e->nmbs * PROF_MB;
         HIPCHECK(hipMalloc(&e->d_prof, sizeof(unsigned long long) * e->prof_cap));
         HIPCHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * e->prof_cap));
     } else if (!enable && e->d_prof) {
@@ -637,7 +637,6 @@ extern "C" int h264mi_pointer_device(const void *p)
 #define SHARE_MAX 32
 #define SHARE_SLOTS 17                    // MaxDpbFrames (16) + the current picture
 #define SHARE_WAIT_US 1000                // default batch wait (H264MI_SHARE_WAIT_US)
-#define SHARE_FLAG_RING 256
 
 struct HipBackendCtx;
 struct SharedEng {
@@ -654,9 +653,9 @@ struct SharedEng {
     const int16_t *coefs[SHARE_MAX];
     uint32_t nc[SHARE_MAX];
     HipBackendCtx *who[SHARE_MAX];
+    bool force[SHARE_MAX];                // test hook: start this picture with a device flag set
     unsigned long long collecting, launched;   // batch ids: collecting > launched while np > 0
     int rc;                               // result of the last launch
-    unsigned *h_flags;                    // pinned: per batch (ring of SHARE_FLAG_RING) the pictures' device flags
 };
 static std::mutex g_share_mu;
 #define SHARE_SIZES 4                     // shared engines per device, one per picture size
@@ -674,9 +673,16 @@ struct HipBackendCtx {
     int lane;           // stream index in e
     hipEvent_t ev_last; // shared: after this instance's latest work on the engine stream
     uint8_t *d_rgba;    // shared: RGBA staging
-    unsigned long long fbatch;   // shared: batch of this instance's latest picture, and its index there
-    int fidx;
     uint8_t **pref;     // per slot: host buffer a D2H copy of the slot's current picture was queued into
+    // pinned, per frame slot: the device flags (ReconArgs::err: residual range,
+    // expired bounded waits) of the picture reconstructed into the slot, copied
+    // behind its launch -- a read reports the flags of the picture it reads,
+    // whatever order pictures are output in and whatever else was read before
+    unsigned *h_slot_err;
+    // test hook (H264MI_DEBUG_FLAG_PICTURE=k): the k-th reconstruction of this
+    // instance (1-based) starts with a forced device flag, to check that the
+    // flag reaches exactly that picture's output whatever the output order
+    unsigned ndecodes, force_flag_at;
     int nslots;
     unsigned enq, synced;   // work items queued on the engine's stream / of those, waited for by hb_sync
 };
@@ -707,19 +713,18 @@ static void share_launch(SharedEng *sh)
 {
     if (sh->np == 0) return;
     h264mi_engine *e = sh->e;
+    for (int i = 0; i < sh->np; i++)
+        if (sh->force[i]) (void)hipMemsetAsync(e->d_err + i, 0x01, sizeof(unsigned), e->st);
     sh->rc = h264mi_engine_decode(e, sh->np, sh->stream, sh->slot, sh->recs, sh->coefs, sh->nc);
-    // this batch's device flags (ReconArgs::err, one word per picture) into
-    // its ring entry, then cleared for the next batch
-    unsigned *hf = sh->h_flags + (size_t)(sh->collecting % SHARE_FLAG_RING) * SHARE_MAX;
-    if (hipMemcpyAsync(hf, e->d_err, sizeof(unsigned) * sh->np, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
-        hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * sh->np, e->st) != hipSuccess)
-        sh->rc = -1;
-    for (int i = 0; i < sh->np; i++) {
-        HipBackendCtx *c = sh->who[i];
-        c->fbatch = sh->collecting;
-        c->fidx = i;
-        (void)hipEventRecord(c->ev_last, e->st);
-    }
+    // each picture's device flags (ReconArgs::err, one word per batch
+    // picture) into its instance's word for the slot it was reconstructed
+    // into, then cleared for the next batch
+    for (int i = 0; i < sh->np && sh->rc == 0; i++)
+        if (hipMemcpyAsync(sh->who[i]->h_slot_err + sh->slot[i], e->d_err + i, sizeof(unsigned),
+                           hipMemcpyDeviceToHost, e->st) != hipSuccess)
+            sh->rc = -1;
+    if (hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * sh->np, e->st) != hipSuccess) sh->rc = -1;
+    for (int i = 0; i < sh->np; i++) (void)hipEventRecord(sh->who[i]->ev_last, e->st);
     g_share_batches[sh->device] += 1;
     g_share_pictures[sh->device] += (unsigned long long)sh->np;
     sh->np = 0;
@@ -749,7 +754,6 @@ static void share_detach(HipBackendCtx *c)
         for (int k = 0; k < SHARE_SIZES; k++)
             if (g_share[sh->device][k] == sh) g_share[sh->device][k] = NULL;
         h264mi_engine_destroy(sh->e);
-        (void)hipHostFree(sh->h_flags);
         delete sh;
     }
     c->sh = NULL; c->e = NULL;
@@ -773,12 +777,6 @@ static int share_attach(HipBackendCtx *c, int w_mbs, int h_mbs, int nslots)
         h264mi_engine *e = h264mi_engine_create(c->device, w_mbs, h_mbs, lanes, SHARE_SLOTS);
         if (!e) return -1;
         sh = new SharedEng();
-        if (hipHostMalloc(&sh->h_flags, sizeof(unsigned) * SHARE_FLAG_RING * SHARE_MAX, hipHostMallocDefault) != hipSuccess) {
-            h264mi_engine_destroy(e);
-            delete sh;
-            return -1;
-        }
-        memset(sh->h_flags, 0, sizeof(unsigned) * SHARE_FLAG_RING * SHARE_MAX);
         sh->device = c->device; sh->w = w_mbs; sh->h = h_mbs; sh->lanes = lanes; sh->e = e;
         sh->used = 0; sh->active = 0; sh->np = 0; sh->collecting = 1; sh->launched = 0; sh->rc = 0;
         g_share[c->device][free_k] = sh;
@@ -794,7 +792,6 @@ static int share_attach(HipBackendCtx *c, int w_mbs, int h_mbs, int nslots)
     sh->used |= 1u << lane;
     sh->active++;
     c->sh = sh; c->lane = lane; c->e = sh->e;
-    c->fbatch = 0; c->fidx = 0;
     return 0;
 }
 
@@ -805,8 +802,16 @@ static int hb_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
     else if (c->e) h264mi_engine_destroy(c->e);
     c->e = NULL;
     free(c->pref);
+    (void)hipHostFree(c->h_slot_err);
+    c->h_slot_err = NULL;
     c->pref = (uint8_t **)calloc((size_t)nslots, sizeof(uint8_t *));
     c->nslots = c->pref ? nslots : 0;
+    if (hipSetDevice(c->device) != hipSuccess ||
+        hipHostMalloc(&c->h_slot_err, sizeof(unsigned) * (nslots > 0 ? nslots : 1), hipHostMallocDefault) != hipSuccess) {
+        c->h_slot_err = NULL;
+        return -1;
+    }
+    memset(c->h_slot_err, 0, sizeof(unsigned) * (nslots > 0 ? nslots : 1));
     if (share_attach(c, w_mbs, h_mbs, nslots) != 0) {
         c->lane = 0;
         c->e = h264mi_engine_create(c->device, w_mbs, h_mbs, 1, nslots);
@@ -819,12 +824,20 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
     HipBackendCtx *c = (HipBackendCtx *)vctx;
     if (cur_slot >= 0 && cur_slot < c->nslots) c->pref[cur_slot] = NULL;
     c->enq++;
+    const bool force = ++c->ndecodes == c->force_flag_at;
     if (!c->sh) {
+        if (force) HIPCHECK(hipMemsetAsync(c->e->d_err, 0x01, sizeof(unsigned), c->e->st));
         int stream = 0;
         const void *recs[1] = {pb->rec};
         const int16_t *coefs[1] = {pb->coef};
         uint32_t nc[1] = {pb->ncoef};
-        return h264mi_engine_decode(c->e, 1, &stream, &cur_slot, recs, coefs, nc);
+        h264mi_engine *e = c->e;
+        if (h264mi_engine_decode(e, 1, &stream, &cur_slot, recs, coefs, nc)) return -1;
+        // the picture's device flags into the slot's word, behind its launch
+        if (cur_slot < 0 || cur_slot >= c->nslots) return -1;
+        HIPCHECK(hipMemcpyAsync(c->h_slot_err + cur_slot, e->d_err, sizeof(unsigned), hipMemcpyDeviceToHost, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned), e->st));
+        return 0;
     }
     SharedEng *sh = c->sh;
     std::unique_lock<std::mutex> l(sh->mu);
@@ -832,6 +845,7 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
     sh->stream[i] = c->lane; sh->slot[i] = cur_slot;
     sh->recs[i] = pb->rec; sh->coefs[i] = pb->coef; sh->nc[i] = pb->ncoef;
     sh->who[i] = c;
+    sh->force[i] = force;
     const unsigned long long mine = sh->collecting;
     if (sh->np >= sh->active) {
         share_launch(sh);
@@ -856,25 +870,18 @@ static int hb_prefetch(void *vctx, int slot, uint8_t *dst)
     return 0;
 }
 
-// the per-picture device error flags (ReconArgs::err: residual range, expired
-// bounded waits) gathered by the read's sync reach the caller as return 1
-static int hb_flagged(h264mi_engine *e, bool wait = true)
+// the device flags of the picture in `slot` (ReconArgs::err: residual range,
+// expired bounded waits), copied behind its launch into the slot's word,
+// reach the caller as return 1; wait: sync first (the copy is stream-ordered)
+static int slot_flagged(HipBackendCtx *c, int slot, bool wait = true)
 {
-    if (wait && h264mi_engine_sync(e)) return -1;
-    const uint32_t n = h264mi_engine_errors(e);
-    if (n) fprintf(stderr, "h264mi: device reported %u flagged picture(s)\n", n);
-    return n ? 1 : 0;
-}
-
-// shared engine: wait for this instance's own work only, then its latest
-// picture's device flags from its batch's ring entry
-static int share_flagged(HipBackendCtx *c)
-{
-    HIPCHECK(hipEventSynchronize(c->ev_last));
-    if (!c->fbatch) return 0;
-    const unsigned f = c->sh->h_flags[(size_t)(c->fbatch % SHARE_FLAG_RING) * SHARE_MAX + c->fidx];
-    c->fbatch = 0;
-    if (f) fprintf(stderr, "h264mi: device flagged a picture (flags %#x)\n", f);
+    if (wait) {
+        if (c->sh) HIPCHECK(hipEventSynchronize(c->ev_last));
+        else if (h264mi_engine_sync(c->e)) return -1;
+    }
+    if (slot < 0 || slot >= c->nslots) return -1;
+    const unsigned f = c->h_slot_err[slot];
+    if (f) fprintf(stderr, "h264mi: device flagged the picture in slot %d (flags %#x)\n", slot, f);
     return f ? 1 : 0;
 }
 
@@ -902,12 +909,12 @@ static int hb_read(void *vctx, int slot, uint8_t *dst)
                                     hipMemcpyDeviceToHost, c->e->st));
             HIPCHECK(hipEventRecord(c->ev_last, c->e->st));
         }
-        return share_flagged(c);
+        return slot_flagged(c, slot);
     }
     // copied there already (hb_prefetch): only wait for it
-    if (slot >= 0 && slot < c->nslots && c->pref[slot] == dst) return hb_flagged(c->e, c->synced != c->enq);
+    if (slot >= 0 && slot < c->nslots && c->pref[slot] == dst) return slot_flagged(c, slot, c->synced != c->enq);
     if (h264mi_engine_read(c->e, 0, slot, dst)) return -1;
-    return hb_flagged(c->e);
+    return slot_flagged(c, slot, false);
 }
 
 static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
@@ -926,10 +933,10 @@ static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
             HIPCHECK(hipMemcpyAsync(dst, c->d_rgba, bytes, hipMemcpyDeviceToHost, e->st));
             HIPCHECK(hipEventRecord(c->ev_last, e->st));
         }
-        return share_flagged(c);
+        return slot_flagged(c, slot);
     }
     if (h264mi_engine_read_rgba(c->e, 0, slot, dst)) return -1;
-    return hb_flagged(c->e);
+    return slot_flagged(c, slot, false);
 }
 
 static void *hb_host_alloc(void *vctx, size_t bytes)
@@ -963,6 +970,7 @@ static void hb_destroy(void *vctx)
     if (c->sh) share_detach(c);
     else if (c->e) h264mi_engine_destroy(c->e);
     free(c->pref);
+    (void)hipHostFree(c->h_slot_err);
     free(c);
 }
 
@@ -995,6 +1003,8 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     }
     HipBackendCtx *c = (HipBackendCtx *)calloc(1, sizeof(HipBackendCtx));
     c->device = device;
+    const char *ff = getenv("H264MI_DEBUG_FLAG_PICTURE");
+    c->force_flag_at = ff && atoi(ff) > 0 ? (unsigned)atoi(ff) : 0;
     be.ctx = c;
     be.configure = hb_configure;
     be.decode = hb_decode;

@@ -22,6 +22,8 @@
 #include "../../../include/h264mi_records.h"
 
 #define WAVE 64
+// profiling build: u64 stamps per MB (row waves [0..2], MC [3], intra [4..5])
+#define PROF_MB 8
 
 struct ReconArgs {
     uint8_t *frames;          // frame pool (I420 per slot)
@@ -363,87 +365,15 @@ __device__ __forceinline__ void luma_row4_reg(const uint32_t (*wr)[3], int xo, i
 }
 
 // ---------------------------------------------------------------------------
-// intra prediction (intra_prediction.c) into an LDS tile with a 1-sample halo
+// intra prediction tiles (intra_prediction.c, per MC wave in LDS): the MB's
+// samples with a one-sample halo, every 4-sample group dword-aligned.  Luma
+// sample (x, y) at ty[(y + 1) * TY_STRIDE + TX0 + x]; the left neighbour
+// column at TX0 - 1; the row above in row 0 (top-left at TX0 - 1, top-right
+// at TX0 + 16..19).  Chroma alike with TC_STRIDE (no top-right).
 // ---------------------------------------------------------------------------
-// luma tile: 17 rows x 24 cols; (row 0) = y=-1, (col 0) = x=-1; cols 17..20 = top-right
 #define TY_STRIDE 24
 #define TC_STRIDE 12
-
-// LDS offset (relative to the block's first sample) of virtual sample Sx[k]
-__device__ __forceinline__ int sx_off(int k, int S, bool avTR)
-{
-    if (k == 4) return -S - 1;                       // p[-1,-1]
-    if (k > 4) {                                     // p[k-5,-1], top-right replicated
-        int t = k - 5;
-        if (t > 3 && !avTR) t = 3;
-        return -S + t;
-    }
-    return (3 - k) * S - 1;                          // p[-1,3-k]
-}
-
-__device__ __forceinline__ int i4_pred(const uint8_t *T /* tile at block (0,0) i.e. &tile[(by+1)*S + bx+1] */,
-                                       int S, int mode, int x, int y, bool avT, bool avL, bool avTR)
-{
-    // S-array of the 4x4 block: Sx[4]=p[-1,-1], Sx[5+k]=p[k,-1], Sx[3-k]=p[-1,k]
-#define PT(k) ((int)T[-S + (((k) > 3 && !avTR) ? 3 : (k))])
-#define PL(k) ((int)T[(k)*S - 1])
-#define PTL ((int)T[-S - 1])
-    int v;
-    switch (mode) {
-    case 0: v = PT(x); break;
-    case 1: v = PL(y); break;
-    case 2: {
-        const int st = PT(0) + PT(1) + PT(2) + PT(3), sl = PL(0) + PL(1) + PL(2) + PL(3);
-        if (avT && avL) v = (st + sl + 4) >> 3;
-        else if (avL) v = (sl + 2) >> 2;
-        else if (avT) v = (st + 2) >> 2;
-        else v = 128;
-        break;
-    }
-    case 3:
-        if (x == 3 && y == 3) v = (PT(6) + 3 * PT(7) + 2) >> 2;
-        else v = (PT(x + y) + 2 * PT(x + y + 1) + PT(x + y + 2) + 2) >> 2;
-        break;
-    default: {
-        // modes 4..8 read a mix of left / top / corner samples; the virtual
-        // array Sx[k]: Sx[4] = p[-1,-1], Sx[5+k] = p[k,-1], Sx[3-k] = p[-1,k]
-        // (resolved to one LDS offset per access -- no private array)
-#define SX(k) ((int)T[sx_off((k), S, avTR)])
-        if (mode == 4) {
-            const int d = x - y;
-            v = (SX(3 + d) + 2 * SX(4 + d) + SX(5 + d) + 2) >> 2;
-        } else if (mode == 5) {
-            const int z = 2 * x - y, i = x - (y >> 1);
-            if (z >= 0 && !(z & 1)) v = (SX(4 + i) + SX(5 + i) + 1) >> 1;
-            else if (z > 0) v = (SX(3 + i) + 2 * SX(4 + i) + SX(5 + i) + 2) >> 2;
-            else if (z == -1) v = (SX(3) + 2 * SX(4) + SX(5) + 2) >> 2;
-            else v = (SX(4 - y) + 2 * SX(5 - y) + SX(6 - y) + 2) >> 2;
-        } else if (mode == 6) {
-            const int z = 2 * y - x, i = y - (x >> 1);
-            if (z >= 0 && !(z & 1)) v = (SX(4 - i) + SX(3 - i) + 1) >> 1;
-            else if (z > 0) v = (SX(5 - i) + 2 * SX(4 - i) + SX(3 - i) + 2) >> 2;
-            else if (z == -1) v = (SX(3) + 2 * SX(4) + SX(5) + 2) >> 2;
-            else v = (SX(4 + x) + 2 * SX(3 + x) + SX(2 + x) + 2) >> 2;
-        } else if (mode == 7) {
-            const int i = x + (y >> 1);
-            if (!(y & 1)) v = (SX(5 + i) + SX(6 + i) + 1) >> 1;
-            else v = (SX(5 + i) + 2 * SX(6 + i) + SX(7 + i) + 2) >> 2;
-        } else {
-            const int z = x + 2 * y, i = y + (x >> 1);
-            if (z > 5) v = SX(0);
-            else if (z == 5) v = (SX(1) + 3 * SX(0) + 2) >> 2;
-            else if (!(z & 1)) v = (SX(3 - i) + SX(2 - i) + 1) >> 1;
-            else v = (SX(3 - i) + 2 * SX(2 - i) + SX(1 - i) + 2) >> 2;
-        }
-#undef SX
-        break;
-    }
-    }
-#undef PT
-#undef PL
-#undef PTL
-    return v;
-}
+#define TX0 4
 
 __device__ __forceinline__ int bs_of(const MbRec &p, int bp, const MbRec &q, int bq, bool mb_edge)
 {
@@ -525,7 +455,6 @@ struct McScratch {
         };
         struct {                         // intra (k_wg MC waves): prediction tiles with halo
             uint8_t ty[17 * TY_STRIDE], tu[9 * TC_STRIDE], tv[9 * TC_STRIDE];
-            uint8_t sx[32];
             uint8_t junk[256];
         };
     };
@@ -614,18 +543,21 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs a)
 // intra reconstruction of one MB inside a wave-private tile whose 1-sample
 // halo (top row incl. top-left/top-right, left column) is already filled.
 // ---------------------------------------------------------------------------
-// I4x4 sub-wavefront: step -> (block of slot 0, block of slot 1), one nibble
-// per step; slot 1 uses 15 for "none" (block 15 is always slot 0)
+// I4x4 sub-wavefront: 16 blocks in 10 steps, two per step where the
+// dependencies allow (left, top, top-right, top-left blocks done first):
 //   {0,-} {1,-} {4,2} {5,3} {6,8} {7,9} {12,10} {13,11} {14,-} {15,-}
-#define I4SCHED0 0xFEDC765410ull
-#define I4SCHED1 0xFFBA9832FFull
+__device__ constexpr int i4s0(int s) { return s < 2 ? s : s < 4 ? s + 2 : s < 6 ? s + 2 : s < 8 ? s + 6 : s + 6; }
+__device__ constexpr int i4s1(int s) { return s == 2 ? 2 : s == 3 ? 3 : s == 4 ? 8 : s == 5 ? 9 : s == 6 ? 10 : s == 7 ? 11 : -1; }
+static_assert(i4s0(0) == 0 && i4s0(2) == 4 && i4s0(4) == 6 && i4s0(6) == 12 && i4s0(9) == 15, "I4x4 schedule");
 
 // Intra 4x4 prediction as a table (8.3.1.2.1-9): every mode and position is
 // v = (A + wB*B + wC*C + rnd) >> sh over the block's 13 neighbours Sx[0..12]
 // (Sx[3-k] = p[-1,k], Sx[4] = p[-1,-1], Sx[5+k] = p[k,-1]), or DC.  Entry:
-// byte offsets of A, B, C in the gathered neighbour array (Sx[i] at i, or
-// i + 3 for i >= 5, so left and top are aligned dwords), wB, wC, sh, DC flag.
-__device__ uint32_t i4_entry(int mode, int x, int y)
+// the tile offsets of A, B, C relative to the block's sample (0,0) as int8
+// (the top-right samples p[4..7,-1] read as p[3,-1] when unavailable, avtr =
+// 0 -- intra_prediction.c:789-792), wB (bits 24-25), wC (26), sh (27-28),
+// DC flag (29).  Index ((avtr * 9 + mode) * 16 + y * 4 + x).
+__device__ uint32_t i4_entry(int mode, int x, int y, int avtr)
 {
     int a = 0, b = 0, c = 0, wb = 0, wc = 0, sh = 0;
     bool dc = false;
@@ -673,137 +605,191 @@ __device__ uint32_t i4_entry(int mode, int x, int y)
         break;
     }
     }
-    auto off = [](int i) { return i <= 4 ? i : i + 3; };
-    return (uint32_t)(off(a) | off(b) << 4 | off(c) << 8 | wb << 12 | wc << 14 | sh << 16) | (dc ? 1u << 20 : 0u);
+    auto rel = [&](int i) {
+        int r;
+        if (i <= 3) r = (3 - i) * TY_STRIDE - 1;                  // p[-1, 3-i]
+        else if (i == 4) r = -TY_STRIDE - 1;                      // p[-1, -1]
+        else r = -TY_STRIDE + ((i - 5 > 3 && !avtr) ? 3 : i - 5); // p[i-5, -1]
+        return (uint32_t)r & 255u;
+    };
+    return rel(a) | rel(b) << 8 | rel(c) << 16 | (uint32_t)wb << 24 | (uint32_t)wc << 26 | (uint32_t)sh << 27 |
+           (dc ? 1u << 29 : 0u);
 }
+#define I4TAB_N (2 * 9 * 16)
 
+// Intra reconstruction of one MB from its tiles, whose halos are filled:
+// prediction + residual (res: the MB's residual staged in LDS) + clip.
+// I16x16 luma and chroma are written straight into the ring slot px; I4x4
+// luma into the tile (each block predicts from the blocks before it) -- the
+// caller copies it.  Every lane issues all of its LDS reads of a phase before
+// it uses any, so a phase costs one LDS round trip
+// (Intra16x16 :626-686, Intra4x4 :700-832, IntraChroma :844-914,
+// AddResidual :926-988).
 __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
-                           uint8_t *ty, uint8_t *tu, uint8_t *tv, const uint32_t *i4tab, uint8_t *sx, uint8_t *junk,
-                           int lane)
+                                           uint8_t *ty, uint8_t *tu, uint8_t *tv, const uint32_t *i4tab, uint8_t *junk,
+                                           uint8_t *px, int lane)
 {
-    const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C;
+    const bool aA = avail & AV_A, aB = avail & AV_B;
     if (mbtype == MBT_I16) {
         const int mode = pred & 3;
         const int y = lane >> 2, x0 = (lane & 3) * 4;
-        int dcv = 128, pa = 0, pb = 0, pc = 0;
-        if (mode == 2) {
-            int st = 0, sl = 0;
-            for (int i = 0; i < 16; i++) { st += ty[1 + i]; sl += ty[(i + 1) * TY_STRIDE]; }
-            if (aA && aB) dcv = (st + sl + 16) >> 5;
-            else if (aA) dcv = (sl + 8) >> 4;
-            else if (aB) dcv = (st + 8) >> 4;
-        } else if (mode == 3) {
-            int H = 0, V = 0;
-            for (int i = 0; i < 8; i++) {
-                H += (i + 1) * ((int)ty[1 + 8 + i] - (int)ty[1 + 6 - i]);
-                V += (i + 1) * ((int)ty[(1 + 8 + i) * TY_STRIDE] - (int)ty[(1 + 6 - i) * TY_STRIDE]);
-            }
-            pa = 16 * ((int)ty[16 * TY_STRIDE] + (int)ty[16]);
-            pb = (5 * H + 32) >> 6;
-            pc = (5 * V + 32) >> 6;
-        }
         int pv[4];
+        if (mode == 0) {                                          // vertical
+            const uint32_t t = *(const uint32_t *)&ty[TX0 + x0];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int x = x0 + i;
-            int pr;
-            if (mode == 0) pr = ty[1 + x];
-            else if (mode == 1) pr = ty[(y + 1) * TY_STRIDE];
-            else if (mode == 2) pr = dcv;
-            else pr = clip255((pa + pb * (x - 7) + pc * (y - 7) + 16) >> 5);
-            pv[i] = clip255(pr + (has_res ? res[y * 16 + x] : 0));
+            for (int i = 0; i < 4; i++) pv[i] = (t >> (8 * i)) & 255;
+        } else if (mode == 1) {                                   // horizontal
+            const int l = ty[(y + 1) * TY_STRIDE + TX0 - 1];
+#pragma unroll
+            for (int i = 0; i < 4; i++) pv[i] = l;
+        } else {
+            uint32_t tdw[4];
+            int lc[16];
+#pragma unroll
+            for (int k = 0; k < 4; k++) tdw[k] = *(const uint32_t *)&ty[TX0 + 4 * k];
+#pragma unroll
+            for (int k = 0; k < 16; k++) lc[k] = ty[(k + 1) * TY_STRIDE + TX0 - 1];
+            if (mode == 2) {                                      // DC
+                int st = 0, sl = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++) st += (int)__builtin_amdgcn_sad_u8(tdw[k], 0u, 0u);
+#pragma unroll
+                for (int k = 0; k < 16; k++) sl += lc[k];
+                const int dcv = (aA && aB) ? (st + sl + 16) >> 5 : aA ? (sl + 8) >> 4 : aB ? (st + 8) >> 4 : 128;
+#pragma unroll
+                for (int i = 0; i < 4; i++) pv[i] = dcv;
+            } else {                                              // plane
+                const int tl = ty[TX0 - 1];
+                auto T = [&](int k) { return k < 0 ? tl : (int)((tdw[k >> 2] >> ((k & 3) * 8)) & 255); };
+                auto Lc = [&](int k) { return k < 0 ? tl : lc[k]; };
+                int H = 0, V = 0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    H += (i + 1) * (T(8 + i) - T(6 - i));
+                    V += (i + 1) * (Lc(8 + i) - Lc(6 - i));
+                }
+                const int pa = 16 * (Lc(15) + T(15)), pb = (5 * H + 32) >> 6, pc = (5 * V + 32) >> 6;
+#pragma unroll
+                for (int i = 0; i < 4; i++) pv[i] = clip255((pa + pb * (x0 + i - 7) + pc * (y - 7) + 16) >> 5);
+            }
         }
-        wave_sync();
+        uint32_t pk = 0;
+        if (has_res) {
+            const uint2 rr = *(const uint2 *)&res[y * 16 + x0];
+            const int r4[4] = {(int)(int16_t)(rr.x & 0xFFFF), (int)(int16_t)(rr.x >> 16), (int)(int16_t)(rr.y & 0xFFFF),
+                               (int)(int16_t)(rr.y >> 16)};
 #pragma unroll
-        for (int i = 0; i < 4; i++) ty[(y + 1) * TY_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
+            for (int i = 0; i < 4; i++) pk |= (uint32_t)clip255(pv[i] + r4[i]) << (8 * i);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) pk |= (uint32_t)pv[i] << (8 * i);
+        }
+        *(uint32_t *)&px[y * 16 + x0] = pk;
     } else {
-        // 10-step sub-wavefront, two blocks per step (I4SCHED0/1): lanes
-        // 0..15 = slot 0, 16..31 = slot 1 (lanes 32..63 mirror, writing to
-        // their junk slots).  Per step: gather each block's 13 neighbours into
-        // sx[slot], then one table-driven formula per sample.
-        const int slot = (lane >> 4) & 1, pos = lane & 15;
-        const int px = pos & 3, py = pos >> 2;
+        // I4x4, lanes 0..15 = block of slot 0, 16..31 = slot 1 (lanes 32..63
+        // mirror, writing to their junk bytes)
+        const int slot = (lane >> 4) & 1, pos = lane & 15, px4 = pos & 3, py4 = pos >> 2;
         const bool lo = lane < 32;
-        // gather offsets relative to the block's (0,0): neighbour i = pos;
-        // top-right samples (i > 8) fall back to p[3,-1] when unavailable
-        const int rel = pos <= 3 ? (3 - pos) * TY_STRIDE - 1 : pos == 4 ? -TY_STRIDE - 1 : -TY_STRIDE + min(pos - 5, 7);
-        const int rel_notr = pos > 8 ? -TY_STRIDE + 3 : rel;
-        const int gdst = pos <= 4 ? pos : pos + 3;
         // blocks whose top-right neighbour is available: 2,6,8,9,10,12,14
         // always; 0,1,4 from the MB above; 5 from the MB above-right
         const uint32_t trmask = 0x5744u | ((avail & AV_B) ? 0x13u : 0u) | ((avail & AV_C) ? 0x20u : 0u);
-        const bool aA4 = avail & AV_A, aB4 = avail & AV_B;
-#pragma unroll 1
-        for (int step = 0; step < 10; step++) {
-            const int s0 = (int)(I4SCHED0 >> (step * 4)) & 15, s1 = (int)(I4SCHED1 >> (step * 4)) & 15;
-            const bool valid = lo && (slot == 0 || s1 != 15);
-            const int b = slot ? s1 : s0;                               // 15 = none for slot 1 (block 15 is slot 0's)
-            const int bx = blk_x(b), by = blk_y(b);
-            const int t0 = (by * 4 + 1) * TY_STRIDE + bx * 4 + 1;       // tile offset of the block's (0,0)
-            const bool avTR = (trmask >> b) & 1;
-            const int mode = (int)(i4 >> (b * 4)) & 15;
-            // independent LDS reads first: table entry, residual, gathered neighbour
-            const uint32_t e = i4tab[(mode < 9 ? mode : 0) * 16 + pos];
-            const int rv = has_res ? res[(by * 4 + py) * 16 + bx * 4 + px] : 0;
-            const uint8_t g = ty[t0 + (avTR ? rel : rel_notr)];
-            *(valid && pos < 13 ? &sx[slot * 16 + gdst] : &junk[lane]) = g;
-            wave_sync();
-            const uint8_t *S = sx + slot * 16;
-            const int A = S[e & 15], B = S[(e >> 4) & 15], C = S[(e >> 8) & 15];
-            const uint32_t lw = *(const uint32_t *)S, tw = *(const uint32_t *)(S + 8);
-            const int sh = (int)((e >> 16) & 3);
-            int v = (A + (int)((e >> 12) & 3) * B + (int)((e >> 14) & 1) * C + ((1 << sh) >> 1)) >> sh;
-            // DC
-            const int sl = (int)__builtin_amdgcn_sad_u8(lw, 0u, 0u), st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
-            const bool avT = by > 0 || aB4, avL = bx > 0 || aA4;
-            const int dsum = (avT ? st : 0) + (avL ? sl : 0);
-            const int dsh = (avT && avL) ? 3 : 2;
-            const int dcv = (avT || avL) ? (dsum + (1 << (dsh - 1))) >> dsh : 128;
-            v = (e >> 20) & 1 ? dcv : v;
-            v = clip255(v + rv);
-            *(valid ? &ty[t0 + py * TY_STRIDE + px] : &junk[lane]) = (uint8_t)v;
+        // every step's table entry and residual sample, issued up front: they
+        // do not depend on the reconstruction
+        uint32_t ent[10];
+        int rv[10];
+#pragma unroll
+        for (int s = 0; s < 10; s++) {
+            const int b0 = i4s0(s), b1 = i4s1(s) < 0 ? i4s0(s) : i4s1(s);
+            const int m0 = (int)(i4 >> (b0 * 4)) & 15, m1 = (int)(i4 >> (b1 * 4)) & 15;
+            const int e0 = ((int)(trmask >> b0) & 1) * 9 + (m0 < 9 ? m0 : 0);
+            const int e1 = ((int)(trmask >> b1) & 1) * 9 + (m1 < 9 ? m1 : 0);
+            ent[s] = i4tab[(slot ? e1 : e0) * 16 + pos];
+            const int o0 = blk_y(b0) * 64 + blk_x(b0) * 4, o1 = blk_y(b1) * 64 + blk_x(b1) * 4;
+            rv[s] = has_res ? (int)res[(slot ? o1 : o0) + py4 * 16 + px4] : 0;
+        }
+#pragma unroll
+        for (int s = 0; s < 10; s++) {
+            const int b0 = i4s0(s), b1 = i4s1(s);
+            const int t0c = (blk_y(b0) * 4 + 1) * TY_STRIDE + TX0 + blk_x(b0) * 4;
+            const int t1c = b1 >= 0 ? (blk_y(b1) * 4 + 1) * TY_STRIDE + TX0 + blk_x(b1) * 4 : t0c;
+            const bool valid = lo && (slot == 0 || b1 >= 0);
+            const int t0 = slot ? t1c : t0c;
+            const uint32_t e = ent[s];
+            const int A = ty[t0 + (int)(int8_t)(e & 255)];
+            const int B = ty[t0 + (int)(int8_t)((e >> 8) & 255)];
+            const int C = ty[t0 + (int)(int8_t)((e >> 16) & 255)];
+            const int sh = (int)((e >> 27) & 3);
+            int v = (A + (int)((e >> 24) & 3) * B + (int)((e >> 26) & 1) * C + ((1 << sh) >> 1)) >> sh;
+            // DC: only in steps where some block is DC (wave-uniform)
+            const int m0 = (int)(i4 >> (b0 * 4)) & 15, m1 = b1 >= 0 ? (int)(i4 >> (b1 * 4)) & 15 : 0;
+#ifdef DBG_DC_ALWAYS
+            if (true) {
+#else
+            if (m0 == 2 || (b1 >= 0 && m1 == 2)) {
+#endif
+                const uint32_t tw = *(const uint32_t *)&ty[t0 - TY_STRIDE];
+                const int sl = ty[t0 - 1] + ty[t0 - 1 + TY_STRIDE] + ty[t0 - 1 + 2 * TY_STRIDE] + ty[t0 - 1 + 3 * TY_STRIDE];
+                const int st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
+                const int bb = slot && b1 >= 0 ? b1 : b0;
+                const bool avT = blk_y(bb) > 0 || aB, avL = blk_x(bb) > 0 || aA;
+                const int dsum = (avT ? st : 0) + (avL ? sl : 0);
+                const int dsh = (avT && avL) ? 3 : 2;
+                const int dcv = (avT || avL) ? (dsum + (1 << (dsh - 1))) >> dsh : 128;
+                v = (e >> 29) & 1 ? dcv : v;
+            }
+            v = clip255(v + rv[s]);
+            *(valid ? &ty[t0 + py4 * TY_STRIDE + px4] : &junk[lane]) = (uint8_t)v;
+#ifdef DBG_LGKM
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
             wave_sync();
         }
     }
-    {   // chroma: lane -> (comp, row, pair)
+    {   // chroma: lane -> (comp, row, pair), straight into the slot
         const int comp = lane >> 5, y = (lane >> 2) & 7, x0 = (lane & 3) * 2;
-        uint8_t *T = comp ? tv : tu;
+        const uint8_t *T = comp ? tv : tu;
         const int cmode = (pred >> 4) & 3;
         int pv[2];
-        int pa = 0, pb = 0, pc = 0;
-        if (cmode == 3) {
-            int H = 0, V = 0;
-            for (int i = 0; i < 4; i++) {
-                H += (i + 1) * ((int)T[1 + 4 + i] - (int)T[1 + 2 - i]);
-                V += (i + 1) * ((int)T[(1 + 4 + i) * TC_STRIDE] - (int)T[(1 + 2 - i) * TC_STRIDE]);
-            }
-            pa = 16 * ((int)T[8 * TC_STRIDE] + (int)T[8]);
-            pb = (34 * H + 32) >> 6;
-            pc = (34 * V + 32) >> 6;
-        }
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            const int x = x0 + i;
+        if (cmode == 0) {                                         // DC per 4x4 quadrant (:1175-1245)
+            const int xo = x0 & 4, yo = y & 4;
+            const uint32_t tw = *(const uint32_t *)&T[TX0 + xo];
+            const int sl = T[(yo + 1) * TC_STRIDE + TX0 - 1] + T[(yo + 2) * TC_STRIDE + TX0 - 1] +
+                           T[(yo + 3) * TC_STRIDE + TX0 - 1] + T[(yo + 4) * TC_STRIDE + TX0 - 1];
+            const int st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
             int pr;
-            if (cmode == 0) {
-                const int xo = x & 4, yo = y & 4;
-                int st = 0, sl = 0;
-                for (int k = 0; k < 4; k++) { st += T[1 + xo + k]; sl += T[(1 + yo + k) * TC_STRIDE]; }
-                if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) {
-                    pr = (aA && aB) ? (st + sl + 4) >> 3 : aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
-                } else if (xo > 0) {
-                    pr = aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
-                } else {
-                    pr = aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
-                }
-            } else if (cmode == 1) pr = T[(y + 1) * TC_STRIDE];
-            else if (cmode == 2) pr = T[1 + x];
-            else pr = clip255((pa + pb * (x - 3) + pc * (y - 3) + 16) >> 5);
-            pv[i] = clip255(pr + (has_res ? res[256 + comp * 64 + y * 8 + x] : 0));
-        }
-        wave_sync();
+            if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) pr = (aA && aB) ? (st + sl + 4) >> 3 : aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
+            else if (xo > 0) pr = aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
+            else pr = aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
+            pv[0] = pv[1] = pr;
+        } else if (cmode == 1) {                                  // horizontal
+            pv[0] = pv[1] = T[(y + 1) * TC_STRIDE + TX0 - 1];
+        } else if (cmode == 2) {                                  // vertical
+            pv[0] = T[TX0 + x0]; pv[1] = T[TX0 + x0 + 1];
+        } else {                                                  // plane
+            const uint32_t t0w = *(const uint32_t *)&T[TX0], t1w = *(const uint32_t *)&T[TX0 + 4];
+            int lc[8];
 #pragma unroll
-        for (int i = 0; i < 2; i++) T[(y + 1) * TC_STRIDE + 1 + x0 + i] = (uint8_t)pv[i];
+            for (int k = 0; k < 8; k++) lc[k] = T[(k + 1) * TC_STRIDE + TX0 - 1];
+            const int tl = T[TX0 - 1];
+            auto Tt = [&](int k) { return k < 0 ? tl : (int)(((k < 4 ? t0w : t1w) >> ((k & 3) * 8)) & 255); };
+            auto Lc = [&](int k) { return k < 0 ? tl : lc[k]; };
+            int H = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                H += (i + 1) * (Tt(4 + i) - Tt(2 - i));
+                V += (i + 1) * (Lc(4 + i) - Lc(2 - i));
+            }
+            const int pa = 16 * (Lc(7) + Tt(7)), pb = (34 * H + 32) >> 6, pc = (34 * V + 32) >> 6;
+#pragma unroll
+            for (int i = 0; i < 2; i++) pv[i] = clip255((pa + pb * (x0 + i - 3) + pc * (y - 3) + 16) >> 5);
+        }
+        const int o = 256 + comp * 64 + y * 8 + x0;
+        if (has_res) {
+            const uint32_t rr = *(const uint32_t *)&res[o];
+            pv[0] = clip255(pv[0] + (int)(int16_t)(rr & 0xFFFF));
+            pv[1] = clip255(pv[1] + (int)(int16_t)(rr >> 16));
+        }
+        *(uint16_t *)&px[o] = (uint16_t)(pv[0] | (pv[1] << 8));
     }
     wave_sync();
 }
@@ -1046,16 +1032,54 @@ __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v,
 // (out of line to keep the kernel's VGPR count for 3 workgroups per CU; the
 // arguments are plain values: a reference to the kernel's ReconArgs would
 // force the whole argument block into private memory)
+// The LDS objects come in as address-space-3 pointers and the record and the
+// error word as address-space-1 ones: a noinline function's generic pointer
+// arguments would turn every access inside into a FLAT instruction (counted
+// by vmcnt and lgkmcnt alike, at far more than LDS latency per dependent
+// access -- measured, 4.7 us per intra MB).  The generic views below are
+// addrspacecasts of those arguments, which the compiler folds back into
+// ds_* / global_* accesses.
+typedef __attribute__((address_space(3))) McScratch lds_McScratch;
+typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
+typedef const __attribute__((address_space(1))) MbRec g_MbRec;
+typedef __attribute__((address_space(1))) unsigned g_u32;
 template <bool UPL, int RK>
-__device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const unsigned long long *mbx_up, unsigned *perr,
-                                                   int W, int c, uint32_t tag, bool has_up, int lane, McScratch &M,
-                                                   MbRing<RK> &R, const uint32_t *i4tab)
+__device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigned long long *mbx_up, g_u32 *perr_g,
+                                                   int W, int c, uint32_t tag, bool has_up, int lane, lds_McScratch *Ml,
+                                                   __attribute__((address_space(3))) MbRing<RK> *Rl, lds_cu32 *i4tab_l,
+                                                   __attribute__((address_space(1))) unsigned long long *pst)
 {
-    const MbRec &rec = *mbrec;
-    const int qtype = rec.type, avail = rec.avail, pred = rec.pred;
-    const uint64_t i4 = *(const uint64_t *)rec.i4;
+    // pst (profiling build): [0] left ready | top ready, [1] prediction done | slot written
+    unsigned long long st0 = 0, st1 = 0;
+    McScratch &M = *(McScratch *)Ml;
+    MbRing<RK> &R = *(MbRing<RK> *)Rl;
+    const uint32_t *i4tab = (const uint32_t *)i4tab_l;
+    unsigned *perr = (unsigned *)perr_g;
+    // the record's fields, wave-uniform (scalar branches below)
+    const uint32_t *rw = (const uint32_t *)mbrec;
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(rw[0]), d1 = __builtin_amdgcn_readfirstlane(rw[1]);
+    const uint32_t cbits = __builtin_amdgcn_readfirstlane(rw[2]);
+    // (readfirstlane returns int: widen through uint32_t, or a mode >= 8 in
+    // block 7 sign-extends into blocks 8..15)
+    const uint64_t i4 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(rw[4]) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(rw[5]) << 32;
+    const int qtype = d0 & 255, avail = d0 >> 24, pred = d1 & 255;
     const int slot = c & (RK - 1);
     const bool aA = avail & AV_A, aB = avail & AV_B, aC = avail & AV_C, aD = avail & AV_D;
+    // the row above's entries first: lanes 24..31 entry c dwords 24..31 (B),
+    // 32 entry c+1 dword 24 (C), 33..35 entry c-1 dwords 27/29/31 (D).  The
+    // loads are issued before the wait for the left MB, so their L2 round
+    // trip overlaps it; re-polled only if some granule is still stale
+    const bool need_top = has_up && (aB || aC || aD);
+    const int dsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;
+    const int dw = lane < 32 ? (lane & 31) : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 24;
+    const unsigned long long *g = mbx_up + min(max(c + dsel, 0), W - 1) * 32 + dw;
+    const bool mine = need_top && ((lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD));
+#ifndef INTRA_TOP_LATE
+    unsigned long long gr = need_top ? ld_granT<UPL>(g) : 0ull;
+#else
+    unsigned long long gr = 0ull;
+#endif
     if (aA) {
         unsigned spins = 0;
         while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[(c - 1) & (RK - 1)])) != c) {
@@ -1064,58 +1088,49 @@ __device__ __attribute__((noinline)) void mc_intra(const MbRec *mbrec, const uns
         }
         wave_sync();
     }
-    uint32_t top = 0;
-    if (has_up && (aB || aC || aD)) {
-        // lanes 24..31: entry c dwords 24..31 (B); 32: entry c+1 dword 24 (C);
-        // 33..35: entry c-1 dwords 27/29/31 (D)
-        const int dsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;
-        const int dw = lane < 32 ? (lane & 31) : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 24;
-        const int ce = min(max(c + dsel, 0), W - 1);
-        const unsigned long long *g = mbx_up + ce * 32 + dw;
-        const bool mine = (lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD);
-        unsigned long long gr = ld_granT<UPL>(g);
+    if (pst) st0 = wall_clock64();
+#ifdef INTRA_TOP_LATE
+    if (need_top) gr = ld_granT<UPL>(g);
+#endif
+    if (need_top) {
         unsigned spins = 0;
         while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
             __builtin_amdgcn_s_sleep(1);
             if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
             if (mine) gr = ld_granT<UPL>(g);
         }
-        top = (uint32_t)gr;
     }
+    const uint32_t top = (uint32_t)gr;
+    if (pst) st0 = (st0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
     const uint8_t *lp = R.px[(c - 1) & (RK - 1)];
-    {   // tile halo: top row (incl. top-left / top-right), left column
-        const uint32_t b0 = top & 255, b1 = (top >> 8) & 255, b2 = (top >> 16) & 255, b3 = top >> 24;
+    {   // tile halo: the row above (dwords), its top-left / top-right, the left column
         if (lane >= 24 && lane < 32) {
-            if (aB) {
-                const int k = lane - 24;
-                uint8_t *dst = k < 4 ? &M.ty[1 + k * 4] : (k < 6 ? &M.tu[1 + (k - 4) * 4] : &M.tv[1 + (k - 6) * 4]);
-                dst[0] = b0; dst[1] = b1; dst[2] = b2; dst[3] = b3;
-            }
+            const int k = lane - 24;
+            if (aB) *(uint32_t *)(k < 4 ? &M.ty[TX0 + k * 4] : k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
         } else if (lane == 32) {
-            if (aC) { M.ty[17] = b0; M.ty[18] = b1; M.ty[19] = b2; M.ty[20] = b3; }
+            if (aC) *(uint32_t *)&M.ty[TX0 + 16] = top;
         } else if (lane < 36) {
-            if (aD) (lane == 33 ? M.ty[0] : lane == 34 ? M.tu[0] : M.tv[0]) = b3;
+            if (aD) (lane == 33 ? M.ty[TX0 - 1] : lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
         } else if (lane >= 40 && lane < 56) {
-            if (aA) M.ty[(lane - 39) * TY_STRIDE] = lp[(lane - 40) * 16 + 15];
+            if (aA) M.ty[(lane - 39) * TY_STRIDE + TX0 - 1] = lp[(lane - 40) * 16 + 15];
         } else if (lane >= 56) {
             const int k = lane - 56;
-            if (aA) { M.tu[(k + 1) * TC_STRIDE] = lp[256 + k * 8 + 7]; M.tv[(k + 1) * TC_STRIDE] = lp[320 + k * 8 + 7]; }
+            if (aA) {
+                M.tu[(k + 1) * TC_STRIDE + TX0 - 1] = lp[256 + k * 8 + 7];
+                M.tv[(k + 1) * TC_STRIDE + TX0 - 1] = lp[320 + k * 8 + 7];
+            }
         }
     }
     wave_sync();
-    intra_tile(qtype, avail, pred, i4, M.res, rec.cbits != 0, M.ty, M.tu, M.tv, i4tab, M.sx, M.junk, lane);
     uint8_t *px = R.px[slot];
-    {   // tile -> slot (tile samples start at column 1: byte reads)
+    intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane);
+    if (pst) st1 = wall_clock64();
+    if (qtype == MBT_I4x4) {   // the luma tile -> slot (I16x16 and chroma went there directly)
         const int orow = lane >> 2, oq = lane & 3;
-        const uint8_t *sy = &M.ty[(orow + 1) * TY_STRIDE + 1 + oq * 4];
-        *(uint32_t *)&px[orow * 16 + oq * 4] = sy[0] | (sy[1] << 8) | (sy[2] << 16) | ((uint32_t)sy[3] << 24);
-    }
-    if (lane < 32) {
-        const int comp = (lane >> 4) & 1, crow = (lane >> 1) & 7, cq = lane & 1;
-        const uint8_t *sp = &(comp ? M.tv : M.tu)[(crow + 1) * TC_STRIDE + 1 + cq * 4];
-        *(uint32_t *)&px[256 + comp * 64 + crow * 8 + cq * 4] = sp[0] | (sp[1] << 8) | (sp[2] << 16) | ((uint32_t)sp[3] << 24);
+        *(uint32_t *)&px[orow * 16 + oq * 4] = *(const uint32_t *)&M.ty[(orow + 1) * TY_STRIDE + TX0 + oq * 4];
     }
     wave_sync();
+    if (pst && lane == 0) { pst[0] = st0; pst[1] = (st1 & 0xFFFFFFFFull) | (wall_clock64() << 32); }
 }
 
 // ---------------------------------------------------------------------------
@@ -1151,7 +1166,7 @@ struct __attribute__((aligned(16))) PPLds {
     PPRegion G[2];
     uint8_t junk[2][256];
     int hdone, copied, pdone, fin;
-    uint32_t i4tab[9 * 16];
+    uint32_t i4tab[I4TAB_N];
     unsigned long long ptw1[8];     // PROF: wave 1's phase sums, added by wave 0
 };
 
@@ -1295,7 +1310,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         // may start); [1] V(c) start (after the hdone wait and halo copy) in
         // bits 0..31, V(c) end in bits 32..63; [2] entry c published in bits
         // 0..31, H(c) end (hdone = c + 1) in bits 32..63
-        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * 4 : nullptr;
+        unsigned long long *pmb = prof ? a.prof + (size_t)a.npics * H * 16 + ((size_t)(p * H + r) * W + c) * PROF_MB : nullptr;
         const cu32p rw = recw + c * 24;
         const uint32_t h0 = rw[0];
         // MB c+1's record dword 0 (avail), for the hand-off patch (a VMEM load:
@@ -1788,14 +1803,17 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             }
             wave_sync();
         }
-        const unsigned long long t0 = PROF ? clock64() : 0;
+        const unsigned long long t0 = PROF ? wall_clock64() : 0;      // MB c's MC start (ring slot free)
         const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], Mw.res, R.db[slot]);
         if (type == MBT_IPCM) {
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
             ((uint32_t *)R.px[slot])[lane] = src[lane];
             if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
         } else if (type >= MBT_I4x4) {
-            mc_intra<UPL, RK>(a.rec + pd.rec_base + r * a.w + c, mbx_up, a.err + p, a.w, c, a.epoch, r > 0, lane, Mw, R, i4tab);
+            mc_intra<UPL, RK>((g_MbRec *)(a.rec + pd.rec_base + r * a.w + c), mbx_up, (g_u32 *)(a.err + p), a.w, c, a.epoch,
+                              r > 0, lane, (lds_McScratch *)&Mw, (__attribute__((address_space(3))) MbRing<RK> *)&R,
+                              (lds_cu32 *)i4tab,
+                              (__attribute__((address_space(1))) unsigned long long *)(PROF ? a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4 : nullptr));
         }
         wave_sync();
         {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
@@ -1804,7 +1822,9 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             const uint32_t v = *(const uint32_t *)&px[kk < 4 ? 240 + kk * 4 : kk < 6 ? 312 + (kk - 4) * 4 : 376 + (kk - 6) * 4];
             if (r + 1 < a.h) st_granT<MEL>(mbx_me + c * 32 + 24 + kk, v, a.epoch);
         }
-        if (PROF && lane == 0) a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * 4 + 3] = clock64() - t0;
+        // PROF stamp [3]: MC start in bits 0..31, flag set (slot final) in bits 32..63 (100 MHz)
+        if (PROF && lane == 0)
+            a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 3] = (t0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
         if (lane == 0) lds_st(&R.flag[slot], c + 1);
         v0 = nv0;
         if (more && D.n) dep_wait(a, p, v0, lane, D);
@@ -1842,7 +1862,8 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
         if (threadIdx.x < RK) R[q].flag[threadIdx.x] = 0;
         if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
-    for (int e = threadIdx.x; e < 9 * 16; e += 64 * (NMC + 2) * RPW) L[0].i4tab[e] = i4_entry(e >> 4, e & 3, (e >> 2) & 3);
+    for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
+        L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
     if (RPW > 1)        // granule tags from an earlier workgroup on this CU must not match
         for (int e = threadIdx.x; e < (RPW - 1) * a.w * 32; e += 64 * (NMC + 2) * RPW) lmbx[e] = 0;
     __syncthreads();

@@ -19,6 +19,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "_build", "liboracle.so")
 REFDEC = os.path.join(HERE, "_ref", "refdec")
+REFDEC_SOFTAVC = os.path.join(HERE, "_ref", "refdec_softavc")
 
 _L = None
 
@@ -31,6 +32,8 @@ def lib() -> C.CDLL:
         L = C.CDLL(LIB)
         L.oracle_decode_stream.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_double)]
         L.oracle_decode_stream.restype = C.c_void_p
+        L.oracle_decode_stream_nals.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_double)]
+        L.oracle_decode_stream_nals.restype = C.c_void_p
         L.oracle_result_info.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                          C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_size_t)]
         L.oracle_result_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
@@ -50,14 +53,19 @@ def lib() -> C.CDLL:
     return _L
 
 
-def decode(stream: bytes, no_reorder: bool = False, info: bool = False):
+def decode(stream: bytes, no_reorder: bool = False, info: bool = False, softavc: int = -1):
     """Decode a whole Annex-B stream on the CPU (DecTestBench semantics incl.
-    the end-of-stream flush).  Returns (frames, errors, width, height, seconds)
-    [+ per output picture (pic_id, is_idr, nbrOfErrMBs) if info]."""
+    the end-of-stream flush; softavc >= 0: the SoftAVC protocol -- one NAL
+    per input buffer, intraConcealmentMethod = softavc).  Returns (frames,
+    errors, width, height, seconds) [+ per output picture (pic_id, is_idr,
+    nbrOfErrMBs) if info]."""
     L = lib()
     buf = C.create_string_buffer(stream, len(stream))
     secs = C.c_double()
-    res = L.oracle_decode_stream(C.cast(buf, C.c_void_p), len(stream), int(no_reorder), C.byref(secs))
+    if softavc >= 0:
+        res = L.oracle_decode_stream_nals(C.cast(buf, C.c_void_p), len(stream), int(softavc), C.byref(secs))
+    else:
+        res = L.oracle_decode_stream(C.cast(buf, C.c_void_p), len(stream), int(no_reorder), C.byref(secs))
     n, e, w, h, nb = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_size_t()
     L.oracle_result_info(res, C.byref(n), C.byref(e), C.byref(w), C.byref(h), C.byref(nb))
     data = np.empty(nb.value, dtype=np.uint8)
@@ -132,6 +140,30 @@ def refdec_frames(stream: bytes, no_reorder: bool = False, info: bool = False):
     fb = w * h * 3 // 2 if w else 0
     frames = [data[i:i + fb] for i in range(0, len(data), fb)] if fb else []
     return (frames, pics) if info else frames
+
+
+def refdec_softavc_frames(stream: bytes, method: int = 1):
+    """The reference decoder driven like SoftAVC (oracle/softavc_bench.c,
+    build container only): (frames, [(picId, isIdr, nbrOfErrMBs)])."""
+    if not os.path.exists(REFDEC_SOFTAVC):
+        raise FileNotFoundError(REFDEC_SOFTAVC)
+    with tempfile.TemporaryDirectory() as td:
+        src, yuv = os.path.join(td, "in.h264"), os.path.join(td, "out.yuv")
+        with open(src, "wb") as f:
+            f.write(stream)
+        out = subprocess.run([REFDEC_SOFTAVC, f"-M{method}", src, yuv], capture_output=True, text=True, check=True)
+        w = h = 0
+        pics = []
+        for line in out.stdout.splitlines():
+            f = line.split()
+            if f[0] == "SIZE":
+                w, h = int(f[1]), int(f[2])
+            elif f[0] == "PIC":
+                pics.append((int(f[1]), int(f[2]), int(f[3])))
+        data = open(yuv, "rb").read()
+    fb = w * h * 3 // 2
+    frames = [data[i:i + fb] for i in range(0, len(data), fb)] if fb else []
+    return frames, pics
 
 
 def yuv2rgba(i420, width: int, height: int) -> bytes:

@@ -82,6 +82,110 @@ void *oracle_decode_stream(const uint8_t *buf, size_t len, int no_reorder, doubl
     return o;
 }
 
+/* SoftAVC protocol (Decoder/SoftAVC.cpp:289-400): one input buffer per NAL
+ * unit (start code included), picId counting input buffers, the buffer
+ * re-fed until consumed, intraConcealmentMethod = intra_conceal
+ * (SoftAVC.cpp:335 sets 1), NextPicture drained after every buffer and
+ * flushed at end of stream. */
+static size_t next_start(const uint8_t *b, size_t n, size_t from)
+{
+    for (size_t i = from; i + 3 < n; i++)
+        if (b[i] == 0 && b[i + 1] == 0 && b[i + 2] == 1) return i > 0 && b[i - 1] == 0 ? i - 1 : i;
+    return n;
+}
+
+/* host/api.c's H264SwDecDecode loop over the decoder core (the oracle has
+ * no HIP backend, so api.c itself cannot link here): returns the
+ * H264SwDecRet code, *consumed = bytes up to pStrmCurrPos */
+enum { R_STRM_PROCESSED = 1, R_PIC_RDY = 2, R_PIC_RDY_BNE = 3, R_HDRS_RDY_BNE = 4, R_STRM_ERR = -2, R_MEMFAIL = -4 };
+static int api_decode(H264Dec *d, int *new_headers, const uint8_t *p0, uint32_t len, uint32_t pic_id, uint32_t *consumed)
+{
+    int ret = R_STRM_PROCESSED;
+    const uint8_t *p = p0;
+    do {
+        int r;
+        uint32_t nread = 0;
+        if (*new_headers) {
+            r = DEC_HDRS_RDY;
+            *new_headers = 0;
+        } else {
+            r = h264dec_decode(d, p, len, pic_id, &nread);
+        }
+        p += nread;
+        len = ((int32_t)(len - nread) >= 0) ? len - nread : 0;
+        switch (r) {
+        case DEC_HDRS_RDY:
+            if (d->dpb.flushed && d->dpb.num_out != d->dpb.out_index) {
+                d->dpb.flushed = 0;
+                *new_headers = 1;
+                ret = R_PIC_RDY_BNE;
+            } else {
+                ret = R_HDRS_RDY_BNE;
+            }
+            len = 0;
+            break;
+        case DEC_PIC_RDY:
+            ret = len == 0 ? R_PIC_RDY : R_PIC_RDY_BNE;
+            len = 0;
+            break;
+        case DEC_PARAM_SET_ERROR:
+            if (!h264dec_valid_param_sets(d) && len == 0) ret = R_STRM_ERR;
+            break;
+        case DEC_MEMALLOC_ERROR:
+            ret = R_MEMFAIL;
+            len = 0;
+            break;
+        default:
+            break;
+        }
+    } while (len);
+    *consumed = (uint32_t)(p - p0);
+    return ret;
+}
+
+void *oracle_decode_stream_nals(const uint8_t *buf, size_t len, int intra_conceal, double *seconds)
+{
+    OracleOut *o = (OracleOut *)calloc(1, sizeof(OracleOut));
+    H264Dec *d = (H264Dec *)calloc(1, sizeof(H264Dec));
+    if (!o || !d) { free(o); free(d); return NULL; }
+    h264dec_init(d, 0, oracle_backend_create());
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    uint32_t pic_id = 0;
+    int new_headers = 0, headers = 0;
+    size_t pos = next_start(buf, len, 0);
+    while (pos < len) {
+        const size_t end = next_start(buf, len, pos + 3);
+        const uint8_t *p = buf + pos;
+        uint32_t left = (uint32_t)(end - pos);
+        pic_id++;
+        while (left > 0) {
+            uint32_t used = 0;
+            d->intra_conceal = intra_conceal;
+            const int r = api_decode(d, &new_headers, p, left, pic_id, &used);
+            if (r == R_HDRS_RDY_BNE) headers = 1;
+            if (r == R_HDRS_RDY_BNE || r == R_PIC_RDY_BNE) {
+                p += used;
+                left -= used < left ? used : left;
+            } else {
+                if (r < 0) o->errors++;
+                left = 0;
+            }
+        }
+        if (headers) drain(d, o);
+        pos = end;
+    }
+    h264dec_flush(d);
+    drain(d, o);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    const Sps *s = h264dec_active_sps(d);
+    if (s) { o->w = s->w_mbs * 16; o->h = s->h_mbs * 16; }
+    h264dec_release(d);
+    free(d);
+    return o;
+}
+
 int oracle_result_info(void *res, int *npics, int *errors, int *w, int *h, size_t *bytes)
 {
     OracleOut *o = (OracleOut *)res;

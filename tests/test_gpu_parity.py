@@ -298,3 +298,28 @@ def test_broadway_glue_callbacks():
     L.broadwayExit()
     assert len(heads) >= 1
     assert md5s(got) == c["frames"]
+
+
+@pytest.mark.parametrize("share", [0, 2])
+@pytest.mark.parametrize("k", [2, 5])
+def test_device_flag_reaches_its_own_picture_under_reordering(share, k, monkeypatch):
+    """A device flag (ReconArgs::err) raised for the k-th reconstruction
+    (test hook H264MI_DEBUG_FLAG_PICTURE) is reported as nbrOfErrMBs = all
+    MBs on exactly the output picture with picId k -- on a stream whose
+    output order differs from decode order (POC type 0, MMCO, long-term),
+    through the private and the shared engine -- and on no other picture;
+    samples are unchanged."""
+    L = _lib.mi()
+    c = CASES["ref_mmco_poc0_reorder"]
+    monkeypatch.setenv("H264MI_DEBUG_FLAG_PICTURE", str(k))
+    assert L.h264mi_set_share(share) == 0
+    try:
+        frames, _, pics = swdec_decode(stream(c), no_reorder=c["no_reorder"], info=True)
+    finally:
+        L.h264mi_set_share(0)
+    ow = c["overrides"]
+    nmbs = ow["w_mbs"] * ow["h_mbs"]
+    assert md5s(frames) == c["frames"]
+    assert [p[0] for p in pics] == [p[0] for p in c["pics"]]
+    for got, ref in zip(pics, c["pics"]):
+        assert got[2] == (nmbs if got[0] == k else ref[2]), (got, ref)

@@ -41,10 +41,10 @@ for i in range(len(run.launches)):
     run.launch(i)
     eng.sync()
 print("kernel", eng.kernel_name(), "config", CFG, "picture", PIC, "intra" if run.is_i[PIC][0] else "inter")
-n = S * h * 16 + S * w * h * 4
+n = S * h * 16 + S * w * h * 8
 buf = (C.c_uint64 * n)()
 L.h264mi_engine_profile(eng._h, 1, buf, n)
-m = np.frombuffer(buf, dtype=np.uint64)[S * h * 16:].reshape(S, h, w, 4)
+m = np.frombuffer(buf, dtype=np.uint64)[S * h * 16:].reshape(S, h, w, 8)
 lo = lambda x: (x & np.uint64(0xFFFFFFFF)).astype(np.int64)
 hi = lambda x: (x >> np.uint64(32)).astype(np.int64)
 Cst = lo(m[..., 0])
@@ -84,6 +84,7 @@ st("period", per)
 # where the hand-off tail and the period come from: by row band and by column band
 print("by row band (all columns 2..w-3):")
 for r0, r1 in ((1, 4), (4, 8), (8, 24), (24, 48), (48, h - 1)):
+    r1 = min(r1, h - 1)
     if r1 <= r0:
         continue
     pr = np.diff(Cst[:, r0:r1, :], axis=2)[:, :, 2:w - 3]
@@ -95,6 +96,9 @@ for r0, r1 in ((1, 4), (4, 8), (8, 24), (24, 48), (48, h - 1)):
           f" p90 {np.percentile(dl, 90) if dl.size else 0:.3f} | gated {g.mean() * 100:.0f} %")
 print("deep rows by column band:")
 for c0, c1 in ((2, 16), (16, 40), (40, 64), (64, 88), (88, w - 2)):
+    c1 = min(c1, w - 2)
+    if c1 <= c0:
+        continue
     tp = Cst[:, rows, c0:c1] - B[:, rows, c0:c1]
     g = tp > 0.05
     dl = (Cst[:, 8:h - 1, c0:c1] - E[:, 7:h - 2, c0:c1])[g]
@@ -104,3 +108,48 @@ for c0, c1 in ((2, 16), (16, 40), (40, 64), (64, 88), (88, w - 2)):
 # row 0's end and the second-to-last row's (the last row publishes nothing,
 # so its H end is not stamped)
 print(f"  row 0 end (us, mean over pictures): {D[:, 0, w - 1].mean():.1f}; row {h - 2} end: {D[:, h - 2, w - 1].mean():.1f}")
+
+# MC waves (stamp [3]: MC start = ring slot free, and flag set = slot final).
+# For intra MBs the MC chain is a wavefront: MB (r, c) needs MB (r, c-1)'s
+# slot (left, LDS flag) and the row above's unfiltered bottom row up to
+# column c+1 (mailbox dwords 24..31 through L2).
+M0, M1 = us(lo(m[..., 3])), us(hi(m[..., 3]))
+types = np.stack([np.frombuffer(caps[s].records_bytes(PIC), np.uint8).reshape(h, w, 96)[..., 0] for s in range(S)])
+intra = types >= 2
+print(f"MC: {intra.mean() * 100:.1f} % intra MBs; MC slot-final of row 0's last MB {M1[:, 0, w - 1].mean():.1f} us, "
+      f"of row {h - 1}'s {M1[:, h - 1, w - 1].mean():.1f} us")
+rr, cc = slice(1, h), slice(1, w - 1)
+left = M1[:, rr, 0:w - 2]
+top = M1[:, 0:h - 1, 2:w]
+own0 = M0[:, rr, cc]
+fin = M1[:, rr, cc]
+ready = np.maximum(np.maximum(left, top), own0)
+im = intra[:, rr, cc]
+if im.any():
+    st("intra MB work (final - max(left, top-right, start))", (fin - ready)[im])
+    gt = (top > left)[im]
+    print(f"  intra MBs gated by the row above (top-right later than left): {gt.mean() * 100:.1f} %")
+    st("intra: final - top-right final (gated by top)", (fin - top)[im][gt])
+    st("intra: final - left final (gated by left)", (fin - left)[im][~gt])
+    per_i = np.diff(M1, axis=2)[:, rr, 1:w - 2][intra[:, rr, 2:w - 1]]
+    st("intra in-row period (slot final c-1 -> c)", per_i)
+nm = ~im
+if nm.any():
+    st("inter MB MC (final - start)", (fin - own0)[nm])
+
+# inside mc_intra ([4]: left ready | top ready, [5]: prediction done | slot written)
+L0, T0 = us(lo(m[..., 4])), us(hi(m[..., 4]))
+P0, W0 = us(lo(m[..., 5])), us(hi(m[..., 5]))
+if im.any():
+    ok = im & (m[:, rr, cc, 4] != 0)
+    st("intra: top poll after left (top ready - left ready)", (T0 - L0)[:, rr, cc][ok])
+    st("intra: prediction (tile done - top ready)", (P0 - T0)[:, rr, cc][ok])
+    st("intra: tile -> slot copy", (W0 - P0)[:, rr, cc][ok])
+    st("intra: slot written -> flag (publish)", (M1 - W0)[:, rr, cc][ok])
+    st("intra: MC start -> left ready", (L0 - M0)[:, rr, cc][ok])
+    i4 = ok & (types[:, rr, cc] == 2)
+    i16 = ok & (types[:, rr, cc] == 3)
+    if i4.any():
+        st("  I4x4 prediction", (P0 - T0)[:, rr, cc][i4])
+    if i16.any():
+        st("  I16x16 prediction", (P0 - T0)[:, rr, cc][i16])
