@@ -617,20 +617,109 @@ __device__ uint32_t i4_entry(int mode, int x, int y, int avtr)
 }
 #define I4TAB_N (2 * 9 * 16)
 
-// Intra reconstruction of one MB from its tiles, whose halos are filled:
-// prediction + residual (res: the MB's residual staged in LDS) + clip.
-// I16x16 luma and chroma are written straight into the ring slot px; I4x4
-// luma into the tile (each block predicts from the blocks before it) -- the
-// caller copies it.  Every lane issues all of its LDS reads of a phase before
-// it uses any, so a phase costs one LDS round trip
+// Cross-MB intra pipelining: the left neighbour MB's samples are read from
+// its ring slot as they land there, not after it is complete.  LeftNb: that
+// slot's samples and progress words (MbRing::lprog / cprog, tagged with the
+// MB index) and this MB's own progress words.
+struct LeftNb {
+    const uint8_t *lp;              // left MB's ring slot (samples), NULL when unavailable (no AV_A)
+    const int *lprog, *cprog;       // its progress words
+    int *my_lprog, *my_cprog;       // this MB's
+    int ltag, mytag;                // (c - 1) << 4, c << 4
+    unsigned *perr;
+};
+__device__ __forceinline__ void prog_wait(const int *p, int want, int lane, unsigned *perr)
+{
+    unsigned spins = 0;
+    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
+    }
+    wave_sync();
+}
+__device__ __forceinline__ void prog_set(int *p, int v, int lane)
+{
+    wave_sync();
+    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Intra reconstruction of one MB from its tiles, whose top halo is filled;
+// the left column comes from the left MB's ring slot, part by part (LeftNb):
+// prediction + residual (res: the MB's residual staged in LDS) + clip, all
+// written straight into the ring slot px (I4x4 luma into the tile as well:
+// each block predicts from the blocks before it).  Chroma first (it waits
+// only for the left MB's chroma), then luma: an I4x4 block in column 0
+// waits for the left MB's block beside it, so the next MB's blocks follow
+// this one's 3 steps behind.  Every lane issues all of its LDS reads of a
+// phase before it uses any, so a phase costs one LDS round trip
 // (Intra16x16 :626-686, Intra4x4 :700-832, IntraChroma :844-914,
 // AddResidual :926-988).
 __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
                                            uint8_t *ty, uint8_t *tu, uint8_t *tv, const uint32_t *i4tab, uint8_t *junk,
-                                           uint8_t *px, int lane)
+                                           uint8_t *px, int lane, const LeftNb &N)
 {
     const bool aA = avail & AV_A, aB = avail & AV_B;
+    {   // chroma: lane -> (comp, row, pair), straight into the slot
+        if (aA) {
+            prog_wait(N.cprog, N.ltag | 1, lane, N.perr);
+            if (lane < 16) {
+                const int k = lane & 7, comp = lane >> 3;
+                (comp ? tv : tu)[(k + 1) * TC_STRIDE + TX0 - 1] = N.lp[256 + comp * 64 + k * 8 + 7];
+            }
+            wave_sync();
+        }
+        const int comp = lane >> 5, y = (lane >> 2) & 7, x0 = (lane & 3) * 2;
+        const uint8_t *T = comp ? tv : tu;
+        const int cmode = (pred >> 4) & 3;
+        int pv[2];
+        if (cmode == 0) {                                         // DC per 4x4 quadrant (:1175-1245)
+            const int xo = x0 & 4, yo = y & 4;
+            const uint32_t tw = *(const uint32_t *)&T[TX0 + xo];
+            const int sl = T[(yo + 1) * TC_STRIDE + TX0 - 1] + T[(yo + 2) * TC_STRIDE + TX0 - 1] +
+                           T[(yo + 3) * TC_STRIDE + TX0 - 1] + T[(yo + 4) * TC_STRIDE + TX0 - 1];
+            const int st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
+            int pr;
+            if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) pr = (aA && aB) ? (st + sl + 4) >> 3 : aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
+            else if (xo > 0) pr = aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
+            else pr = aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
+            pv[0] = pv[1] = pr;
+        } else if (cmode == 1) {                                  // horizontal
+            pv[0] = pv[1] = T[(y + 1) * TC_STRIDE + TX0 - 1];
+        } else if (cmode == 2) {                                  // vertical
+            pv[0] = T[TX0 + x0]; pv[1] = T[TX0 + x0 + 1];
+        } else {                                                  // plane
+            const uint32_t t0w = *(const uint32_t *)&T[TX0], t1w = *(const uint32_t *)&T[TX0 + 4];
+            int lc[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) lc[k] = T[(k + 1) * TC_STRIDE + TX0 - 1];
+            const int tl = T[TX0 - 1];
+            auto Tt = [&](int k) { return k < 0 ? tl : (int)(((k < 4 ? t0w : t1w) >> ((k & 3) * 8)) & 255); };
+            auto Lc = [&](int k) { return k < 0 ? tl : lc[k]; };
+            int H = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                H += (i + 1) * (Tt(4 + i) - Tt(2 - i));
+                V += (i + 1) * (Lc(4 + i) - Lc(2 - i));
+            }
+            const int pa = 16 * (Lc(7) + Tt(7)), pb = (34 * H + 32) >> 6, pc = (34 * V + 32) >> 6;
+#pragma unroll
+            for (int i = 0; i < 2; i++) pv[i] = clip255((pa + pb * (x0 + i - 3) + pc * (y - 3) + 16) >> 5);
+        }
+        const int o = 256 + comp * 64 + y * 8 + x0;
+        if (has_res) {
+            const uint32_t rr = *(const uint32_t *)&res[o];
+            pv[0] = clip255(pv[0] + (int)(int16_t)(rr & 0xFFFF));
+            pv[1] = clip255(pv[1] + (int)(int16_t)(rr >> 16));
+        }
+        *(uint16_t *)&px[o] = (uint16_t)(pv[0] | (pv[1] << 8));
+        prog_set(N.my_cprog, N.mytag | 1, lane);
+    }
     if (mbtype == MBT_I16) {
+        if (aA) {
+            prog_wait(N.lprog, N.ltag | 10, lane, N.perr);
+            if (lane < 16) ty[(lane + 1) * TY_STRIDE + TX0 - 1] = N.lp[lane * 16 + 15];
+            wave_sync();
+        }
         const int mode = pred & 3;
         const int y = lane >> 2, x0 = (lane & 3) * 4;
         int pv[4];
@@ -685,6 +774,7 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
             for (int i = 0; i < 4; i++) pk |= (uint32_t)pv[i] << (8 * i);
         }
         *(uint32_t *)&px[y * 16 + x0] = pk;
+        prog_set(N.my_lprog, N.mytag | 10, lane);
     } else {
         // I4x4, lanes 0..15 = block of slot 0, 16..31 = slot 1 (lanes 32..63
         // mirror, writing to their junk bytes)
@@ -710,8 +800,18 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
 #pragma unroll
         for (int s = 0; s < 10; s++) {
             const int b0 = i4s0(s), b1 = i4s1(s);
+            // a block in column 0 (steps 0, 2, 4, 6: blocks 0, 2, 8, 10) reads
+            // the left MB's block beside it (5, 7, 13, 15: its steps 3, 5, 7, 9)
+            if ((s & 1) == 0 && s <= 6 && aA) {
+                const int by = s == 0 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3;
+                prog_wait(N.lprog, N.ltag | (s + 4), lane, N.perr);
+                if (lane < 4) ty[(by * 4 + lane + 1) * TY_STRIDE + TX0 - 1] = N.lp[(by * 4 + lane) * 16 + 15];
+                wave_sync();
+            }
             const int t0c = (blk_y(b0) * 4 + 1) * TY_STRIDE + TX0 + blk_x(b0) * 4;
             const int t1c = b1 >= 0 ? (blk_y(b1) * 4 + 1) * TY_STRIDE + TX0 + blk_x(b1) * 4 : t0c;
+            const int p0c = blk_y(b0) * 64 + blk_x(b0) * 4;
+            const int p1c = b1 >= 0 ? blk_y(b1) * 64 + blk_x(b1) * 4 : p0c;
             const bool valid = lo && (slot == 0 || b1 >= 0);
             const int t0 = slot ? t1c : t0c;
             const uint32_t e = ent[s];
@@ -722,11 +822,7 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
             int v = (A + (int)((e >> 24) & 3) * B + (int)((e >> 26) & 1) * C + ((1 << sh) >> 1)) >> sh;
             // DC: only in steps where some block is DC (wave-uniform)
             const int m0 = (int)(i4 >> (b0 * 4)) & 15, m1 = b1 >= 0 ? (int)(i4 >> (b1 * 4)) & 15 : 0;
-#ifdef DBG_DC_ALWAYS
-            if (true) {
-#else
             if (m0 == 2 || (b1 >= 0 && m1 == 2)) {
-#endif
                 const uint32_t tw = *(const uint32_t *)&ty[t0 - TY_STRIDE];
                 const int sl = ty[t0 - 1] + ty[t0 - 1 + TY_STRIDE] + ty[t0 - 1 + 2 * TY_STRIDE] + ty[t0 - 1 + 3 * TY_STRIDE];
                 const int st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
@@ -739,57 +835,9 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
             }
             v = clip255(v + rv[s]);
             *(valid ? &ty[t0 + py4 * TY_STRIDE + px4] : &junk[lane]) = (uint8_t)v;
-#ifdef DBG_LGKM
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-            wave_sync();
+            *(valid ? &px[(slot ? p1c : p0c) + py4 * 16 + px4] : &junk[64 + lane]) = (uint8_t)v;
+            prog_set(N.my_lprog, N.mytag | (s + 1), lane);
         }
-    }
-    {   // chroma: lane -> (comp, row, pair), straight into the slot
-        const int comp = lane >> 5, y = (lane >> 2) & 7, x0 = (lane & 3) * 2;
-        const uint8_t *T = comp ? tv : tu;
-        const int cmode = (pred >> 4) & 3;
-        int pv[2];
-        if (cmode == 0) {                                         // DC per 4x4 quadrant (:1175-1245)
-            const int xo = x0 & 4, yo = y & 4;
-            const uint32_t tw = *(const uint32_t *)&T[TX0 + xo];
-            const int sl = T[(yo + 1) * TC_STRIDE + TX0 - 1] + T[(yo + 2) * TC_STRIDE + TX0 - 1] +
-                           T[(yo + 3) * TC_STRIDE + TX0 - 1] + T[(yo + 4) * TC_STRIDE + TX0 - 1];
-            const int st = (int)__builtin_amdgcn_sad_u8(tw, 0u, 0u);
-            int pr;
-            if ((xo == 0 && yo == 0) || (xo > 0 && yo > 0)) pr = (aA && aB) ? (st + sl + 4) >> 3 : aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
-            else if (xo > 0) pr = aB ? (st + 2) >> 2 : aA ? (sl + 2) >> 2 : 128;
-            else pr = aA ? (sl + 2) >> 2 : aB ? (st + 2) >> 2 : 128;
-            pv[0] = pv[1] = pr;
-        } else if (cmode == 1) {                                  // horizontal
-            pv[0] = pv[1] = T[(y + 1) * TC_STRIDE + TX0 - 1];
-        } else if (cmode == 2) {                                  // vertical
-            pv[0] = T[TX0 + x0]; pv[1] = T[TX0 + x0 + 1];
-        } else {                                                  // plane
-            const uint32_t t0w = *(const uint32_t *)&T[TX0], t1w = *(const uint32_t *)&T[TX0 + 4];
-            int lc[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) lc[k] = T[(k + 1) * TC_STRIDE + TX0 - 1];
-            const int tl = T[TX0 - 1];
-            auto Tt = [&](int k) { return k < 0 ? tl : (int)(((k < 4 ? t0w : t1w) >> ((k & 3) * 8)) & 255); };
-            auto Lc = [&](int k) { return k < 0 ? tl : lc[k]; };
-            int H = 0, V = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                H += (i + 1) * (Tt(4 + i) - Tt(2 - i));
-                V += (i + 1) * (Lc(4 + i) - Lc(2 - i));
-            }
-            const int pa = 16 * (Lc(7) + Tt(7)), pb = (34 * H + 32) >> 6, pc = (34 * V + 32) >> 6;
-#pragma unroll
-            for (int i = 0; i < 2; i++) pv[i] = clip255((pa + pb * (x0 + i - 3) + pc * (y - 3) + 16) >> 5);
-        }
-        const int o = 256 + comp * 64 + y * 8 + x0;
-        if (has_res) {
-            const uint32_t rr = *(const uint32_t *)&res[o];
-            pv[0] = clip255(pv[0] + (int)(int16_t)(rr & 0xFFFF));
-            pv[1] = clip255(pv[1] + (int)(int16_t)(rr >> 16));
-        }
-        *(uint16_t *)&px[o] = (uint16_t)(pv[0] | (pv[1] << 8));
     }
     wave_sync();
 }
@@ -1017,6 +1065,10 @@ struct __attribute__((aligned(16))) MbRing {
     uint8_t px[RK][384];
     uint8_t db[RK][64];
     int flag[RK];
+    // intra progress of the MB in the slot, tagged (c << 4) | n: lprog n =
+    // I4x4 steps whose samples are in px (10: all luma), cprog n = 1 once its
+    // chroma is -- the next MB's intra reads its left neighbours as they land
+    int lprog[RK], cprog[RK];
     int consumed;
 };
 
@@ -1075,23 +1127,8 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     const int dw = lane < 32 ? (lane & 31) : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 24;
     const unsigned long long *g = mbx_up + min(max(c + dsel, 0), W - 1) * 32 + dw;
     const bool mine = need_top && ((lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD));
-#ifndef INTRA_TOP_LATE
     unsigned long long gr = need_top ? ld_granT<UPL>(g) : 0ull;
-#else
-    unsigned long long gr = 0ull;
-#endif
-    if (aA) {
-        unsigned spins = 0;
-        while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[(c - 1) & (RK - 1)])) != c) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
-        }
-        wave_sync();
-    }
     if (pst) st0 = wall_clock64();
-#ifdef INTRA_TOP_LATE
-    if (need_top) gr = ld_granT<UPL>(g);
-#endif
     if (need_top) {
         unsigned spins = 0;
         while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
@@ -1102,8 +1139,8 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     }
     const uint32_t top = (uint32_t)gr;
     if (pst) st0 = (st0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
-    const uint8_t *lp = R.px[(c - 1) & (RK - 1)];
-    {   // tile halo: the row above (dwords), its top-left / top-right, the left column
+    {   // tile halo: the row above (dwords), its top-left / top-right (the left
+        // column is read from the left MB's slot as it lands, intra_tile)
         if (lane >= 24 && lane < 32) {
             const int k = lane - 24;
             if (aB) *(uint32_t *)(k < 4 ? &M.ty[TX0 + k * 4] : k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
@@ -1111,25 +1148,19 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
             if (aC) *(uint32_t *)&M.ty[TX0 + 16] = top;
         } else if (lane < 36) {
             if (aD) (lane == 33 ? M.ty[TX0 - 1] : lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
-        } else if (lane >= 40 && lane < 56) {
-            if (aA) M.ty[(lane - 39) * TY_STRIDE + TX0 - 1] = lp[(lane - 40) * 16 + 15];
-        } else if (lane >= 56) {
-            const int k = lane - 56;
-            if (aA) {
-                M.tu[(k + 1) * TC_STRIDE + TX0 - 1] = lp[256 + k * 8 + 7];
-                M.tv[(k + 1) * TC_STRIDE + TX0 - 1] = lp[320 + k * 8 + 7];
-            }
         }
     }
     wave_sync();
     uint8_t *px = R.px[slot];
-    intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane);
+    const int ls = (c - 1) & (RK - 1);
+    LeftNb N;
+    N.lp = R.px[ls];
+    N.lprog = &R.lprog[ls]; N.cprog = &R.cprog[ls];
+    N.my_lprog = &R.lprog[slot]; N.my_cprog = &R.cprog[slot];
+    N.ltag = (c - 1) << 4; N.mytag = c << 4;
+    N.perr = perr;
+    intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
     if (pst) st1 = wall_clock64();
-    if (qtype == MBT_I4x4) {   // the luma tile -> slot (I16x16 and chroma went there directly)
-        const int orow = lane >> 2, oq = lane & 3;
-        *(uint32_t *)&px[orow * 16 + oq * 4] = *(const uint32_t *)&M.ty[(orow + 1) * TY_STRIDE + TX0 + oq * 4];
-    }
-    wave_sync();
     if (pst && lane == 0) { pst[0] = st0; pst[1] = (st1 & 0xFFFFFFFFull) | (wall_clock64() << 32); }
 }
 
@@ -1825,7 +1856,11 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         // PROF stamp [3]: MC start in bits 0..31, flag set (slot final) in bits 32..63 (100 MHz)
         if (PROF && lane == 0)
             a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 3] = (t0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
-        if (lane == 0) lds_st(&R.flag[slot], c + 1);
+        if (lane == 0) {
+            lds_st(&R.lprog[slot], (c << 4) | 10);
+            lds_st(&R.cprog[slot], (c << 4) | 1);
+            lds_st(&R.flag[slot], c + 1);
+        }
         v0 = nv0;
         if (more && D.n) dep_wait(a, p, v0, lane, D);
         if (more) mc_issue(a, pd, p, r * a.w + c + NMC, v0, lane, ld);
@@ -1859,7 +1894,7 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
     const int j = jg / hg, g = jg - j * hg, p = j * S + s;
     for (int q = 0; q < RPW; q++) {
-        if (threadIdx.x < RK) R[q].flag[threadIdx.x] = 0;
+        if (threadIdx.x < RK) { R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1; }
         if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
     for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
