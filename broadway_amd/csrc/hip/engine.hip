@@ -257,6 +257,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     }
     a.epoch = e->epoch;
     a.prof = e->d_prof;
+    a.prof_mode = e->d_prof && getenv("H264MI_PROF_MODE") ? atoi(getenv("H264MI_PROF_MODE")) : 0;
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;

@@ -59,6 +59,10 @@ struct ReconArgs {
     // by row r's workgroup after its frame stores and an agent release)
     int P;
     unsigned int *done;
+    // profiling build only: 1 = the row waves only drain the MC ring (no
+    // deblocking, no stores) -- SQ counters of such a launch minus those of
+    // a normal one split the instruction counts by wave role (tools/sq_roles.py)
+    int prof_mode;
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -1209,6 +1213,18 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                        const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
     const int W = a.w, H = a.h;
+    if (PROF && a.prof_mode == 1) {     // role split (see ReconArgs::prof_mode): drain the ring only
+        if (w == 0)
+            for (int c = 0; c < W; c++) {
+                unsigned spins = 0;
+                while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[c & (RK - 1)])) != c + 1) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 22)) break;
+                }
+                if (lane == 0) lds_st(&R->consumed, c + 1);
+            }
+        return;
+    }
     const PicDesc *pdp = a.pics + p;
     const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
     const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);

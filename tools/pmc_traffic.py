@@ -33,6 +33,22 @@ def per_launch(path, counter):
     return {k: (sum(v) / len(v), len(v)) for k, v in d.items()}
 
 
+def calibration(src):
+    """FETCH_SIZE per kernel of tools/ubench/fetch_calib vs the bytes it reads
+    (printed by the program): factor = bytes / (FETCH_SIZE KiB * 1024)."""
+    log, cc = os.path.join(src, "calib.log"), os.path.join(src, "calib", "calib_counter_collection.csv")
+    if not (os.path.exists(log) and os.path.exists(cc)):
+        return None
+    want = {}
+    for line in open(log):
+        f = line.split()
+        if len(f) >= 3 and f[0].startswith("k_") and f[1] == "bytes":
+            want[f[0]] = int(f[2])
+    got = per_launch(cc, "FETCH_SIZE")
+    return {k: {"bytes": b, "FETCH_SIZE_KiB": round(got[k][0], 1), "factor": round(b / (got[k][0] * 1024), 3)}
+            for k, b in want.items() if k in got}
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
@@ -59,6 +75,10 @@ def main(tag):
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
                "hbm_bytes_per_step": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    cal = calibration(src)
+    if cal:
+        json.dump(cal, open(os.path.join(dst, f"{tag}_fetch_calib.json"), "w"), indent=1)
+        print(json.dumps(cal, indent=1))
     for extra in ("chain_s8.log", "chain_s1.log"):
         if os.path.exists(os.path.join(src, extra)):
             shutil.copy(os.path.join(src, extra), os.path.join(dst, f"{tag}_{extra}"))

@@ -50,7 +50,9 @@ hi = lambda x: (x >> np.uint64(32)).astype(np.int64)
 Cst = lo(m[..., 0])
 A, B = lo(m[..., 1]), hi(m[..., 1])
 E, D = lo(m[..., 2]), hi(m[..., 2])
-base = Cst[Cst > 0].min()
+# earliest stamp of the launch: the MC waves run ahead of the row chain
+m3 = lo(m[..., 3])
+base = min(Cst[Cst > 0].min(), m3[m3 > 0].min())
 us = lambda x: ((x - base) % (1 << 32)) / 100.0
 A, B, Cst, D, E = us(A), us(B), us(Cst), us(D), us(E)
 
@@ -115,7 +117,7 @@ print(f"  row 0 end (us, mean over pictures): {D[:, 0, w - 1].mean():.1f}; row {
 # column c+1 (mailbox dwords 24..31 through L2).
 M0, M1 = us(lo(m[..., 3])), us(hi(m[..., 3]))
 types = np.stack([np.frombuffer(caps[s].records_bytes(PIC), np.uint8).reshape(h, w, 96)[..., 0] for s in range(S)])
-intra = types >= 2
+intra = (types == 2) | (types == 3)     # I4x4 / I16x16 (I_PCM is a copy)
 print(f"MC: {intra.mean() * 100:.1f} % intra MBs; MC slot-final of row 0's last MB {M1[:, 0, w - 1].mean():.1f} us, "
       f"of row {h - 1}'s {M1[:, h - 1, w - 1].mean():.1f} us")
 rr, cc = slice(1, h), slice(1, w - 1)
@@ -137,19 +139,20 @@ nm = ~im
 if nm.any():
     st("inter MB MC (final - start)", (fin - own0)[nm])
 
-# inside mc_intra ([4]: left ready | top ready, [5]: prediction done | slot written)
+# inside mc_intra ([4]: top loads issued | top ready, [5]: intra_tile done
+# (left waits, prediction and slot writes, chroma first) | stamp written)
 L0, T0 = us(lo(m[..., 4])), us(hi(m[..., 4]))
-P0, W0 = us(lo(m[..., 5])), us(hi(m[..., 5]))
+P0 = us(lo(m[..., 5]))
 if im.any():
-    ok = im & (m[:, rr, cc, 4] != 0)
-    st("intra: top poll after left (top ready - left ready)", (T0 - L0)[:, rr, cc][ok])
-    st("intra: prediction (tile done - top ready)", (P0 - T0)[:, rr, cc][ok])
-    st("intra: tile -> slot copy", (W0 - P0)[:, rr, cc][ok])
-    st("intra: slot written -> flag (publish)", (M1 - W0)[:, rr, cc][ok])
-    st("intra: MC start -> left ready", (L0 - M0)[:, rr, cc][ok])
+    # stamps of this launch only (a stale stamp of an earlier launch predates base)
+    ok = im & (m[:, rr, cc, 4] != 0) & (L0[:, rr, cc] >= M0[:, rr, cc]) & (P0[:, rr, cc] <= M1[:, rr, cc])
+    st("intra: MC start -> top loads issued (residual, record)", (L0 - M0)[:, rr, cc][ok])
+    st("intra: top wait (top ready - loads issued)", (T0 - L0)[:, rr, cc][ok])
+    st("intra: intra_tile (left waits + prediction + slot writes)", (P0 - T0)[:, rr, cc][ok])
+    st("intra: tile done -> flag (bottom-row publish)", (M1 - P0)[:, rr, cc][ok])
     i4 = ok & (types[:, rr, cc] == 2)
     i16 = ok & (types[:, rr, cc] == 3)
     if i4.any():
-        st("  I4x4 prediction", (P0 - T0)[:, rr, cc][i4])
+        st("  I4x4 intra_tile", (P0 - T0)[:, rr, cc][i4])
     if i16.any():
-        st("  I16x16 prediction", (P0 - T0)[:, rr, cc][i16])
+        st("  I16x16 intra_tile", (P0 - T0)[:, rr, cc][i16])

@@ -5,6 +5,9 @@
 //   k_window  : 3 dwords per lane from rows of a 1920-wide plane (MC window
 //               pattern: 4 lanes per block row, blocks at pseudo-random spots)
 //   k_x4      : 16 B per lane streaming (the guide's calibrated case)
+//   k_x2      : 8 B per lane streaming (global_load_dwordx2: the mailbox
+//               granules {dword, epoch} and chroma MC rows)
+//   k_x3      : 12 B per lane streaming (global_load_dwordx3: luma MC rows)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -22,6 +25,27 @@ __global__ void k_x4(const uint4 *__restrict__ src, uint32_t *out, size_t n)
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const uint4 v = src[i];
         acc += v.x + v.y + v.z + v.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+__global__ void k_x2(const uint2 *__restrict__ src, uint32_t *out, size_t n)
+{
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint2 v = src[i];
+        acc += v.x + v.y;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// 12 B per lane: lane i of the grid reads bytes [12 i, 12 i + 12)
+__global__ void k_x3(const uint32_t *__restrict__ src, uint32_t *out, size_t n)
+{
+    uint32_t acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const uint3 v = *(const uint3 *)(src + 3 * i);
+        acc += v.x + v.y + v.z;
     }
     if (acc == 0x12345678u) out[0] = acc;
 }
@@ -48,17 +72,20 @@ int main()
 {
     const size_t bytes = 512ull << 20;
     uint8_t *buf; uint32_t *out;
-    hipMalloc(&buf, bytes); hipMalloc(&out, 4);
-    hipMemset(buf, 1, bytes);
-    hipDeviceSynchronize();
+    if (hipMalloc(&buf, bytes) != hipSuccess || hipMalloc(&out, 4) != hipSuccess) return 1;
+    if (hipMemset(buf, 1, bytes) != hipSuccess) return 1;
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
     hipLaunchKernelGGL(k_dword, dim3(8192), dim3(256), 0, 0, (const uint32_t *)buf, out, bytes / 4);
     hipLaunchKernelGGL(k_x4, dim3(8192), dim3(256), 0, 0, (const uint4 *)buf, out, bytes / 16);
+    hipLaunchKernelGGL(k_x2, dim3(8192), dim3(256), 0, 0, (const uint2 *)buf, out, bytes / 8);
+    const size_t n3 = bytes / 12;
+    hipLaunchKernelGGL(k_x3, dim3(8192), dim3(256), 0, 0, (const uint32_t *)buf, out, n3);
     // window: plane 1920 x (bytes / 1920) rows, multiple of 16
     const int W = 1920, H = (int)((bytes / W) / 16 * 16);
     const int ntiles = (W / 16) * (H / 16);   // 2654435761 is odd and ntiles = 120 * k: not a permutation in
                                               // general -> count distinct tiles on the host below
     hipLaunchKernelGGL(k_window, dim3(8192), dim3(256), 0, 0, (const uint8_t *)buf, out, W, H, ntiles);
-    hipDeviceSynchronize();
+    if (hipDeviceSynchronize() != hipSuccess) return 1;
     // distinct tiles touched by k_window
     uint8_t *seen = (uint8_t *)calloc(ntiles, 1);
     size_t distinct = 0;
@@ -66,6 +93,7 @@ int main()
         const int tt = (int)(((unsigned)t * 2654435761u) % (unsigned)ntiles);
         if (!seen[tt]) { seen[tt] = 1; distinct++; }
     }
+    printf("k_x2 bytes %zu\nk_x3 bytes %zu\n", bytes, n3 * 12);
     printf("k_dword bytes %zu\nk_x4 bytes %zu\nk_window bytes %zu (distinct tiles %zu of %d)\n", bytes, bytes,
            distinct * 256, distinct, ntiles);
     return 0;
