@@ -912,6 +912,11 @@ def main(argv=None):
             "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S * P,
                                    "steps_per_launch": P,
                                    "timed_launches": launches_timed,
+                                   # this run's k_wgpp dispatch indices (0-based, in
+                                   # rocprofv3 kernel-trace order): the timed window and
+                                   # the launches the HIP events sampled
+                                   "trace_window": [run.n_warm, len(run.launches)],
+                                   "trace_sampled": sampled,
                                    "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}},
             "p_only": p_only,
             "wall_read_GBs": round(frame_read_gbs, 2),

@@ -7,10 +7,11 @@
  * drop-in names for code written against OpenMAX DL; the decoder's own path
  * is the fused k_prep / k_wgpp kernels (include/h264mi.h).
  *
- * Not provided: the CAVLC parsers omxVCM4P10_DecodeCoeffsToPairCAVLC /
- * DecodeChromaDcCoeffsToPairCAVLC (bitstream parsing stays on the host,
- * csrc/common/cavlc.c), the encoder-side primitives (motion estimation,
- * SAD/SATD, forward transforms) and MPEG-4 part 2.
+ * The two CAVLC parsers (omxVCM4P10_DecodeCoeffsToPairCAVLC /
+ * DecodeChromaDcCoeffsToPairCAVLC) run on the host (csrc/host/omx_cavlc.c):
+ * bitstream parsing stays on the CPU in this design.  Not provided: the
+ * encoder-side primitives (motion estimation, SAD/SATD, forward transforms)
+ * and MPEG-4 part 2.
  *
  * Argument errors: every check of the reference is made before any output
  * is written (the reference's deblocking filters check bS / thresholds per
@@ -38,6 +39,7 @@ typedef struct { OMX_INT width; OMX_INT height; } OMXSize;
 
 enum {                           /* omxtypes.h:51-67 */
     H264MI_OMX_Sts_NoErr = 0,
+    H264MI_OMX_Sts_Err = -2,
     H264MI_OMX_Sts_BadArgErr = -5,
 };
 
@@ -46,6 +48,18 @@ enum {                           /* omxVC.h:516-525 availability bits */
     H264MI_OMX_VC_UPPER_LEFT = 32, H264MI_OMX_VC_UPPER_RIGHT = 64,
 };
 
+/* omxVC.h:3101 -- CAVLC ChromaDCLevel (2x2) -> packed position-coefficient
+ * pairs at *ppPosCoefbuf (advanced past them; untouched for an empty block) */
+OMXResult omxVCM4P10_DecodeChromaDcCoeffsToPairCAVLC(const OMX_U8 **ppBitStream, OMX_S32 *pOffset, OMX_U8 *pNumCoeff,
+                                                     OMX_U8 **ppPosCoefbuf);
+/* omxVC.h:3160 -- CAVLC 4x4 block (sMaxNumCoeff 15 or 16; sVLCSelect = nC >= 0) */
+OMXResult omxVCM4P10_DecodeCoeffsToPairCAVLC(const OMX_U8 **ppBitStream, OMX_S32 *pOffset, OMX_U8 *pNumCoeff,
+                                             OMX_U8 **ppPosCoefbuf, OMX_INT sVLCSelect, OMX_INT sMaxNumCoeff);
+/* diagnostic: 1 if this thread's last CAVLC call above returned
+ * H264MI_OMX_Sts_Err for a bit pattern the reference decodes by reading its
+ * tables out of range (TotalCoeff > sMaxNumCoeff, TotalCoeff + total_zeros >
+ * sMaxNumCoeff, run_before > zerosLeft: undefined behaviour there), else 0 */
+int h264mi_omx_cavlc_divergent(void);
 /* omxVC.h:2426 -- predMode OMXVCM4P10Intra4x4PredMode 0..8 (VERT, HOR, DC,
  * DIAG_DL, DIAG_DR, VR, HD, VL, HU) */
 OMXResult omxVCM4P10_PredictIntra_4x4(const OMX_U8 *pSrcLeft, const OMX_U8 *pSrcAbove, const OMX_U8 *pSrcAboveLeft,

@@ -175,6 +175,79 @@ def _luma_spec(src, x0, y0, step, w, h, dx, dy):
     return out.astype(np.uint8)
 
 
+# The same positions exist LP64-clean in the reference's h264bsd core
+# (h264bsdPredictSamples, h264bsd_reconstruct.c:1819-1950, built with the
+# reference decoder's sources into oracle/_ref/libh264bsdref.so): the numpy
+# restatement above is pinned to it on all 16 positions (CPU), and the GPU
+# primitive is compared with it directly (test_interpolate_luma_vs_h264bsd).
+BSD_SO = os.path.join(ROOT, "oracle", "_ref", "libh264bsdref.so")
+PARTS = ((16, 16), (16, 8), (8, 16), (8, 8), (8, 4), (4, 8), (4, 4))
+
+
+class _Image(C.Structure):      # h264bsd_image.h:45-55 (data, width / height in MBs, ...)
+    _fields_ = [("data", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("luma", C.c_void_p), ("cb", C.c_void_p), ("cr", C.c_void_p)]
+
+
+class _Mv(C.Structure):         # h264bsd_macroblock_layer.h:119-123
+    _fields_ = [("hor", C.c_int16), ("ver", C.c_int16)]
+
+
+@pytest.fixture(scope="module")
+def bsd():
+    if not os.path.exists(BSD_SO):
+        pytest.skip("oracle/_ref/libh264bsdref.so not built (needs /root/reference at build time)")
+    lib = C.CDLL(BSD_SO, mode=os.RTLD_LOCAL)
+    lib.h264bsdPredictSamples.argtypes = [C.c_void_p, C.POINTER(_Mv), C.POINTER(_Image)] + [C.c_uint32] * 6
+    lib.h264bsdPredictSamples.restype = None
+    return lib
+
+
+def _bsd_luma(bsd, pic, wmb, hmb, x0, y0, w, h, dx, dy):
+    """luma prediction of a w x h partition at integer (x0, y0) + (dx, dy) / 4"""
+    img = _Image(pic.ctypes.data, wmb, hmb, 0, 0, 0)
+    mv = _Mv(4 * x0 + dx, 4 * y0 + dy)
+    data = np.zeros(384, np.uint8)
+    bsd.h264bsdPredictSamples(data.ctypes.data, C.byref(mv), C.byref(img), 0, 0, 0, 0, w, h)
+    return data[:256].reshape(16, 16)[:h, :w]
+
+
+def test_luma_spec_restatement_pinned_to_h264bsd(bsd):
+    rng = np.random.default_rng(11)
+    wmb, hmb = 4, 4
+    W = 16 * wmb
+    pic = rng.integers(0, 256, W * 16 * hmb * 3 // 2, dtype=np.uint8)
+    for w, h in PARTS:
+        for dx in range(4):
+            for dy in range(4):
+                for _ in range(2):
+                    x0 = int(rng.integers(2, W - w - 3))
+                    y0 = int(rng.integers(2, 16 * hmb - h - 3))
+                    want = _bsd_luma(bsd, pic, wmb, hmb, x0, y0, w, h, dx, dy)
+                    got = _luma_spec(pic[:W * 16 * hmb], x0, y0, W, w, h, dx, dy)
+                    assert np.array_equal(got, want), (w, h, dx, dy, x0, y0)
+
+
+@pytest.mark.gpu
+def test_interpolate_luma_vs_h264bsd(libs, bsd):
+    ours, _ = libs
+    rng = np.random.default_rng(12)
+    wmb, hmb = 6, 4
+    W = 16 * wmb
+    for w, h in PARTS:
+        for dx in range(4):
+            for dy in range(4):
+                pic = rng.integers(0, 256, W * 16 * hmb * 3 // 2, dtype=np.uint8)
+                x0 = int(rng.integers(2, W - w - 3))
+                y0 = int(rng.integers(2, 16 * hmb - h - 3))
+                want = _bsd_luma(bsd, pic, wmb, hmb, x0, y0, w, h, dx, dy)
+                src = Buf(pic.size, data=pic)
+                dst = Buf(16 * 16)
+                assert ours.omxVCM4P10_InterpolateLuma(src.p(y0 * W + x0), W, dst.p(), 16, dx, dy, Size(w, h)) == 0
+                got = dst.a.reshape(16, 16)[:h, :w]
+                assert np.array_equal(got, want), (w, h, dx, dy, x0, y0)
+
+
 @pytest.mark.gpu
 def test_interpolate_luma_vs_reference(libs):
     ours, ref = libs

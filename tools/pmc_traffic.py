@@ -49,6 +49,32 @@ def calibration(src):
             for k, b in want.items() if k in got}
 
 
+def trace_window(src):
+    """k_wgpp durations of the bench's timed window in the rocprofv3 kernel
+    trace of the same command (bench line kernels.k_wgpp.trace_window /
+    trace_sampled: dispatch indices in trace order), beside the bench's own
+    HIP-event average"""
+    tr, bj = os.path.join(src, "prof", "bench_kernel_trace.csv"), os.path.join(src, "prof_bench.json")
+    if not (os.path.exists(tr) and os.path.exists(bj)):
+        return None
+    line = json.loads(open(bj).read().strip().splitlines()[-1])
+    k = line["kernels"]["k_wgpp"]
+    if "trace_window" not in k:
+        return None
+    rows = [r for r in csv.DictReader(open(tr)) if kname(r["Kernel_Name"]) == "k_wgpp"]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
+    a, b = k["trace_window"]
+    win = dur[a:b]
+    smp = [dur[i] for i in k["trace_sampled"] if i < len(dur)]
+    return {"k_wgpp_dispatches_in_trace": len(dur), "timed_window": [a, b],
+            "rocprof_timed_window_avg_us": round(sum(win) / max(len(win), 1), 2),
+            "rocprof_sampled_avg_us": round(sum(smp) / max(len(smp), 1), 2),
+            "bench_hip_event_avg_us": k["avg_launch_us"],
+            "note": "the stats CSV's k_wgpp average also counts pre-roll / warmup launches (IDR-heavy) "
+                    "and the P-only leg's; this is the timed window alone"}
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
@@ -75,6 +101,10 @@ def main(tag):
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
                "hbm_bytes_per_step": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    tw = trace_window(src)
+    if tw:
+        out["trace_window"] = tw
+        json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     cal = calibration(src)
     if cal:
         json.dump(cal, open(os.path.join(dst, f"{tag}_fetch_calib.json"), "w"), indent=1)
