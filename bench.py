@@ -513,6 +513,9 @@ class _DryEngine:
     def pointer_device(self, p):
         return self.alloc_dev.get(p, -1)
 
+    def hint_intra(self, *a):
+        pass
+
     def decode_device_steps(self, *a):
         self.launches += 1
 
@@ -609,6 +612,9 @@ class DeviceRun:
         k_prep runs in its tail workgroups."""
         S, P = self.S, self.P
         desc = self.d_desc + i * P * S * 32
+        # the launch's shape hint: does it hold an intra-heavy picture
+        self.eng.hint_intra(any(2 * self.caps[s].pictures[k].n_intra > self.nmbs
+                                for step in self.launches[i] for s, k in enumerate(step)))
         if i + 1 < len(self.launches):
             self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc,
                                          self.d_recs, self.d_coef, desc + P * S * 32)

@@ -140,6 +140,8 @@ def mi() -> C.CDLL:
     L.h264mi_engine_decode.restype = i32
     L.h264mi_engine_decode_device.argtypes = [vp, i32, vp, vp, vp]
     L.h264mi_engine_decode_device.restype = i32
+    L.h264mi_engine_hint_intra.argtypes = [vp, i32]
+    L.h264mi_engine_hint_intra.restype = i32
     L.h264mi_engine_decode_device_next.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.h264mi_engine_decode_device_next.restype = i32
     L.h264mi_engine_decode_device_steps.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp]

@@ -43,7 +43,8 @@ struct h264mi_engine {
     int prep_wgs;                      // tail workgroups per launch (H264MI_PREP_WGS, default 2048)
     unsigned long long rows_launched;
     int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
-    int mc_waves;                      // MC waves per row workgroup: 3, or 2 (H264MI_MC_WAVES, sizing study)
+    int mc_waves;                      // MC waves per row workgroup: 0 = per launch (below), 2 or 3 forced (H264MI_MC_WAVES)
+    int launch_intra;                  // next launch: 1 = has an intra-heavy picture, 0 = none, -1 = unknown
     int rpw_max;                       // MB rows per k_wgpp workgroup allowed by LDS, 1..3
     int rpw_env;                       // H264MI_RPW: fixed rows per workgroup (0: by batch size)
     int ncu;
@@ -154,14 +155,34 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
         const char *pa = getenv("H264MI_PREP_AT");
         e->prep_at_pct = pa ? atoi(pa) : 0;
         const char *mw = getenv("H264MI_MC_WAVES");
-        e->mc_waves = (mw && atoi(mw) == 2) ? 2 : 3;
+        e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
+        e->launch_intra = -1;
         const char *rp = getenv("H264MI_RPW");
         e->rpw_env = rp ? atoi(rp) : 0;
         if (e->rpw_env < 0 || e->rpw_env > 3) e->rpw_env = 0;
         // the group's LDS mailboxes (w * 256 B per inner row boundary) beside
         // the static LDS of its rows (regions, MC scratch, a RINGG-slot ring)
         // within the CU's 160 KB
-        const size_t row_lds = sizeof(PPLds) + (size_t)e->mc_waves * sizeof(McScratch) + sizeof(MbRing<RINGG>);
+        // k_wgpp's LDS is dynamic (WgppLds): allow every variant the CU's 160 KB
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 2>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
         e->rpw_max = e->mc_waves == 2 ? 2 : 3;
         while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * w_mbs * 256 + (size_t)e->rpw_max * row_lds > 156 * 1024)
             e->rpw_max--;
@@ -232,6 +253,22 @@ static int rows_per_wg(const h264mi_engine *e, int S)
     return rpw;
 }
 
+// MC waves per single-row workgroup, per launch.  Three MC waves make a
+// 5-wave workgroup, admitted 2 per CU (tools/ubench/census.hip): a 1080p
+// picture's rows 64..67 then wait ~180 us for a slot, but intra pictures,
+// whose MC is the critical path, need the third wave.  Two make a 4-wave
+// workgroup, 3 per CU, every row resident from the start; with the MC
+// urgency priority (recon_kernels.hip mc_row) P pictures gain (measured,
+// configs[3] P-only: 350 vs 355 us per launch; a launch with an I picture:
+// ~40 us slower).  So: 2 unless the launch holds an intra-heavy picture
+// (more than half its MBs intra) or its content is unknown.
+static int launch_nmc(const h264mi_engine *e, int rpw)
+{
+    if (e->mc_waves) return e->mc_waves;
+    if (rpw > 1) return 3;
+    return e->launch_intra == 0 ? 2 : 3;
+}
+
 static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, const int16_t *d_coef,
                         const PicDesc *d_pics, const MbRec *next_rec, const int16_t *next_coef,
                         const PicDesc *next_pics)
@@ -239,6 +276,11 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     const int npics = S * P;
     const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
     const int hb = e->prep_parity;
+    // study knob (H264MI_NO_TAIL_PREP=1): every batch's k_prep as its own
+    // launch in front of k_wgpp, none in the tail -- k_wgpp's time without
+    // the next batch's prep work beside the chain
+    static const bool no_tail = getenv("H264MI_NO_TAIL_PREP") && atoi(getenv("H264MI_NO_TAIL_PREP"));
+    if (no_tail) next_rec = nullptr, next_coef = nullptr, next_pics = nullptr;
     if (!(e->prepped_rec && e->prepped_rec == (const void *)d_rec && e->prepped_pics == (const void *)d_pics))
         if (launch_prep(e, npics, d_rec, d_coef, d_pics, hb)) return -1;
     ReconArgs a;
@@ -290,20 +332,25 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     e->last_kernel = "k_wgpp";
     const int rpw = rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
-    const size_t lmbx = (size_t)(rpw - 1) * e->w * 256;
+    const int nmc = launch_nmc(e, rpw);
+    e->launch_intra = -1;                     // a hint covers one launch
+    const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w) : WgppLds<2, 1>::bytes(e->w))
+                        : rpw == 3 ? WgppLds<3, 3>::bytes(e->w) : rpw == 2 ? WgppLds<3, 2>::bytes(e->w)
+                        : WgppLds<3, 1>::bytes(e->w);
     if (a.prof) {
         if (rec) (void)hipEventRecord(t0, e->st);
         if (rpw == 3) hipLaunchKernelGGL((k_wgpp<3, true, true, 3>), grid, dim3(960), lmbx, e->st, a);
         else if (rpw == 2) hipLaunchKernelGGL((k_wgpp<3, true, true, 2>), grid, dim3(640), lmbx, e->st, a);
-        else hipLaunchKernelGGL((k_wgpp<3, true, true, 1>), grid, dim3(320), 0, e->st, a);
+        else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, true, true, 1>), grid, dim3(256), lmbx, e->st, a);
+        else hipLaunchKernelGGL((k_wgpp<3, true, true, 1>), grid, dim3(320), lmbx, e->st, a);
         if (rec) (void)hipEventRecord(t2, e->st);
-    } else if (e->mc_waves == 2) {
+    } else if (nmc == 2) {
         // sizing study (H264MI_MC_WAVES=2): two MC waves per row workgroup
         if (rpw == 2)
             hipExtLaunchKernelGGL((k_wgpp<2, false, true, 2>), grid, dim3(512), lmbx, e->st, rec ? t0 : nullptr,
                                   rec ? t2 : nullptr, 0, a);
         else
-            hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1>), grid, dim3(256), 0, e->st, rec ? t0 : nullptr,
+            hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1>), grid, dim3(256), lmbx, e->st, rec ? t0 : nullptr,
                                   rec ? t2 : nullptr, 0, a);
     } else if (rpw == 3) {
         // the timing events ride on the kernel's own dispatch packet
@@ -314,7 +361,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         hipExtLaunchKernelGGL((k_wgpp<3, false, true, 2>), grid, dim3(640), lmbx, e->st, rec ? t0 : nullptr,
                               rec ? t2 : nullptr, 0, a);
     } else {
-        hipExtLaunchKernelGGL((k_wgpp<3, false, true, 1>), grid, dim3(320), 0, e->st, rec ? t0 : nullptr,
+        hipExtLaunchKernelGGL((k_wgpp<3, false, true, 1>), grid, dim3(320), lmbx, e->st, rec ? t0 : nullptr,
                               rec ? t2 : nullptr, 0, a);
     }
     HIPCHECK(hipGetLastError());
@@ -360,7 +407,25 @@ extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stre
     if (cbase) HIPCHECK(hipMemcpyAsync(e->d_coef, e->h_coef, cbase * 32, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipMemcpyAsync(e->d_pics, e->h_pics, sizeof(PicDesc) * npics, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipEventRecord(e->ev_staged, e->st));
+    // the batch's shape hint from its records (launch_nmc)
+    int heavy = 0;
+    for (int i = 0; i < npics && !heavy; i++) {
+        const MbRec *r = (const MbRec *)recs[i];
+        int n = 0;
+        for (int m = 0; m < e->nmbs; m++) n += r[m].type >= MBT_I4x4;
+        heavy = 2 * n > e->nmbs;
+    }
+    e->launch_intra = heavy;
     return launch_batch(e, npics, 1, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
+}
+
+// the next launch's content, for callers holding their records on the device
+// (launch_nmc): 1 = some picture has more than half its MBs intra, 0 = none
+extern "C" int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy)
+{
+    if (!e || intra_heavy < 0 || intra_heavy > 1) return -1;
+    e->launch_intra = intra_heavy;
+    return 0;
 }
 
 extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
@@ -393,6 +458,22 @@ extern "C" int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P,
     HIPCHECK(hipSetDevice(e->dev));
     return launch_batch(e, S, P, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
                         next_coef, (const PicDesc *)next_pics);
+}
+
+// diagnostics: resident k_wgpp workgroups per CU the runtime computes for
+// the main single-row kernel (rpw 1), and its kernel attributes
+extern "C" int h264mi_kernel_occupancy(int *blocks_per_cu, int *lds_bytes, int *vgprs, int *sgprs)
+{
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&k_wgpp<3, false, true, 1>)) != hipSuccess) return -1;
+    int n = 0;
+    const size_t lds = WgppLds<3, 1>::bytes(120);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wgpp<3, false, true, 1>, 320, lds) != hipSuccess) return -1;
+    if (blocks_per_cu) *blocks_per_cu = n;
+    if (lds_bytes) *lds_bytes = (int)(fa.sharedSizeBytes + lds);
+    if (vgprs) *vgprs = fa.numRegs;
+    if (sgprs) *sgprs = 0;
+    return 0;
 }
 
 extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)

@@ -1349,7 +1349,12 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     const bool prof = PROF && a.prof != nullptr;
     unsigned long long tc0 = 0, tc1, tva = 0, tvd = 0;
 #define PPT(i) do { if (prof) { tc1 = clock64(); pt[i] += tc1 - tc0; tc0 = tc1; } } while (0)
-    if (prof && w == 0 && lane == 0) a.prof[((size_t)r * a.npics + p) * 16] = wall_clock64();
+    if (prof && w == 0 && lane == 0) {
+        a.prof[((size_t)r * a.npics + p) * 16] = wall_clock64();
+        // placement: HW_REG_HW_ID (CU / SH / SE of this wave) and HW_REG_XCC_ID
+        a.prof[((size_t)r * a.npics + p) * 16 + 10] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        a.prof[((size_t)r * a.npics + p) * 16 + 11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
 
     for (int c = w; c < W; c += 2) {
         if (prof) tc0 = clock64();
@@ -1851,6 +1856,15 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             wave_sync();
         }
         const unsigned long long t0 = PROF ? wall_clock64() : 0;      // MB c's MC start (ring slot free)
+        if (NMC == 2) {
+            // urgency (2-MC-wave workgroups, 3 per CU): an MC wave whose row
+            // unit is within 8 MBs of it issues ahead of the MC waves of rows
+            // whose deblocking is far off -- the rows sharing a CU all start
+            // their MC at once, and the top rows' MC gates their chains
+            // (measured: P-only 350 vs 354 us per launch; 3 MC waves: slower)
+            if (c - __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < 8) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], Mw.res, R.db[slot]);
         if (type == MBT_IPCM) {
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
@@ -1888,15 +1902,42 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
 // to the next one through an LDS mailbox (dynamic shared memory, w * 256 B
 // per inner boundary) instead of an L2 round trip: (RPW - 1) / RPW of the
 // picture's row-to-row hand-offs become LDS ones.
+//
+// LDS: one dynamic block, [RPW regions | RPW * NMC MC scratch | RPW rings |
+// (RPW - 1) mailboxes], sized on the host by WgppLds::bytes.  Dynamic rather
+// than static so that the compiler's occupancy check, which reads only
+// static LDS, accepts any register budget (WGPP_WAVES_PER_EU).  Residency
+// (tools/ubench/census.hip): 320-thread (5-wave) workgroups are admitted 2
+// per CU at 117 VGPRs and 3 at 93; 256-thread ones 3 at 117.  A 1080p
+// picture's 68 rows on one XCD's 32 CUs need 3 per CU: with 3 MC waves
+// (5-wave workgroups, 128 VGPRs) rows 64..67 wait for a free slot (~180 us
+// into the launch); a 96-VGPR budget admits them but spills and slows every
+// MB (396 vs 366 us per launch), so that variant stays a build option.
+template <int NMC, int RPW>
+struct WgppLds {
+    static constexpr int RK = RPW == 1 ? RING1 : RINGG;
+    static constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+    static constexpr size_t offM = a16(sizeof(PPLds) * RPW);
+    static constexpr size_t offR = offM + a16(sizeof(McScratch) * RPW * NMC);
+    static constexpr size_t offX = offR + a16(sizeof(MbRing<RK>) * RPW);
+    static size_t bytes(int w) { return offX + (size_t)(RPW - 1) * w * 256; }
+};
+#ifndef WGPP_WAVES_PER_EU
+#define WGPP_WAVES_PER_EU 4
+#endif
+
 template <int NMC, bool PROF, bool PREP, int RPW>
-__global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_per_eu(NMC == 3 || RPW > 1 ? 4 : 3))) void k_wgpp(ReconArgs a)
+__global__ __launch_bounds__(64 * (NMC + 2) * RPW)
+__attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : 3))) void k_wgpp(ReconArgs a)
 {
-    __shared__ PPLds L[RPW];
-    __shared__ McScratch M[RPW * NMC];
-    constexpr int RK = RPW == 1 ? RING1 : RINGG;
+    using Lay = WgppLds<NMC, RPW>;
+    constexpr int RK = Lay::RK;
     static_assert(RK >= NMC * RPW, "tail workgroups use one ring db entry per wave as k_prep scratch");
-    __shared__ MbRing<RK> R[RPW];
-    extern __shared__ unsigned long long lmbx[];
+    extern __shared__ __attribute__((aligned(16))) unsigned char wg_lds[];
+    PPLds *const L = (PPLds *)wg_lds;
+    McScratch *const M = (McScratch *)(wg_lds + Lay::offM);
+    MbRing<RK> *const R = (MbRing<RK> *)(wg_lds + Lay::offR);
+    unsigned long long *const lmbx = (unsigned long long *)(wg_lds + Lay::offX);
     const int S = a.S;
     const int hg = (a.h + RPW - 1) / RPW;
     // blockIdx = (j * hg + g) * S + s: step j's pictures (one per stream)
@@ -1922,6 +1963,8 @@ __global__ __launch_bounds__(64 * (NMC + 2) * RPW) __attribute__((amdgpu_waves_p
     const int q = RPW == 1 ? 0 : wid0 / (NMC + 2), wid = wid0 - q * (NMC + 2);
     const int r = g * RPW + q;
     if (r >= a.h) return;
+    if (PROF && RPW == 1 && wid0 >= 1 && lane == 0)    // placement of waves 1..4 (wave 0: row_pp)
+        a.prof[((size_t)r * a.npics + p) * 16 + 11 + wid0] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     const size_t W32 = (size_t)a.w * 32;
     // mailboxes: the group's first row reads the row above from L2, its last
     // row publishes there; inner boundaries use lmbx[(q - 1) * W32 ..]
@@ -1966,4 +2009,5 @@ template __global__ void k_wgpp<3, false, true, 2>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 2>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 3>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 2>(ReconArgs);
+template __global__ void k_wgpp<2, true, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 3>(ReconArgs);

@@ -107,6 +107,12 @@ class Engine:
                                                     n_recs, n_coef, n_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device_next failed")
 
+    def hint_intra(self, intra_heavy: bool) -> None:
+        """Shape hint for the next device-resident launch: does some picture
+        have more than half its MBs intra (include/h264mi.h)."""
+        if self._L.h264mi_engine_hint_intra(self._h, int(bool(intra_heavy))) != 0:
+            raise RuntimeError("h264mi_engine_hint_intra failed")
+
     def set_steps(self, steps: int) -> None:
         """Pictures per stream per launch for decode_device_steps (1..2)."""
         if self._L.h264mi_engine_set_steps(self._h, steps) != 0:

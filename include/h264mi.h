@@ -170,6 +170,15 @@ void h264mi_engine_destroy(h264mi_engine *e);
 int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
                          const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef);
 
+/* Shape hint for the next launch of a device-resident batch (the host path,
+ * h264mi_engine_decode, derives it from the records itself): 1 if some picture
+ * of the batch has more than half its MBs intra, 0 if none.  P-picture
+ * launches then run 4-wave row workgroups (2 MC waves, every MB row resident
+ * at once), intra-heavy ones 5-wave workgroups (3 MC waves); without a hint
+ * the launch uses 3.  A hint covers one launch.  Returns 0, or -1 on a bad
+ * argument. */
+int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy);
+
 /* Device-resident variant (records already in HBM; kernel-only timing):
  * d_recs = npics*w*h MbRec in batch order with coefficient offsets relative
  * to d_coef, d_pics = npics PicDesc. */

@@ -101,13 +101,17 @@ def test_decoder_js_api_holds_reordered_pictures():
     assert 0 < len(got) < len(c["frames"]) and got == c["frames"][:len(got)]
 
 
-@pytest.mark.parametrize("rpw", [None, "1", "2", "3"])
-def test_engine_multistream_batch_vs_oracle_replay(rpw, monkeypatch):
+@pytest.mark.parametrize("rpw,mc", [(None, None), ("1", None), ("2", None), ("3", None), (None, "2"), (None, "3"),
+                                    ("2", "2")])
+def test_engine_multistream_batch_vs_oracle_replay(rpw, mc, monkeypatch):
     """4 streams per launch vs the oracle replay; rpw: k_wgpp rows per
     workgroup forced (H264MI_RPW; 7 rows leave a partial last group), None =
-    the engine's choice by batch size."""
+    the engine's choice by batch size; mc: MC waves per row forced
+    (H264MI_MC_WAVES), None = per launch by intra share."""
     if rpw:
         monkeypatch.setenv("H264MI_RPW", rpw)
+    if mc:
+        monkeypatch.setenv("H264MI_MC_WAVES", mc)
     streams = [gen.generate(2, 40 + i, nframes=6, w_mbs=10, h_mbs=7, crop_bottom=0, slices=2, gop=4)
                for i in range(4)]
     caps = [Capture(s) for s in streams]
@@ -127,13 +131,17 @@ def test_engine_multistream_batch_vs_oracle_replay(rpw, monkeypatch):
     assert eng.errors() == 0
 
 
-@pytest.mark.parametrize("rpw", [None, "3"])
-def test_engine_bench_streams_vs_reference(rpw, monkeypatch):
+@pytest.mark.parametrize("rpw,mc", [(None, None), (None, "2"), (None, "3"), ("3", None)])
+def test_engine_bench_streams_vs_reference(rpw, mc, monkeypatch):
     """The bench workload (configs[3]: 8 concurrent 1080p streams, one picture
     of each per launch), 12 pictures, every frame vs the reference MD5s; also
-    with three MB rows per k_wgpp workgroup (the large-batch layout)."""
+    with three MB rows per k_wgpp workgroup (the large-batch layout), and with
+    the row workgroup's MC waves forced to 2 or 3 for every launch (mc None:
+    per launch, 3 for the IDR launch, 2 for the P launches)."""
     if rpw:
         monkeypatch.setenv("H264MI_RPW", rpw)
+    if mc:
+        monkeypatch.setenv("H264MI_MC_WAVES", mc)
     names = [f"bench_1080p_s{s}" for s in range(100, 108)]
     caps = []
     for n in names:

@@ -93,7 +93,9 @@ for r0, r1 in ((1, 4), (4, 8), (8, 24), (24, 48), (48, h - 1)):
     tp = (Cst[:, r0:r1, cols] - B[:, r0:r1, cols])
     g = tp > 0.05
     dl = (Cst[:, r0:r1, cols] - E[:, r0 - 1:r1 - 1, cols])[g]
-    print(f"  rows {r0:2d}..{r1 - 1:2d}: period mean {pr.mean():.3f} p50 {np.percentile(pr, 50):.3f}"
+    # row lag: H start of MB 2 of row r minus that of row r-1 (the wavefront's slope)
+    lag = (Cst[:, r0:r1, 2] - Cst[:, r0 - 1:r1 - 1, 2]).mean()
+    print(f"  rows {r0:2d}..{r1 - 1:2d}: lag {lag:.2f} | period mean {pr.mean():.3f} p50 {np.percentile(pr, 50):.3f}"
           f" | top mean {tp.mean():.3f} | delta mean {dl.mean() if dl.size else 0:.3f}"
           f" p90 {np.percentile(dl, 90) if dl.size else 0:.3f} | gated {g.mean() * 100:.0f} %")
 print("deep rows by column band:")
@@ -156,3 +158,35 @@ if im.any():
         st("  I4x4 intra_tile", (P0 - T0)[:, rr, cc][i4])
     if i16.any():
         st("  I16x16 intra_tile", (P0 - T0)[:, rr, cc][i16])
+
+if os.environ.get("PROF_ROWS"):
+    # per row, mean over pictures (us): MC start of MB 0, MC final of MB 2,
+    # V(2) start, H(2) start, the row above's entry 2 published, last MB's H end
+    print("row   mc0.start  mc2.final   V2.start   H2.start  above.E2   lag  rowend")
+    for r in range(1, h):
+        print(f"{r:3d} {M0[:, r, 0].mean():10.1f} {M1[:, r, 2].mean():10.1f} {A[:, r, 2].mean():10.1f}"
+              f" {Cst[:, r, 2].mean():10.1f} {E[:, r - 1, 2].mean():9.1f} {(Cst[:, r, 2] - Cst[:, r - 1, 2]).mean():5.2f}"
+              f" {D[:, r, w - 1].mean():7.1f}")
+
+if os.environ.get("PROF_ROWS"):
+    # placement of each row's workgroup: XCC, SE, SH, CU (HW_REG_HW_ID / XCC_ID)
+    rw = np.frombuffer(buf, dtype=np.uint64)[:S * h * 16].reshape(h, S, 16)
+    hwid, xcc = rw[..., 10].astype(np.int64), rw[..., 11].astype(np.int64) & 15
+    cu, sh, se = (hwid >> 8) & 15, (hwid >> 12) & 1, (hwid >> 13) & 7
+    print("picture 0 rows: xcc/se/sh/cu")
+    print(" ".join(f"{r}:{xcc[r, 0]}/{se[r, 0]}/{sh[r, 0]}/{cu[r, 0]}" for r in range(h)))
+    print("xcc per picture:", [sorted(set(xcc[:, s].tolist())) for s in range(S)])
+    import collections
+    for s in range(min(S, 2)):
+        cnt = collections.Counter((int(se[r, s]), int(sh[r, s]), int(cu[r, s])) for r in range(h))
+        print(f"picture {s}: {len(cnt)} distinct CUs, rows per CU {sorted(collections.Counter(cnt.values()).items())}")
+
+if os.environ.get("PROF_ROWS"):
+    # SIMD of each of the 5 waves of the workgroups sharing a CU (picture 0)
+    simd = lambda v: (v >> 4) & 3
+    by_cu = collections.defaultdict(list)
+    for r in range(h):
+        by_cu[(int(se[r, 0]), int(sh[r, 0]), int(cu[r, 0]))].append(r)
+    for k, rs in list(by_cu.items())[:8]:
+        print("CU", k, " ".join(f"row {r}: simd " + ",".join(str(int(simd(rw[r, 0, i]))) for i in (10, 12, 13, 14, 15))
+                                for r in rs))
