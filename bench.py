@@ -367,7 +367,8 @@ def end_to_end(streams, nframes, reps=3):
     every output picture.  Rate = all pictures / the slowest process's decode
     time (HIP start-up of each process excluded; it is paid before its timed
     loop)."""
-    exe = os.path.join(ROOT, "broadway_amd", "lib", "h264mi_dec")
+    from broadway_amd import _lib
+    exe = os.path.join(_lib.LIB_DIR, "h264mi_dec")      # H264MI_LIB_DIR: an A/B build's
     if not os.path.exists(exe):
         return None
     streams = streams[:MAX_E2E_PROCS]

@@ -20,7 +20,29 @@ typedef struct {
     size_t   pos;       /* bit position */
     size_t   end_bits;  /* position of rbsp_stop_one_bit (exclusive end of data) */
     int      err;       /* set when reading past the end */
+    /* read cache: the 64 bits from bit cbase (a byte boundary), MSB first;
+     * pos stays the reader's state, the cache only saves re-reading bytes */
+    uint64_t cache;
+    size_t   cbase;
 } BitReader;
+
+/* the 8 bytes at byte (zero past the end) into the cache */
+static inline void br_refill_(BitReader *br)
+{
+    const size_t byte = br->pos >> 3;
+    uint64_t v = 0;
+    if (byte + 8 <= br->size) {
+        memcpy(&v, br->buf + byte, 8);
+        v = __builtin_bswap64(v);
+    } else {
+        for (int i = 0; i < 8; i++) {
+            v <<= 8;
+            if (byte + i < br->size) v |= br->buf[byte + i];
+        }
+    }
+    br->cache = v;
+    br->cbase = byte << 3;
+}
 
 static inline void br_init(BitReader *br, const uint8_t *buf, size_t size)
 {
@@ -38,26 +60,21 @@ static inline void br_init(BitReader *br, const uint8_t *buf, size_t size)
         int tz = __builtin_ctz(b);
         br->end_bits = (n - 1) * 8 + (7 - tz);
     }
+    br_refill_(br);
 }
 
-/* peek up to 32 bits (zero-padded past the end) */
-static inline uint32_t br_peek(const BitReader *br, int n)
+/* peek up to 32 bits (zero-padded past the end).  Logically const: only the
+ * cache moves. */
+static inline uint32_t br_peek(const BitReader *cbr, int n)
 {
     if (n == 0) return 0;
-    size_t byte = br->pos >> 3;
-    int sh = (int)(br->pos & 7);
-    uint64_t v = 0;
-    if (byte + 8 <= br->size) {
-        memcpy(&v, br->buf + byte, 8);
-        v = __builtin_bswap64(v);
-    } else {
-        for (int i = 0; i < 8; i++) {
-            v <<= 8;
-            if (byte + i < br->size) v |= br->buf[byte + i];
-        }
+    BitReader *br = (BitReader *)cbr;
+    size_t off = br->pos - br->cbase;
+    if (off + (size_t)n > 64) {        /* also pos < cbase: off wraps to a huge value */
+        br_refill_(br);
+        off = br->pos & 7;
     }
-    v <<= sh;
-    return (uint32_t)(v >> (64 - n));
+    return (uint32_t)((br->cache << off) >> (64 - n));
 }
 
 static inline void br_skip(BitReader *br, int n)

@@ -24,23 +24,25 @@ int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, ui
 
     int level[16];
     int suffix_len = (tc > 10 && t1 < 3) ? 1 : 0;
-    for (int i = 0; i < tc; i++) {
-        if (i < t1) {
-            level[i] = br_u1(br) ? -1 : 1;
-            ++*abs_sum;
-            continue;
-        }
-        /* level_prefix: leading zero bits then a one (§9.2.2.1) */
-        uint32_t p = br_peek(br, 16);
-        if (p == 0) return -1;                   /* level_prefix > 15 */
-        int prefix = __builtin_clz(p) - 16;
-        br_skip(br, prefix + 1);
-        int code = (prefix < 15 ? prefix : 15) << suffix_len;
+    int i = 0;
+    if (t1) {                                    /* trailing_ones_sign_flags, one read */
+        const uint32_t sg = br_u(br, t1);
+        for (; i < t1; i++) level[i] = ((sg >> (t1 - 1 - i)) & 1) ? -1 : 1;
+        *abs_sum += (uint32_t)t1;
+    }
+    for (; i < tc; i++) {
+        /* level_prefix (leading zero bits then a one, §9.2.2.1) and
+         * level_suffix from one 32-bit window: prefix <= 15, suffix <= 12 */
+        const uint32_t w = br_peek(br, 32);
+        if ((w >> 16) == 0) return -1;           /* level_prefix > 15 */
+        const int prefix = __builtin_clz(w);
         int ssize = suffix_len;
         if (prefix == 14 && suffix_len == 0) ssize = 4;
-        if (prefix >= 15) ssize = prefix - 3;
-        if (ssize > 0) code += (int)br_u(br, ssize);
-        if (prefix >= 15 && suffix_len == 0) code += 15;
+        if (prefix == 15) ssize = 12;
+        int code = prefix << suffix_len;
+        if (ssize > 0) code += (int)((w << (prefix + 1)) >> (32 - ssize));
+        br_skip(br, prefix + 1 + ssize);
+        if (prefix == 15 && suffix_len == 0) code += 15;
         if (i == t1 && t1 < 3) code += 2;
         int lv = (code & 1) ? (-code - 1) >> 1 : (code + 2) >> 1;
         level[i] = lv;

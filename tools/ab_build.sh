@@ -8,13 +8,13 @@ OUT=$ROOT/abtest/$NAME
 mkdir -p "$OUT"
 if [ "$REV" = "-" ]; then
   make -s -C "$ROOT/broadway_amd/csrc"
-  cp "$ROOT"/broadway_amd/lib/*.so "$OUT/"
+  cp "$ROOT"/broadway_amd/lib/*.so "$ROOT"/broadway_amd/lib/h264mi_dec "$OUT/"
 else
   TMP=$(mktemp -d)
   git -C "$ROOT" archive "$REV" broadway_amd/csrc include bindings | tar -x -C "$TMP"
   mkdir -p "$TMP/broadway_amd/lib"
   make -s -C "$TMP/broadway_amd/csrc" -j8
-  cp "$TMP"/broadway_amd/lib/*.so "$OUT/"
+  cp "$TMP"/broadway_amd/lib/*.so "$TMP"/broadway_amd/lib/h264mi_dec "$OUT/"
   rm -rf "$TMP"
 fi
 ls -la "$OUT"
