@@ -1126,11 +1126,17 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     // 32 entry c+1 dword 24 (C), 33..35 entry c-1 dwords 27/29/31 (D).  The
     // loads are issued before the wait for the left MB, so their L2 round
     // trip overlaps it; re-polled only if some granule is still stale
-    const bool need_top = has_up && (aB || aC || aD);
+    // the above-right MB (C) is read by one prediction only: I4x4 block 5
+    // in Diagonal_Down_Left or Vertical_Left (8.3.1.2.4 / .7); every other MB
+    // skips its granule, so the MC chain of the row below waits on MB c of
+    // this row, not c + 1 (the wavefront's slope: one in-row step per row)
+    const int m5 = (int)(i4 >> 20) & 15;
+    const bool needC = aC && qtype == MBT_I4x4 && (m5 == 3 || m5 == 7);
+    const bool need_top = has_up && (aB || needC || aD);
     const int dsel = lane == 32 ? 1 : (lane > 32 && lane < 36) ? -1 : 0;
     const int dw = lane < 32 ? (lane & 31) : lane == 32 ? 24 : lane < 36 ? 27 + 2 * (lane - 33) : 24;
     const unsigned long long *g = mbx_up + min(max(c + dsel, 0), W - 1) * 32 + dw;
-    const bool mine = need_top && ((lane >= 24 && lane < 32 && aB) || (lane == 32 && aC) || (lane >= 33 && lane < 36 && aD));
+    const bool mine = need_top && ((lane >= 24 && lane < 32 && aB) || (lane == 32 && needC) || (lane >= 33 && lane < 36 && aD));
     unsigned long long gr = need_top ? ld_granT<UPL>(g) : 0ull;
     if (pst) st0 = wall_clock64();
     if (need_top) {
@@ -1149,7 +1155,7 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
             const int k = lane - 24;
             if (aB) *(uint32_t *)(k < 4 ? &M.ty[TX0 + k * 4] : k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
         } else if (lane == 32) {
-            if (aC) *(uint32_t *)&M.ty[TX0 + 16] = top;
+            if (needC) *(uint32_t *)&M.ty[TX0 + 16] = top;
         } else if (lane < 36) {
             if (aD) (lane == 33 ? M.ty[TX0 - 1] : lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
         }
