@@ -4,9 +4,11 @@
 // one launch reconstructs one picture from each stream of the batch).
 #include "recon_kernels.hip"
 #include "color.hip"
+#include "conceal.hip"
 #include <hip/hip_ext.h>
 
 #include <stdio.h>
+#include <atomic>
 #include <stdlib.h>
 #include <string.h>
 #include "../../../include/h264mi.h"
@@ -40,6 +42,10 @@ struct h264mi_engine {
     int prep_parity;
     const void *prepped_rec, *prepped_pics;
     unsigned long long *d_rows_done;   // row workgroups finished, all launches (tail-prep trigger)
+    // k_conceal inputs (order + decoded flags): pinned staging, device copy,
+    // and an event after the upload (the staging's reuse waits for it)
+    uint8_t *h_conceal, *d_conceal;
+    hipEvent_t ev_conceal;
     int prep_wgs;                      // tail workgroups per launch (H264MI_PREP_WGS, default 2048)
     unsigned long long rows_launched;
     int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
@@ -210,6 +216,9 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
     (void)hipFree(e->d_rows_done);
+    if (e->h_conceal) (void)hipHostFree(e->h_conceal);
+    if (e->d_conceal) (void)hipFree(e->d_conceal);
+    if (e->ev_conceal) (void)hipEventDestroy(e->ev_conceal);
     h264mi_engine_set_timing(e, 0);
     if (e->st) (void)hipStreamDestroy(e->st);
     free(e);
@@ -644,6 +653,44 @@ extern "C" void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot)
 
 extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? e->frame_bytes : 0; }
 
+// neighbour-based concealment of a picture's missing MBs on the device
+// (k_conceal, conceal.hip), behind the work already on the engine's stream:
+// slot `slot` of stream `stream` holds the decoded MBs reconstructed with the
+// loop filter off; order[0..n) are the MBs to conceal in h264bsdConceal's
+// order, decoded[0..w*h) the MBs decoded (1) or missing (0).  The inputs are
+// copied before returning.
+static std::atomic<unsigned long long> g_conceal_launches{0};
+// diagnostics: k_conceal launches in this process (tests: the device path ran)
+extern "C" unsigned long long h264mi_conceal_launches(void) { return g_conceal_launches.load(); }
+
+extern "C" int h264mi_engine_conceal(h264mi_engine *e, int stream, int slot, const int *order, int n,
+                                     const uint8_t *decoded)
+{
+    if (!e || stream < 0 || stream >= e->nstreams || slot < 0 || slot >= e->nslots || n < 0 || n > e->nmbs ||
+        (n && (!order || !decoded)))
+        return -1;
+    if (!n) return 0;
+    for (int i = 0; i < n; i++) if (order[i] < 0 || order[i] >= e->nmbs) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    const size_t bytes = (size_t)e->nmbs * (sizeof(int) + 1);
+    if (!e->d_conceal) {
+        HIPCHECK(hipMalloc(&e->d_conceal, bytes));
+        HIPCHECK(hipHostMalloc(&e->h_conceal, bytes, hipHostMallocDefault));
+        HIPCHECK(hipEventCreateWithFlags(&e->ev_conceal, hipEventDisableTiming));
+    } else {
+        HIPCHECK(hipEventSynchronize(e->ev_conceal));
+    }
+    memcpy(e->h_conceal, order, sizeof(int) * (size_t)n);
+    memcpy(e->h_conceal + sizeof(int) * (size_t)e->nmbs, decoded, (size_t)e->nmbs);
+    HIPCHECK(hipMemcpyAsync(e->d_conceal, e->h_conceal, bytes, hipMemcpyHostToDevice, e->st));
+    HIPCHECK(hipEventRecord(e->ev_conceal, e->st));
+    hipLaunchKernelGGL(k_conceal, dim3(1), dim3(64), (size_t)e->nmbs, e->st, (uint8_t *)h264mi_engine_frame_ptr(e, stream, slot),
+                       e->w, e->h, (const int *)e->d_conceal, n, (const uint8_t *)(e->d_conceal + sizeof(int) * (size_t)e->nmbs));
+    HIPCHECK(hipGetLastError());
+    g_conceal_launches++;
+    return 0;
+}
+
 extern "C" void *h264mi_device_alloc(size_t bytes)
 {
     void *p = NULL;
@@ -1029,6 +1076,19 @@ static void *hb_host_alloc(void *vctx, size_t bytes)
 
 static void hb_host_free(void *vctx, void *p) { (void)hipHostFree(p); }
 
+static int hb_conceal(void *vctx, int slot, const int *order, int n, const uint8_t *decoded)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    if (slot >= 0 && slot < c->nslots) c->pref[slot] = NULL;
+    if (c->sh) {
+        std::lock_guard<std::mutex> l(c->sh->mu);
+        if (h264mi_engine_conceal(c->e, c->lane, slot, order, n, decoded)) return -1;
+        HIPCHECK(hipEventRecord(c->ev_last, c->e->st));
+        return 0;
+    }
+    return h264mi_engine_conceal(c->e, c->lane, slot, order, n, decoded);
+}
+
 static int hb_copy(void *vctx, int dst, int src)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
@@ -1095,6 +1155,8 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     be.host_alloc = hb_host_alloc;
     be.host_free = hb_host_free;
     be.copy = hb_copy;
+    // H264MI_HOST_CONCEAL=1: conceal on the host (a copy of the picture, conceal.c)
+    be.conceal = getenv("H264MI_HOST_CONCEAL") && atoi(getenv("H264MI_HOST_CONCEAL")) ? NULL : hb_conceal;
     be.sync = hb_sync;
     be.prefetch = hb_prefetch;
     be.destroy = hb_destroy;

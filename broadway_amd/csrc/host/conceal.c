@@ -197,10 +197,11 @@ int h264dec_conceal(H264Dec *d, int is_i)
     }
 
     /* neighbour-based: pass 1 reconstructs the decoded MBs unfiltered */
+    const int on_backend = d->be.conceal != NULL;
     uint8_t *saved = (uint8_t *)malloc((size_t)nmbs);
-    uint8_t *img = (uint8_t *)malloc(d->frame_bytes);
+    uint8_t *img = on_backend ? NULL : (uint8_t *)malloc(d->frame_bytes);
     uint32_t grey = 0;
-    if (!saved || !img || pcm_alloc(pb, &grey)) { free(saved); free(img); return -1; }
+    if (!saved || (!on_backend && !img) || pcm_alloc(pb, &grey)) { free(saved); free(img); return -1; }
     memset(pb->coef + (size_t)grey * 16, 128, 384);
     for (int i = 0; i < nmbs; i++) {
         saved[i] = pb->rec[i].avail;
@@ -208,7 +209,7 @@ int h264dec_conceal(H264Dec *d, int is_i)
         else pb->rec[i].avail &= (uint8_t)~(DB_LEFT | DB_TOP | DB_INNER);
     }
     int rc = d->be.decode(d->be.ctx, pb, d->cur_slot);
-    if (!rc) rc = d->be.read(d->be.ctx, d->cur_slot, img) < 0 ? -1 : 0;
+    if (!rc && !on_backend) rc = d->be.read(d->be.ctx, d->cur_slot, img) < 0 ? -1 : 0;
     for (int i = 0; i < nmbs; i++) if (pb->decoded[i]) pb->rec[i].avail = saved[i];
     free(saved);
     if (rc) { free(img); return -1; }
@@ -222,6 +223,21 @@ int h264dec_conceal(H264Dec *d, int is_i)
     for (int j = col + 1; j < w; j++) if (!dec[row * w + j]) order[n++] = row * w + j;
     for (int j = 0; j < w; j++) for (int i = row - 1; i >= 0; i--) order[n++] = i * w + j;
     for (int i = row + 1; i < h; i++) for (int j = 0; j < w; j++) if (!dec[i * w + j]) order[n++] = i * w + j;
+    if (on_backend) {
+        /* the backend conceals in place (k_conceal); pass 2 copies each
+         * concealed MB from the slot itself (zero-vector skip records read
+         * only the MB's own samples, which nothing else writes before) and
+         * filters it as intra */
+        if (d->be.conceal(d->be.ctx, d->cur_slot, order, n, dec)) { free(order); return -1; }
+        for (int k = 0; k < n; k++) {
+            const int mb = order[k];
+            copy_record(&pb->rec[mb], d->cur_slot);
+            conceal_fields(&pb->rec[mb], w, mb);
+            dec[mb] = 1;
+        }
+        free(order);
+        return n;
+    }
     for (int k = 0; k < n; k++) {
         const int mb = order[k];
         conceal_mb_intra(img, w, h, mb / w, mb % w, dec);

@@ -35,6 +35,11 @@ typedef struct H264Backend {
     void (*host_free)(void *ctx, void *p);
     /* copy one slot into another (error concealment of lost pictures) */
     int  (*copy)(void *ctx, int dst_slot, int src_slot);
+    /* optional: neighbour-based concealment on the backend, in place on slot
+     * (holding the decoded MBs reconstructed with the loop filter off), of
+     * the MBs order[0..n) in that order; decoded = the w*h decoded flags.
+     * NULL: the host conceals a copy of the picture (conceal.c) */
+    int  (*conceal)(void *ctx, int slot, const int *order, int n, const uint8_t *decoded);
     /* optional: wait for the reconstructions issued so far (timing split of
      * the output path into device wait and copy) */
     int  (*sync)(void *ctx);

@@ -179,6 +179,19 @@ int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const i
  * argument. */
 int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy);
 
+/* Neighbour-based error concealment on the device (ConcealMb's intra branch,
+ * h264bsd_conceal.c:337-579, replaces the host pass over a copy of the
+ * picture): the MBs order[0..n) of stream `stream`'s slot `slot` -- which holds
+ * the picture's decoded MBs reconstructed with the loop filter off -- are
+ * concealed in place in that order, behind the work already queued;
+ * decoded[0..w*h) flags the decoded MBs.  Inputs are copied before return.
+ * 0, or -1 on a bad argument / HIP error.  The H264SwDec* path uses it for I
+ * pictures with lost MBs (H264MI_HOST_CONCEAL=1: the host path instead). */
+int h264mi_engine_conceal(h264mi_engine *e, int stream, int slot, const int *order, int n,
+                          const uint8_t *decoded);
+/* diagnostics: k_conceal launches in this process */
+unsigned long long h264mi_conceal_launches(void);
+
 /* Device-resident variant (records already in HBM; kernel-only timing):
  * d_recs = npics*w*h MbRec in batch order with coefficient offsets relative
  * to d_coef, d_pics = npics PicDesc. */

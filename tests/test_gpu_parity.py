@@ -77,6 +77,29 @@ def test_swdec_degenerate_shapes_vs_reference(rpw, monkeypatch):
 PICS = [n for n in CASES if "pics" in CASES[n]]
 
 
+def test_device_concealment_runs_and_matches_the_host_path(monkeypatch):
+    """Neighbour-based concealment of I pictures with lost MBs runs on the
+    device (k_conceal, h264mi_engine_conceal) by default, and the host path
+    (H264MI_HOST_CONCEAL=1, a copy of the picture concealed on the CPU) gives
+    the same pictures: both equal the reference decoder's."""
+    L = _lib.mi()
+    L.h264mi_conceal_launches.restype = C.c_ulonglong
+    names = [n for n in PICS if n.startswith("err_")]
+    before = L.h264mi_conceal_launches()
+    for n in names:
+        c = CASES[n]
+        frames, _ = swdec_decode(stream(c), no_reorder=c["no_reorder"])
+        assert md5s(frames) == c["frames"], n
+    assert L.h264mi_conceal_launches() > before, "no damaged stream took the device concealment path"
+    monkeypatch.setenv("H264MI_HOST_CONCEAL", "1")
+    before = L.h264mi_conceal_launches()
+    for n in names:
+        c = CASES[n]
+        frames, _ = swdec_decode(stream(c), no_reorder=c["no_reorder"])
+        assert md5s(frames) == c["frames"], n
+    assert L.h264mi_conceal_launches() == before
+
+
 @pytest.mark.parametrize("name", PICS)
 def test_swdec_damaged_and_refpic_streams_vs_reference(name):
     """Through H264SwDec* on the GPU, every output picture, picture id, IDR

@@ -97,7 +97,7 @@ def main(tag):
     # (the pipeline's first step) is spread over them
     step /= kernels[step_kernels[0]]["launches"]
     out = {"tag": tag, "kernels": kernels, "hbm_bytes_per_step": int(step),
-           "note": "FETCH_SIZE doubled per the gfx950 correction (calibrated for 16-B/lane streaming reads)"}
+           "note": "FETCH_SIZE doubled per the gfx950 correction; the factor 2.0 is measured for this kernel's 4-, 8-, 12- and 16-B per-lane loads (tools/ubench/fetch_calib.hip, profiles/r34_fetch_calib.json)"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
                "hbm_bytes_per_step": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
