@@ -190,3 +190,11 @@ if os.environ.get("PROF_ROWS"):
     for k, rs in list(by_cu.items())[:8]:
         print("CU", k, " ".join(f"row {r}: simd " + ",".join(str(int(simd(rw[r, 0, i]))) for i in (10, 12, 13, 14, 15))
                                 for r in rs))
+
+if os.environ.get("PROF_ROW0"):
+    # row r's MC and deblocking per MB, mean over pictures (us): MC start /
+    # final, V start (A), H end (D); MB types of picture 0
+    r0 = int(os.environ.get("PROF_ROW0"))
+    print(f"row {r0}: c type  mc.start  mc.final  V.start  H.end")
+    for c in range(w):
+        print(f"{c:3d} {int(types[0, r0, c]):2d} {M0[:, r0, c].mean():8.1f} {M1[:, r0, c].mean():8.1f} {A[:, r0, c].mean():8.1f} {D[:, r0, c].mean():8.1f}")
