@@ -784,7 +784,11 @@ struct SharedEng {
     HipBackendCtx *who[SHARE_MAX];
     bool force[SHARE_MAX];                // test hook: start this picture with a device flag set
     unsigned long long collecting, launched;   // batch ids: collecting > launched while np > 0
-    int rc;                               // result of the last launch
+    // result of each launch, by batch id: a waiter whose batch was launched
+    // by another thread reads its own batch's entry, however many batches
+    // launched before it got the lock back
+#define SHARE_RC_RING 64
+    int rc_ring[SHARE_RC_RING];
 };
 static std::mutex g_share_mu;
 #define SHARE_SIZES 4                     // shared engines per device, one per picture size
@@ -844,15 +848,16 @@ static void share_launch(SharedEng *sh)
     h264mi_engine *e = sh->e;
     for (int i = 0; i < sh->np; i++)
         if (sh->force[i]) (void)hipMemsetAsync(e->d_err + i, 0x01, sizeof(unsigned), e->st);
-    sh->rc = h264mi_engine_decode(e, sh->np, sh->stream, sh->slot, sh->recs, sh->coefs, sh->nc);
+    int rc = h264mi_engine_decode(e, sh->np, sh->stream, sh->slot, sh->recs, sh->coefs, sh->nc);
     // each picture's device flags (ReconArgs::err, one word per batch
     // picture) into its instance's word for the slot it was reconstructed
     // into, then cleared for the next batch
-    for (int i = 0; i < sh->np && sh->rc == 0; i++)
+    for (int i = 0; i < sh->np && rc == 0; i++)
         if (hipMemcpyAsync(sh->who[i]->h_slot_err + sh->slot[i], e->d_err + i, sizeof(unsigned),
                            hipMemcpyDeviceToHost, e->st) != hipSuccess)
-            sh->rc = -1;
-    if (hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * sh->np, e->st) != hipSuccess) sh->rc = -1;
+            rc = -1;
+    if (hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * sh->np, e->st) != hipSuccess) rc = -1;
+    sh->rc_ring[sh->collecting % SHARE_RC_RING] = rc;
     for (int i = 0; i < sh->np; i++) (void)hipEventRecord(sh->who[i]->ev_last, e->st);
     g_share_batches[sh->device] += 1;
     g_share_pictures[sh->device] += (unsigned long long)sh->np;
@@ -907,7 +912,7 @@ static int share_attach(HipBackendCtx *c, int w_mbs, int h_mbs, int nslots)
         if (!e) return -1;
         sh = new SharedEng();
         sh->device = c->device; sh->w = w_mbs; sh->h = h_mbs; sh->lanes = lanes; sh->e = e;
-        sh->used = 0; sh->active = 0; sh->np = 0; sh->collecting = 1; sh->launched = 0; sh->rc = 0;
+        sh->used = 0; sh->active = 0; sh->np = 0; sh->collecting = 1; sh->launched = 0;
         g_share[c->device][free_k] = sh;
     }
     std::lock_guard<std::mutex> l(sh->mu);
@@ -981,7 +986,9 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
     } else if (!sh->cv.wait_for(l, std::chrono::microseconds(g_share_wait_us), [&] { return sh->launched >= mine; })) {
         share_launch(sh);                 // the others are late: launch what is there
     }
-    return sh->rc;
+    // (a waiter gets the lock back long before SHARE_RC_RING more batches
+    // launch: each later batch takes a picture or a 1 ms wait of another instance)
+    return sh->rc_ring[mine % SHARE_RC_RING];
 }
 
 static int hb_prefetch(void *vctx, int slot, uint8_t *dst)
