@@ -6,7 +6,7 @@
 
 #include <stdlib.h>
 
-int mbctx_neighbour(const PicCtx *pc, int cur, int n)
+static int neighbour_of(const PicCtx *pc, int cur, int n)
 {
     int w = pc->w;
     int col = cur % w;
@@ -20,6 +20,19 @@ int mbctx_neighbour(const PicCtx *pc, int cur, int n)
     if (a < 0) return -1;
     if (pc->mb[a].slice != pc->mb[cur].slice) return -1;
     return a;
+}
+
+int mbctx_neighbour(const PicCtx *pc, int cur, int n)
+{
+    if (pc->nb_key == cur + 1) return pc->nb[n];
+    return neighbour_of(pc, cur, n);
+}
+
+void mbctx_begin_mb(PicCtx *pc, int cur)
+{
+    pc->nb_key = 0;
+    for (int n = 0; n < 4; n++) pc->nb[n] = neighbour_of(pc, cur, n);
+    pc->nb_key = cur + 1;
 }
 
 /* locate 4x4 block at (x4,y4) relative to MB cur (x4 in -1..4, y4 in -1..3) */

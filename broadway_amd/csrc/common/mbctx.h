@@ -30,6 +30,11 @@ typedef struct PicCtx {
     int      w, h;        /* picture size in MBs */
     int      cip;         /* constrained_intra_pred_flag */
     MbInfo  *mb;          /* w*h entries */
+    /* neighbour cache of the MB being parsed (mbctx_begin_mb): nb[n] is
+     * mbctx_neighbour(cur, n) while nb_key == cur + 1 (0: no cache; a
+     * zero-initialised context has none) */
+    int      nb_key;
+    int      nb[4];
 } PicCtx;
 
 enum { NB_A = 0, NB_B = 1, NB_C = 2, NB_D = 3 };
@@ -39,6 +44,11 @@ static inline int mb_is_intra(const MbInfo *m) { return m->type >= 2; }
 /* address of neighbour MB n of `cur`, or -1 when not available (outside the
  * picture or in another slice) */
 int mbctx_neighbour(const PicCtx *pc, int cur, int n);
+/* the parser's MB loop: cache the four neighbours of cur once its slice tag
+ * is set (every derivation below asks for them several times per MB), and
+ * drop the cache when the MB is done (mbctx_end_mb) */
+void mbctx_begin_mb(PicCtx *pc, int cur);
+static inline void mbctx_end_mb(PicCtx *pc) { pc->nb_key = 0; }
 
 /* nC for luma block `blk` (z-scan) of MB cur */
 int mbctx_nc_luma(const PicCtx *pc, int cur, int blk);

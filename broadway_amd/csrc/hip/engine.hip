@@ -66,6 +66,7 @@ struct h264mi_engine {
     unsigned *h_err;
     hipStream_t st;
     hipEvent_t ev_staged, ev0, ev1, ev2;
+    hipEvent_t ev_block;      // H264MI_BLOCKING_SYNC: h264mi_engine_sync sleeps on this event
     uint32_t err_accum;
     int timing;
     // per-batch kernel timing (h264mi_engine_set_timing): event triples
@@ -108,6 +109,52 @@ static int alloc_pic_buffers(h264mi_engine *e, int cap)
     return 0;
 }
 
+// settings read from the environment at engine creation (and again when a
+// pooled engine is taken for a new decoder instance)
+static void engine_config(h264mi_engine *e)
+{
+    e->timing = getenv("H264MI_TIMING") != NULL;
+    const char *pw = getenv("H264MI_PREP_WGS");
+    e->prep_wgs = pw && atoi(pw) > 0 ? atoi(pw) : 2048;
+    const char *pa = getenv("H264MI_PREP_AT");
+    e->prep_at_pct = pa ? atoi(pa) : 0;
+    const char *mw = getenv("H264MI_MC_WAVES");
+    e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
+    e->launch_intra = -1;
+    const char *rp = getenv("H264MI_RPW");
+    e->rpw_env = rp ? atoi(rp) : 0;
+    if (e->rpw_env < 0 || e->rpw_env > 3) e->rpw_env = 0;
+    // the group's LDS mailboxes (w * 256 B per inner row boundary) beside
+    // the static LDS of its rows (regions, MC scratch, a RINGG-slot ring)
+    // within the CU's 160 KB
+    // k_wgpp's LDS is dynamic (WgppLds): allow every variant the CU's 160 KB
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 3>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 3>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
+    e->rpw_max = e->mc_waves == 2 ? 2 : 3;
+    while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * e->w * 256 + (size_t)e->rpw_max * row_lds > 156 * 1024)
+        e->rpw_max--;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev) != hipSuccess || ncu < 1) ncu = 256;
+    e->ncu = ncu;
+}
+
 extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
 {
     if (w_mbs < 1 || h_mbs < 1 || h_mbs > 1024 || nstreams < 1 || nslots < 1) return NULL;
@@ -119,8 +166,8 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     if (hipSetDevice(device) != hipSuccess) return NULL;
     // H264MI_BLOCKING_SYNC=1: a thread waiting for the GPU sleeps instead of
     // spinning (many decoder processes with parse threads on few host cores)
-    if (getenv("H264MI_BLOCKING_SYNC") && atoi(getenv("H264MI_BLOCKING_SYNC")))
-        (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
+    const bool blocking = getenv("H264MI_BLOCKING_SYNC") && atoi(getenv("H264MI_BLOCKING_SYNC"));
+    if (blocking) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
     h264mi_engine *e = (h264mi_engine *)calloc(1, sizeof(h264mi_engine));
     if (!e) return NULL;
     e->dev = device;
@@ -130,7 +177,6 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->frame_bytes = (size_t)e->nmbs * 384;
     e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
     e->h_coef_cap = e->coef_cap;
-    e->timing = getenv("H264MI_TIMING") != NULL;
     bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
 
               hipMalloc(&e->d_rec, sizeof(MbRec) * nstreams * e->nmbs) == hipSuccess &&
@@ -143,9 +189,10 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
               hipHostMalloc(&e->h_pics, sizeof(PicDesc) * nstreams, hipHostMallocDefault) == hipSuccess &&
 
               hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking) == hipSuccess &&
-              hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_staged, hipEventDisableTiming | (blocking ? hipEventBlockingSync : 0)) == hipSuccess &&
               hipEventCreate(&e->ev0) == hipSuccess && hipEventCreate(&e->ev1) == hipSuccess &&
               hipEventCreate(&e->ev2) == hipSuccess &&
+              (!blocking || hipEventCreateWithFlags(&e->ev_block, hipEventDisableTiming | hipEventBlockingSync) == hipSuccess) &&
               hipMalloc(&e->d_rows_done, sizeof(unsigned long long)) == hipSuccess;
     ok = ok && alloc_pic_buffers(e, nstreams) == 0;
     if (!ok) {
@@ -155,47 +202,7 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     }
     (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * nslots * nstreams, e->st);
     (void)hipMemsetAsync(e->d_rows_done, 0, sizeof(unsigned long long), e->st);
-    {
-        const char *pw = getenv("H264MI_PREP_WGS");
-        e->prep_wgs = pw && atoi(pw) > 0 ? atoi(pw) : 2048;
-        const char *pa = getenv("H264MI_PREP_AT");
-        e->prep_at_pct = pa ? atoi(pa) : 0;
-        const char *mw = getenv("H264MI_MC_WAVES");
-        e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
-        e->launch_intra = -1;
-        const char *rp = getenv("H264MI_RPW");
-        e->rpw_env = rp ? atoi(rp) : 0;
-        if (e->rpw_env < 0 || e->rpw_env > 3) e->rpw_env = 0;
-        // the group's LDS mailboxes (w * 256 B per inner row boundary) beside
-        // the static LDS of its rows (regions, MC scratch, a RINGG-slot ring)
-        // within the CU's 160 KB
-        // k_wgpp's LDS is dynamic (WgppLds): allow every variant the CU's 160 KB
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 1>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 1>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 2>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 2>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 3>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, true, true, 3>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 2>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
-        e->rpw_max = e->mc_waves == 2 ? 2 : 3;
-        while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * w_mbs * 256 + (size_t)e->rpw_max * row_lds > 156 * 1024)
-            e->rpw_max--;
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
-        e->ncu = ncu;
-    }
+    engine_config(e);
     e->epoch = 0;
     (void)hipEventRecord(e->ev_staged, e->st);
     (void)hipStreamSynchronize(e->st);
@@ -215,6 +222,7 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->ev2) (void)hipEventDestroy(e->ev2);
+    if (e->ev_block) (void)hipEventDestroy(e->ev_block);
     (void)hipFree(e->d_rows_done);
     if (e->h_conceal) (void)hipHostFree(e->h_conceal);
     if (e->d_conceal) (void)hipFree(e->d_conceal);
@@ -222,6 +230,62 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
     h264mi_engine_set_timing(e, 0);
     if (e->st) (void)hipStreamDestroy(e->st);
     free(e);
+}
+
+// Released private engines, kept for the next decoder instance of the same
+// shape: DecTestBench-style callers create one H264SwDec instance per stream
+// (H264SwDecInit ... H264SwDecRelease), and a fresh engine costs ~20 device
+// and pinned allocations, a stream, events and a frame clear.  A pooled
+// engine is idle (its stream drained) and is handed out as a fresh one would
+// be: frames cleared, no batch prepped, settings re-read.  H264MI_ENGINE_POOL=0
+// turns it off.
+#include <mutex>
+#define ENGINE_POOL_MAX 4
+static std::mutex g_pool_mu;
+static h264mi_engine *g_pool[ENGINE_POOL_MAX];
+
+static bool engine_pool_on()
+{
+    const char *v = getenv("H264MI_ENGINE_POOL");
+    return !v || atoi(v) != 0;
+}
+
+static h264mi_engine *engine_get(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
+{
+    h264mi_engine *e = NULL;
+    if (engine_pool_on()) {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (int i = 0; i < ENGINE_POOL_MAX && !e; i++) {
+            h264mi_engine *x = g_pool[i];
+            if (x && x->dev == device && x->w == w_mbs && x->h == h_mbs && x->nstreams == nstreams && x->nslots == nslots) {
+                e = x;
+                g_pool[i] = NULL;
+            }
+        }
+    }
+    if (!e) return h264mi_engine_create(device, w_mbs, h_mbs, nstreams, nslots);
+    if (hipSetDevice(device) != hipSuccess) { h264mi_engine_destroy(e); return NULL; }
+    engine_config(e);
+    e->prepped_rec = e->prepped_pics = NULL;
+    e->err_accum = 0;
+    e->steps = 1;
+    e->last_kernel = NULL;
+    // the epoch keeps counting: the mailboxes hold tags of earlier launches only
+    (void)hipMemsetAsync(e->d_frames, 0, e->frame_bytes * e->nslots * e->nstreams, e->st);
+    return e;
+}
+
+static void engine_put(h264mi_engine *e)
+{
+    if (!e) return;
+    // engines with diagnostics state (timing events, profiling buffers) are not kept
+    if (engine_pool_on() && !e->tev && !e->d_prof && hipSetDevice(e->dev) == hipSuccess &&
+        hipStreamSynchronize(e->st) == hipSuccess) {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (int i = 0; i < ENGINE_POOL_MAX; i++)
+            if (!g_pool[i]) { g_pool[i] = e; return; }
+    }
+    h264mi_engine_destroy(e);
 }
 
 // k_prep of a batch as its own launch (the batch was not prepped by the
@@ -381,8 +445,21 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     return 0;
 }
 
+// intra_heavy: the batch's launch shape hint when the caller knows it (the
+// host path counts intra MBs while parsing); -1: derive it from the records
+static int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
+                              const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef,
+                              int intra_heavy);
+
 extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
                                     const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef)
+{
+    return engine_decode_host(e, npics, stream, cur_slot, recs, coefs, ncoef, -1);
+}
+
+static int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
+                              const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef,
+                              int intra_heavy)
 {
     if (!e || npics < 1 || npics > e->nstreams) return -1;
     HIPCHECK(hipSetDevice(e->dev));
@@ -417,8 +494,8 @@ extern "C" int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stre
     HIPCHECK(hipMemcpyAsync(e->d_pics, e->h_pics, sizeof(PicDesc) * npics, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipEventRecord(e->ev_staged, e->st));
     // the batch's shape hint from its records (launch_nmc)
-    int heavy = 0;
-    for (int i = 0; i < npics && !heavy; i++) {
+    int heavy = intra_heavy > 0;
+    for (int i = 0; i < npics && !heavy && intra_heavy < 0; i++) {
         const MbRec *r = (const MbRec *)recs[i];
         int n = 0;
         for (int m = 0; m < e->nmbs; m++) n += r[m].type >= MBT_I4x4;
@@ -514,7 +591,15 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     // picture slots
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * e->pipe_cap, hipMemcpyDeviceToHost, e->st));
     HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * e->pipe_cap, e->st));
-    HIPCHECK(hipStreamSynchronize(e->st));
+    if (e->ev_block) {
+        // a blocking-sync event: the waiting thread sleeps whatever the
+        // device's scheduling flags (set once per process, before the first
+        // context, or not at all)
+        HIPCHECK(hipEventRecord(e->ev_block, e->st));
+        HIPCHECK(hipEventSynchronize(e->ev_block));
+    } else {
+        HIPCHECK(hipStreamSynchronize(e->st));
+    }
     for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
     return 0;
 }
@@ -783,6 +868,7 @@ struct SharedEng {
     uint32_t nc[SHARE_MAX];
     HipBackendCtx *who[SHARE_MAX];
     bool force[SHARE_MAX];                // test hook: start this picture with a device flag set
+    bool heavy[SHARE_MAX];                // more than half the picture's MBs intra (launch_nmc)
     unsigned long long collecting, launched;   // batch ids: collecting > launched while np > 0
     // result of each launch, by batch id: a waiter whose batch was launched
     // by another thread reads its own batch's entry, however many batches
@@ -848,7 +934,9 @@ static void share_launch(SharedEng *sh)
     h264mi_engine *e = sh->e;
     for (int i = 0; i < sh->np; i++)
         if (sh->force[i]) (void)hipMemsetAsync(e->d_err + i, 0x01, sizeof(unsigned), e->st);
-    int rc = h264mi_engine_decode(e, sh->np, sh->stream, sh->slot, sh->recs, sh->coefs, sh->nc);
+    bool heavy = false;
+    for (int i = 0; i < sh->np; i++) heavy |= sh->heavy[i];
+    int rc = engine_decode_host(e, sh->np, sh->stream, sh->slot, sh->recs, sh->coefs, sh->nc, heavy ? 1 : 0);
     // each picture's device flags (ReconArgs::err, one word per batch
     // picture) into its instance's word for the slot it was reconstructed
     // into, then cleared for the next batch
@@ -933,7 +1021,7 @@ static int hb_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
     if (c->sh) share_detach(c);
-    else if (c->e) h264mi_engine_destroy(c->e);
+    else if (c->e) engine_put(c->e);
     c->e = NULL;
     free(c->pref);
     (void)hipHostFree(c->h_slot_err);
@@ -948,7 +1036,7 @@ static int hb_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
     memset(c->h_slot_err, 0, sizeof(unsigned) * (nslots > 0 ? nslots : 1));
     if (share_attach(c, w_mbs, h_mbs, nslots) != 0) {
         c->lane = 0;
-        c->e = h264mi_engine_create(c->device, w_mbs, h_mbs, 1, nslots);
+        c->e = engine_get(c->device, w_mbs, h_mbs, 1, nslots);
     }
     return c->e && c->pref ? 0 : -1;
 }
@@ -966,7 +1054,7 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
         const int16_t *coefs[1] = {pb->coef};
         uint32_t nc[1] = {pb->ncoef};
         h264mi_engine *e = c->e;
-        if (h264mi_engine_decode(e, 1, &stream, &cur_slot, recs, coefs, nc)) return -1;
+        if (engine_decode_host(e, 1, &stream, &cur_slot, recs, coefs, nc, 2 * (int)pb->n_intra > pb->nmbs)) return -1;
         // the picture's device flags into the slot's word, behind its launch
         if (cur_slot < 0 || cur_slot >= c->nslots) return -1;
         HIPCHECK(hipMemcpyAsync(c->h_slot_err + cur_slot, e->d_err, sizeof(unsigned), hipMemcpyDeviceToHost, e->st));
@@ -980,6 +1068,7 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
     sh->recs[i] = pb->rec; sh->coefs[i] = pb->coef; sh->nc[i] = pb->ncoef;
     sh->who[i] = c;
     sh->force[i] = force;
+    sh->heavy[i] = 2 * (int)pb->n_intra > pb->nmbs;
     const unsigned long long mine = sh->collecting;
     if (sh->np >= sh->active) {
         share_launch(sh);
@@ -1075,13 +1164,45 @@ static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
     return slot_flagged(c, slot, false);
 }
 
+// Pinned host blocks (decoder output frames) kept after free for the next
+// decoder instance: pinning tens of MB per instance is a large share of a
+// short stream's host time.  Exact-size reuse, at most HOST_POOL_BYTES kept.
+#define HOST_POOL_N 16
+#define HOST_POOL_BYTES (1ull << 30)
+static std::mutex g_hpool_mu;
+static struct { void *p; size_t bytes; } g_hpool[HOST_POOL_N], g_hlive[4 * HOST_POOL_N];
+
 static void *hb_host_alloc(void *vctx, size_t bytes)
 {
     void *p = NULL;
-    return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : NULL;
+    {
+        std::lock_guard<std::mutex> g(g_hpool_mu);
+        for (int i = 0; i < HOST_POOL_N && !p; i++)
+            if (g_hpool[i].p && g_hpool[i].bytes == bytes) { p = g_hpool[i].p; g_hpool[i].p = NULL; }
+    }
+    if (!p && hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return NULL;
+    std::lock_guard<std::mutex> g(g_hpool_mu);
+    for (int i = 0; i < 4 * HOST_POOL_N; i++)
+        if (!g_hlive[i].p) { g_hlive[i].p = p; g_hlive[i].bytes = bytes; break; }
+    return p;
 }
 
-static void hb_host_free(void *vctx, void *p) { (void)hipHostFree(p); }
+static void hb_host_free(void *vctx, void *p)
+{
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_hpool_mu);
+        size_t bytes = 0;
+        for (int i = 0; i < 4 * HOST_POOL_N; i++)
+            if (g_hlive[i].p == p) { bytes = g_hlive[i].bytes; g_hlive[i].p = NULL; break; }
+        size_t kept = 0;
+        for (int i = 0; i < HOST_POOL_N; i++) kept += g_hpool[i].p ? g_hpool[i].bytes : 0;
+        if (bytes && engine_pool_on() && kept + bytes <= HOST_POOL_BYTES)
+            for (int i = 0; i < HOST_POOL_N; i++)
+                if (!g_hpool[i].p) { g_hpool[i].p = p; g_hpool[i].bytes = bytes; return; }
+    }
+    (void)hipHostFree(p);
+}
 
 static int hb_conceal(void *vctx, int slot, const int *order, int n, const uint8_t *decoded)
 {
@@ -1117,7 +1238,7 @@ static void hb_destroy(void *vctx)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
     if (c->sh) share_detach(c);
-    else if (c->e) h264mi_engine_destroy(c->e);
+    else if (c->e) engine_put(c->e);
     free(c->pref);
     (void)hipHostFree(c->h_slot_err);
     free(c);

@@ -32,6 +32,7 @@ typedef struct PicBuild {
 int  picbuild_init(PicBuild *pb, int w_mbs, int h_mbs);
 void picbuild_free(PicBuild *pb);
 void picbuild_reset(PicBuild *pb, int cip);      /* start of a new picture */
+void picbuild_reuse(PicBuild *pb, int cip);      /* the next slice into a private PicBuild (slice ids count on) */
 
 /* Parse the slice_data() of one slice (reader positioned after the header).
  * ref_slot[i] = DPB slot of RefPicList0[i] (-1 if absent).  The slice gets

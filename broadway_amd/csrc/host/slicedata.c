@@ -14,6 +14,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+static void picbuild_reset_counts(PicBuild *pb, int cip);
+
 int picbuild_init(PicBuild *pb, int w_mbs, int h_mbs)
 {
     memset(pb, 0, sizeof(*pb));
@@ -34,10 +36,30 @@ void picbuild_free(PicBuild *pb)
     pb->rec = NULL; pb->pc.mb = NULL; pb->coef = NULL; pb->decoded = NULL;
 }
 
+/* a private PicBuild that receives one slice at a time (specparse.c): the
+ * slice ids keep counting up instead of every MB's id being cleared, so an
+ * MB left from an earlier slice never carries the new slice's id (neighbours
+ * outside the slice stay unavailable); a full reset only when the ids wrap */
+void picbuild_reuse(PicBuild *pb, int cip)
+{
+    const int n = pb->nslices;
+    if (n >= SLICE_NONE - 2) {
+        picbuild_reset(pb, cip);
+        return;
+    }
+    picbuild_reset_counts(pb, cip);
+    pb->nslices = n;
+}
+
 void picbuild_reset(PicBuild *pb, int cip)
 {
     /* h264bsdResetStorage (storage.c:442-462): no MB decoded, no slice id */
     for (int i = 0; i < pb->nmbs; i++) pb->pc.mb[i].slice = SLICE_NONE;
+    picbuild_reset_counts(pb, cip);
+}
+
+static void picbuild_reset_counts(PicBuild *pb, int cip)
+{
     memset(pb->decoded, 0, (size_t)pb->nmbs);
     pb->last_mb_addr = 0;
     pb->pc.cip = cip;
@@ -403,8 +425,17 @@ static void failed_mb(PicBuild *pb, int cur)
     pb->decoded[cur] = 1;
 }
 
+static int slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps *pps, const int *ref_slot);
+
 int parse_slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps *pps,
                      const int *ref_slot)
+{
+    const int r = slice_data(pb, br, sh, pps, ref_slot);
+    mbctx_end_mb(&pb->pc);      /* the neighbour cache lives for one MB of this slice only */
+    return r;
+}
+
+static int slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps *pps, const int *ref_slot)
 {
     int cur = sh->first_mb;
     int qp = sh->slice_qp;
@@ -421,6 +452,7 @@ int parse_slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps 
                 if (pb->decoded[cur]) return -1;      /* primary picture, already decoded */
                 memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
                 pb->pc.mb[cur].slice = tag;
+                mbctx_begin_mb(&pb->pc, cur);
                 pb->mb_decode_err = 0;
                 decode_skip(pb, cur, qp, ref_slot);
                 finish_rec(pb, cur, sh, pps, tag);
@@ -437,6 +469,7 @@ int parse_slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps 
         if (pb->decoded[cur]) return -1;
         memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
         pb->pc.mb[cur].slice = tag;                   /* SetMbParams precedes the parse */
+        mbctx_begin_mb(&pb->pc, cur);
         pb->mb_decode_err = 0;
         if (parse_mb(pb, br, cur, sh, pps, ref_slot, &qp)) return -1;
         finish_rec(pb, cur, sh, pps, tag);

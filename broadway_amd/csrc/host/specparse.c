@@ -97,9 +97,10 @@ static void run_job(SpecPool *sp, SpecJob *j)
         if (j->pb_ready) picbuild_free(&j->pb);
         j->pb_ready = 0;
         if (picbuild_init(&j->pb, sp->w, sp->h)) return;
+        picbuild_reset(&j->pb, sp->cip);
         j->pb_ready = 1;
     }
-    picbuild_reset(&j->pb, sp->cip);
+    picbuild_reuse(&j->pb, sp->cip);
     j->pb.cur_slot = sp->cur_slot;
     if (parse_slice_data(&j->pb, &br, &j->sh, &sp->pps, j->ref_slot)) return;
     j->ok = 1;

@@ -174,6 +174,7 @@ int main(int argc, char **argv)
         const double cpu = (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) + 1e-6 * (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) +
                            (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec);
         printf("cpu_seconds %.6f\n", cpu);
+        printf("cpu_sys_seconds %.6f\n", (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec));
         unsigned long long nb = 0, np = 0;
         h264mi_share_stats(0, &nb, &np);
         if (share) printf("share_batches %llu\nshare_pictures %llu\n", nb, np);
