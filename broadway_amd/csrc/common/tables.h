@@ -59,7 +59,19 @@ extern VlcTable gTotalZerosDcDec[3];
 extern VlcTable gRunBeforeDec[7];
 
 void h264_tables_init(void);   /* idempotent, thread-safe */
-int  vlc_decode(const VlcTable *t, uint32_t peek16, int *len);  /* returns sym or -1 */
+/* returns sym or -1; inline: the CAVLC decode calls it several times per
+ * coded block */
+static inline int vlc_decode(const VlcTable *t, uint32_t peek16, int *len)
+{
+    const uint32_t hi = (peek16 >> 8) & 0xFF;
+    int s = t->sym[hi];
+    if (s >= 0) { *len = t->len[hi]; return s; }
+    if (s == -1) { *len = 0; return -1; }
+    const int sub = -(s + 2);
+    const uint32_t lo = peek16 & 0xFF;
+    *len = t->sub_len[sub][lo];
+    return t->sub_sym[sub][lo];
+}
 
 static inline int coeff_token_class(int nC)
 {

@@ -333,11 +333,14 @@ static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint
     if (!dst && q->ncoef) return 0;
     if (q->ncoef) memcpy(dst, q->coef, (size_t)q->ncoef * 32);
     const uint16_t tag = (uint16_t)++pb->nslices;
+    /* of the neighbour state (MbInfo) later code reads only the slice id of
+     * MBs in other slices: neighbours across a slice boundary are unavailable
+     * (mbctx_neighbour), and un-marking / concealment look at ids and
+     * decoded flags */
     for (int i = first; i < first + count; i++) {
         pb->rec[i] = q->rec[i];
         pb->rec[i].coef += off;
         pb->rec[i].slice = tag;
-        pb->pc.mb[i] = q->pc.mb[i];
         pb->pc.mb[i].slice = tag;
         pb->decoded[i] = 1;
     }
