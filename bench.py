@@ -376,6 +376,10 @@ def end_to_end(streams, nframes, reps=3):
     # are the bound on this path (tools/e2e_env_sweep.sh: 1.89k -> 2.08k fps)
     env = dict(os.environ)
     env.setdefault("H264MI_BLOCKING_SYNC", "1")
+    # 8 decoder processes on the box's 16-core share: the calling thread plus
+    # 2 slice workers each (profiles/r51_host_ab.txt: 5.9 vs 6.4 ms host CPU
+    # per picture with 3 workers, same rate); the library default stays 3
+    env.setdefault("H264MI_PARSE_THREADS", "2")
     td = tempfile.mkdtemp(prefix="h264e2e")
     try:
         procs = []
@@ -413,7 +417,7 @@ def end_to_end(streams, nframes, reps=3):
             # per picture inside one decoder process (H264SwDecGetTiming):
             # host parse / record upload + launch / wait for the GPU / D2H copy
             res["per_picture_ms"] = {k[2:]: round(v * 1e3 / pics, 3) for k, v in sorted(parts.items())}
-            res["parse_threads_per_process"] = 1 + int(os.environ.get("H264MI_PARSE_THREADS", "3"))
+            res["parse_threads_per_process"] = 1 + int(env["H264MI_PARSE_THREADS"])
             res["host_sync"] = "blocking" if env["H264MI_BLOCKING_SYNC"] == "1" else "spin"
             # host CPU time (all threads of all processes) per picture, and the
             # cores that keeps busy at the measured rate

@@ -581,6 +581,20 @@ extern "C" const char *h264mi_engine_kernel(h264mi_engine *e)
     return e && e->last_kernel ? e->last_kernel : "";
 }
 
+// wait for everything queued on the engine's stream (sleeping under
+// H264MI_BLOCKING_SYNC); no flag accounting
+static int engine_wait(h264mi_engine *e)
+{
+    HIPCHECK(hipSetDevice(e->dev));
+    if (e->ev_block) {
+        HIPCHECK(hipEventRecord(e->ev_block, e->st));
+        HIPCHECK(hipEventSynchronize(e->ev_block));
+    } else {
+        HIPCHECK(hipStreamSynchronize(e->st));
+    }
+    return 0;
+}
+
 extern "C" int h264mi_engine_sync(h264mi_engine *e)
 {
     if (!e) return -1;
@@ -591,15 +605,9 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     // picture slots
     HIPCHECK(hipMemcpyAsync(e->h_err, e->d_err, sizeof(unsigned) * e->pipe_cap, hipMemcpyDeviceToHost, e->st));
     HIPCHECK(hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * e->pipe_cap, e->st));
-    if (e->ev_block) {
-        // a blocking-sync event: the waiting thread sleeps whatever the
-        // device's scheduling flags (set once per process, before the first
-        // context, or not at all)
-        HIPCHECK(hipEventRecord(e->ev_block, e->st));
-        HIPCHECK(hipEventSynchronize(e->ev_block));
-    } else {
-        HIPCHECK(hipStreamSynchronize(e->st));
-    }
+    // a blocking-sync event: the waiting thread sleeps whatever the device's
+    // scheduling flags (which take effect only before the first context)
+    if (engine_wait(e)) return -1;
     for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
     return 0;
 }
@@ -1102,7 +1110,7 @@ static int slot_flagged(HipBackendCtx *c, int slot, bool wait = true)
 {
     if (wait) {
         if (c->sh) HIPCHECK(hipEventSynchronize(c->ev_last));
-        else if (h264mi_engine_sync(c->e)) return -1;
+        else if (engine_wait(c->e)) return -1;      // (flags: copied into h_slot_err behind each decode)
     }
     if (slot < 0 || slot >= c->nslots) return -1;
     const unsigned f = c->h_slot_err[slot];
@@ -1116,7 +1124,7 @@ static int hb_sync(void *vctx)
     const unsigned n = c->enq;
     if (c->sh) {
         HIPCHECK(hipEventSynchronize(c->ev_last));
-    } else if (h264mi_engine_sync(c->e)) {
+    } else if (engine_wait(c->e)) {
         return -1;
     }
     c->synced = n;
