@@ -152,6 +152,8 @@ def mi() -> C.CDLL:
     L.h264mi_set_share.restype = i32
     L.h264mi_share_stats.argtypes = [i32, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
     L.h264mi_share_stats.restype = i32
+    L.h264mi_engine_pool_stats.argtypes = [C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]
+    L.h264mi_engine_pool_stats.restype = None
     L.h264mi_engine_read.argtypes = [vp, i32, i32, vp]
     L.h264mi_engine_read.restype = i32
     L.h264mi_engine_read_rgba.argtypes = [vp, i32, i32, vp]

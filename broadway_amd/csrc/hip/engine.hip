@@ -243,6 +243,13 @@ extern "C" void h264mi_engine_destroy(h264mi_engine *e)
 #define ENGINE_POOL_MAX 4
 static std::mutex g_pool_mu;
 static h264mi_engine *g_pool[ENGINE_POOL_MAX];
+static std::atomic<unsigned long long> g_pool_reused, g_pool_created;
+
+extern "C" void h264mi_engine_pool_stats(unsigned long long *reused, unsigned long long *created)
+{
+    if (reused) *reused = g_pool_reused.load();
+    if (created) *created = g_pool_created.load();
+}
 
 static bool engine_pool_on()
 {
@@ -263,7 +270,11 @@ static h264mi_engine *engine_get(int device, int w_mbs, int h_mbs, int nstreams,
             }
         }
     }
-    if (!e) return h264mi_engine_create(device, w_mbs, h_mbs, nstreams, nslots);
+    if (!e) {
+        g_pool_created++;
+        return h264mi_engine_create(device, w_mbs, h_mbs, nstreams, nslots);
+    }
+    g_pool_reused++;
     if (hipSetDevice(device) != hipSuccess) { h264mi_engine_destroy(e); return NULL; }
     engine_config(e);
     e->prepped_rec = e->prepped_pics = NULL;

@@ -191,6 +191,9 @@ int h264mi_engine_conceal(h264mi_engine *e, int stream, int slot, const int *ord
                           const uint8_t *decoded);
 /* diagnostics: k_conceal launches in this process */
 unsigned long long h264mi_conceal_launches(void);
+/* diagnostics: engines of H264SwDec* instances taken from the pool of
+ * released ones (H264MI_ENGINE_POOL) / newly created, in this process */
+void h264mi_engine_pool_stats(unsigned long long *reused, unsigned long long *created);
 
 /* Device-resident variant (records already in HBM; kernel-only timing):
  * d_recs = npics*w*h MbRec in batch order with coefficient offsets relative

@@ -354,3 +354,31 @@ def test_device_flag_reaches_its_own_picture_under_reordering(share, k, monkeypa
     assert [p[0] for p in pics] == [p[0] for p in c["pics"]]
     for got, ref in zip(pics, c["pics"]):
         assert got[2] == (nmbs if got[0] == k else ref[2]), (got, ref)
+
+
+def test_swdec_pooled_engines_vs_reference(monkeypatch):
+    """Instances created one after another take the engine a released one left
+    in the pool (H264MI_ENGINE_POOL, engine.hip engine_get / engine_put): the
+    reused engine must behave as a fresh one -- cleared frame slots, no batch
+    left prepped, flags of its own pictures only.  A damaged stream, a clean
+    one and the damaged one again on one picture size, each equal to the
+    reference; then the same with the pool off."""
+    L = _lib.mi()
+    names = ["err_drop_pic_gaps_11x9", "err_range_p_11x9", "err_trunc_slice_11x9", "err_drop_pic_gaps_11x9"]
+    reused0, created0 = C.c_ulonglong(), C.c_ulonglong()
+    L.h264mi_engine_pool_stats(C.byref(reused0), C.byref(created0))
+    for n in names:
+        c = CASES[n]
+        frames, _, pics = swdec_decode(stream(c), no_reorder=c["no_reorder"], info=True)
+        assert md5s(frames) == c["frames"] and [list(p) for p in pics] == c["pics"], n
+    reused1, created1 = C.c_ulonglong(), C.c_ulonglong()
+    L.h264mi_engine_pool_stats(C.byref(reused1), C.byref(created1))
+    assert reused1.value - reused0.value >= len(names) - 1
+    monkeypatch.setenv("H264MI_ENGINE_POOL", "0")
+    for n in names[:2]:
+        c = CASES[n]
+        frames, _, pics = swdec_decode(stream(c), no_reorder=c["no_reorder"], info=True)
+        assert md5s(frames) == c["frames"] and [list(p) for p in pics] == c["pics"], n
+    reused2, created2 = C.c_ulonglong(), C.c_ulonglong()
+    L.h264mi_engine_pool_stats(C.byref(reused2), C.byref(created2))
+    assert reused2.value == reused1.value and created2.value - created1.value == 2
