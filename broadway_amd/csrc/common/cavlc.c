@@ -14,7 +14,10 @@ int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, ui
 {
     int len;
     *abs_sum = 0;
-    memset(coef, 0, sizeof(int16_t) * (size_t)maxcoef);
+    /* constant sizes: inlined stores instead of a library call per block */
+    if (maxcoef == 16) memset(coef, 0, 32);
+    else if (maxcoef == 15) memset(coef, 0, 30);
+    else memset(coef, 0, sizeof(int16_t) * (size_t)maxcoef);
     int sym = vlc_decode(&gCoeffTokenDec[coeff_token_class(nC)], br_peek(br, 16), &len);
     if (sym < 0) return -1;
     br_skip(br, len);

@@ -28,10 +28,24 @@ int mbctx_neighbour(const PicCtx *pc, int cur, int n)
     return neighbour_of(pc, cur, n);
 }
 
+static int nn_luma(const MbInfo *m, int blk);
+static int nn_chroma(const MbInfo *m, int comp, int blk);
+
 void mbctx_begin_mb(PicCtx *pc, int cur)
 {
     pc->nb_key = 0;
     for (int n = 0; n < 4; n++) pc->nb[n] = neighbour_of(pc, cur, n);
+    const MbInfo *A = pc->nb[NB_A] >= 0 ? &pc->mb[pc->nb[NB_A]] : NULL;
+    const MbInfo *B = pc->nb[NB_B] >= 0 ? &pc->mb[pc->nb[NB_B]] : NULL;
+    for (int i = 0; i < 4; i++) {
+        pc->nl[i] = (int8_t)(A ? nn_luma(A, blk_index(3, i)) : -1);
+        pc->nt[i] = (int8_t)(B ? nn_luma(B, blk_index(i, 3)) : -1);
+    }
+    for (int c = 0; c < 2; c++)
+        for (int i = 0; i < 2; i++) {
+            pc->ncl[c][i] = (int8_t)(A ? nn_chroma(A, c, i * 2 + 1) : -1);
+            pc->nct[c][i] = (int8_t)(B ? nn_chroma(B, c, 2 + i) : -1);
+        }
     pc->nb_key = cur + 1;
 }
 
@@ -60,9 +74,25 @@ static int nn_luma(const MbInfo *m, int blk)
     return m->tc[blk];
 }
 
+static inline int nc_of(int nA, int nB)
+{
+    if (nA >= 0 && nB >= 0) return (nA + nB + 1) >> 1;
+    if (nA >= 0) return nA;
+    if (nB >= 0) return nB;
+    return 0;
+}
+
 int mbctx_nc_luma(const PicCtx *pc, int cur, int blk)
 {
     int x = kBlkX[blk], y = kBlkY[blk];
+    if (pc->nb_key == cur + 1) {
+        /* the current MB's blocks to the left / above precede blk in z-scan
+         * and hold their TotalCoeff already (its type is not skip or PCM) */
+        const MbInfo *m = &pc->mb[cur];
+        const int nA = x > 0 ? m->tc[blk_index(x - 1, y)] : pc->nl[y];
+        const int nB = y > 0 ? m->tc[blk_index(x, y - 1)] : pc->nt[x];
+        return nc_of(nA, nB);
+    }
     int aA, bA, aB, bB;
     int avA = blk_nb(pc, cur, x - 1, y, &aA, &bA);
     int avB = blk_nb(pc, cur, x, y - 1, &aB, &bB);
@@ -84,6 +114,12 @@ static int nn_chroma(const MbInfo *m, int comp, int blk)
 int mbctx_nc_chroma(const PicCtx *pc, int cur, int comp, int blk)
 {
     int x = blk & 1, y = blk >> 1;
+    if (pc->nb_key == cur + 1) {
+        const MbInfo *m = &pc->mb[cur];
+        const int nA = x > 0 ? m->tcc[comp * 4 + blk - 1] : pc->ncl[comp][y];
+        const int nB = y > 0 ? m->tcc[comp * 4 + blk - 2] : pc->nct[comp][x];
+        return nc_of(nA, nB);
+    }
     int avA, avB, nA = 0, nB = 0;
     if (x > 0) { avA = 1; nA = nn_chroma(&pc->mb[cur], comp, blk - 1); }
     else {

@@ -35,6 +35,11 @@ typedef struct PicCtx {
      * zero-initialised context has none) */
     int      nb_key;
     int      nb[4];
+    /* with it, the neighbours' TotalCoeff next to the MB (-1: neighbour
+     * unavailable): luma left column / top row (rows / columns 0..3), chroma
+     * per component the left column / top row (0..1) -- nC (§9.2.1) without
+     * the per-block neighbour walk */
+    int8_t   nl[4], nt[4], ncl[2][2], nct[2][2];
 } PicCtx;
 
 enum { NB_A = 0, NB_B = 1, NB_C = 2, NB_D = 3 };
