@@ -53,6 +53,7 @@ def report(d0, d1):
     mbs = S * W * H
     keys = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
             "SQ_INSTS_SMEM", "SQ_WAVES"]
+    keys += sorted(k for k in a if k not in keys)     # cycle counters (quad-cycles, summed over waves)
     out = {"mbs_per_launch": mbs, "method": "SQ counters per k_wgpp launch (profiling build), normal run minus a run "
                                             "whose row waves only drain the MC ring; per MB of the launch"}
     for k in keys:
