@@ -75,10 +75,90 @@ def trace_window(src):
                     "and the P-only leg's; this is the timed window alone"}
 
 
+def _counters(path):
+    """{kernel: {counter: (mean per launch, launches)}} of one counter-collection CSV"""
+    d = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        d[kname(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: (sum(v) / len(v), len(v)) for c, v in cs.items()} for k, cs in d.items()}
+
+
+def exact_bytes(src, prefix, prog):
+    """Memory-side bytes per launch from the L2's request-size counters
+    (tools/pmc_bytes.sh): read = 32 n32 + 64 n64 + 128 n128 (TCC_EA0_RDREQ_*B),
+    split by destination with the 32-B-unit counters RDREQ_{DRAM,GMI,IO}_32B;
+    write = 32 x WRREQ_WRITE_{DRAM,GMI,IO}_32B.  None when the passes are absent."""
+    paths = {p: os.path.join(src, f"bytes_{prefix}_{p}", f"{prog}_counter_collection.csv") for p in ("rd", "src", "wr")}
+    if not all(os.path.exists(p) for p in paths.values()):
+        return None
+    c = {p: _counters(q) for p, q in paths.items()}
+    out = {}
+    for k in c["rd"]:
+        rd, sr, wr = c["rd"][k], c["src"].get(k, {}), c["wr"].get(k, {})
+        g = lambda t, n: t.get(n, (0.0, 0))[0]
+        n32, n64, n128 = g(rd, "TCC_EA0_RDREQ_32B_sum"), g(rd, "TCC_EA0_RDREQ_64B_sum"), g(rd, "TCC_EA0_RDREQ_128B_sum")
+        out[k] = {"launches": rd["TCC_EA0_RDREQ_sum"][1],
+                  "rdreq": {"all": g(rd, "TCC_EA0_RDREQ_sum"), "32B": n32, "64B": n64, "128B": n128},
+                  "read_bytes": int(32 * n32 + 64 * n64 + 128 * n128),
+                  "read_bytes_dram": int(32 * g(sr, "TCC_EA0_RDREQ_DRAM_32B_sum")),
+                  "read_bytes_gmi": int(32 * g(sr, "TCC_EA0_RDREQ_GMI_32B_sum")),
+                  "read_bytes_io": int(32 * g(sr, "TCC_EA0_RDREQ_IO_32B_sum")),
+                  "write_bytes_dram": int(32 * g(wr, "TCC_EA0_WRREQ_WRITE_DRAM_32B_sum")),
+                  "write_bytes_gmi": int(32 * g(wr, "TCC_EA0_WRREQ_WRITE_GMI_32B_sum")),
+                  "write_bytes_io": int(32 * g(wr, "TCC_EA0_WRREQ_WRITE_IO_32B_sum"))}
+    return out
+
+
+def bytes_report(tag, src, dst):
+    """profiles/<tag>_bytes.json from tools/pmc_bytes.sh: the calibration
+    program's known byte counts against the request-size accounting, and the
+    bench's bytes per reconstruction step (k_wgpp + the standalone k_prep
+    spread over the k_wgpp launches, as main() does); the request-size
+    figures are added to profiles/traffic.json beside the FETCH_SIZE one"""
+    rep = {"tag": tag, "method": "tools/pmc_bytes.sh: rocprofv3 --pmc, three passes of <= 4 TCC counters "
+                                 "(TCC_EA0_RDREQ_{32B,64B,128B}, RDREQ_{DRAM,GMI,IO}_32B, "
+                                 "WRREQ_WRITE_{DRAM,GMI,IO}_32B); bytes per launch"}
+    want = {}
+    log = os.path.join(src, "bytes_calib.log")
+    if os.path.exists(log):
+        for line in open(log):
+            f = line.split()
+            if len(f) >= 3 and f[0].startswith("k_") and f[1] == "bytes":
+                want[f[0]] = int(f[2])
+    cal = exact_bytes(src, "calib", "calib") or {}
+    rep["calibration"] = {k: {"bytes_read_by_program": b, "request_size_bytes": cal[k]["read_bytes"],
+                              "ratio": round(cal[k]["read_bytes"] / b, 3),
+                              "dram_32B_unit_bytes": cal[k]["read_bytes_dram"], "rdreq": cal[k]["rdreq"]}
+                          for k, b in want.items() if k in cal}
+    ex = exact_bytes(src, "bench", "bench")
+    rep["kernels"] = ex
+    main_k = "k_wgpp"
+    n = ex[main_k]["launches"]
+    keys = ("read_bytes", "read_bytes_dram", "read_bytes_gmi", "read_bytes_io",
+            "write_bytes_dram", "write_bytes_gmi", "write_bytes_io")
+    step = {k: sum(ex[kk][k] * ex[kk]["launches"] for kk in ex if kk in ("k_wgpp", "k_prep")) / n for k in keys}
+    step = {k: int(v) for k, v in step.items()}
+    step["dram_bytes"] = step["read_bytes_dram"] + step["write_bytes_dram"]
+    step["all_bytes"] = step["read_bytes"] + step["write_bytes_dram"] + step["write_bytes_gmi"] + step["write_bytes_io"]
+    rep["per_step"] = step
+    json.dump(rep, open(os.path.join(dst, f"{tag}_bytes.json"), "w"), indent=1)
+    tp = os.path.join(dst, "traffic.json")
+    t = json.load(open(tp)) if os.path.exists(tp) else {}
+    t["request_size_accounting"] = {"source": f"profiles/{tag}_bytes.json (tools/pmc_bytes.sh)",
+                                    "dram_bytes_per_step": step["dram_bytes"],
+                                    "all_bytes_per_step": step["all_bytes"],
+                                    "read_bytes_per_step": step["read_bytes"],
+                                    "write_bytes_dram_per_step": step["write_bytes_dram"]}
+    json.dump(t, open(tp, "w"), indent=1)
+    print(json.dumps(rep, indent=1))
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
+    if os.path.exists(os.path.join(src, "bytes_bench_rd")) and not os.path.exists(os.path.join(src, "prof")):
+        return bytes_report(tag, src, dst)
     shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     fetch = per_launch(os.path.join(src, "pmc_fetch", "bench_counter_collection.csv"), "FETCH_SIZE")
     write = per_launch(os.path.join(src, "pmc_write", "bench_counter_collection.csv"), "WRITE_SIZE")
