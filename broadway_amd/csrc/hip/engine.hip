@@ -384,6 +384,12 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     a.epoch = e->epoch;
     a.prof = e->d_prof;
     a.prof_mode = e->d_prof && getenv("H264MI_PROF_MODE") ? atoi(getenv("H264MI_PROF_MODE")) : 0;
+    // study knobs: MC lead over the row's deblocking (MBs; 0 / unset = the
+    // ring depth), before the chain has begun (LEAD0, at least 4) and after
+    static const int mc_lead0 = getenv("H264MI_MC_LEAD0") ? std::max(4, atoi(getenv("H264MI_MC_LEAD0"))) : 0;
+    static const int mc_lead = getenv("H264MI_MC_LEAD") ? std::max(4, atoi(getenv("H264MI_MC_LEAD"))) : 0;
+    a.mc_lead0 = mc_lead0;
+    a.mc_lead = mc_lead;
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;

@@ -63,6 +63,10 @@ struct ReconArgs {
     // deblocking, no stores) -- SQ counters of such a launch minus those of
     // a normal one split the instruction counts by wave role (tools/sq_roles.py)
     int prof_mode;
+    // how far (MBs) a row's MC waves may run ahead of its deblocking: lead0
+    // until the row's chain has taken its first MB, lead after that; 0 = the
+    // ring depth (H264MI_MC_LEAD0 / H264MI_MC_LEAD, engine.hip)
+    int mc_lead0, mc_lead;
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -1849,13 +1853,20 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     McLoad ld;
     if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
     if (c0 < a.w) mc_issue(a, pd, p, r * a.w + c0, v0, lane, ld);
+    const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
+    const int lead0 = a.mc_lead0 > 0 && a.mc_lead0 < lead ? a.mc_lead0 : lead;
     for (int c = c0; c < a.w; c += NMC) {
         const int slot = c & (RK - 1);
         const bool more = c + NMC < a.w;
         const uint32_t nv0 = more ? recrow[(size_t)(c + NMC) * 24 + (lane < 24 ? lane : 0)] : 0;
-        if (c >= RK) {
+        if (c >= lead0) {
+            // slot free (ring depth) and at most lead MBs ahead; before the
+            // row's chain has begun (consumed < 1: MB 1 not taken yet) at
+            // most lead0 -- with the defaults (lead0 = lead = RK) exactly
+            // the ring's own condition
+            const int need = max(c - lead + 1, lead0 < lead ? 1 : 0);
             unsigned spins = 0;
-            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RK + 1) {
+            while (__builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < need) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 16u); break; }
             }
