@@ -732,6 +732,20 @@ def alg_bytes(run, launch_ids):
     return tot
 
 
+def ref_line_bytes(run, launch_ids):
+    """The listed launches' reference footprint in whole 128-B lines (per
+    picture: distinct lines of each reference slot its MC windows touch,
+    h264mi_capture_ref_lines): the line-granular, compulsory part of the
+    reference reads, beside R_alg's bytes used.  With 4 reference frames per
+    stream it is close to 4 whole frames per picture."""
+    tot = 0
+    for i in launch_ids:
+        for step in run.launches[i]:
+            for s, k in enumerate(step):
+                tot += run.caps[s].pictures[k].ref_line_bytes
+    return tot
+
+
 def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0):
     """One single-GPU measurement of another SURVEY §8d config with the same
     step structure (records resident in HBM, one k_wgpp launch per step,
@@ -834,6 +848,7 @@ def main(argv=None):
     # (per picture: MC reference footprint + coded 4x4 blocks x 32 B + 96-B
     # MB records) / their average k_wgpp duration
     launch_bytes = alg_bytes(run, sampled) / max(len(sampled), 1)
+    launch_ref_lines = ref_line_bytes(run, sampled) / max(len(sampled), 1)
     achieved = launch_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
     traffic = load_traffic()
     frame_read_gbs = alg_bytes(run, range(run.n_warm, len(run.launches))) * world / dt / 1e9
@@ -919,6 +934,12 @@ def main(argv=None):
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
                          "alg_bytes_per_launch": int(launch_bytes),
+                         # reference reads at 128-B line granularity (compulsory for these
+                         # windows; R_alg counts only the bytes used) and the PMC traffic by
+                         # request size (tools/pmc_bytes.sh), DESIGN.md §3.3
+                         "ref_line_bytes_per_launch": int(launch_ref_lines),
+                         "traffic_by_request_size": (traffic.get("request_size_accounting") or {}).get(
+                             "dram_bytes_per_step") if traffic else None,
                          "avg_launch_kernel_us": round(step_us, 2),
                          "timed_launches_sampled": len(sampled),
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),

@@ -193,6 +193,8 @@ def mi() -> C.CDLL:
     L.h264mi_capture_picture.restype = i32
     L.h264mi_capture_stats.argtypes = [vp, i32, C.POINTER(u32), C.POINTER(u32), C.POINTER(u32)]
     L.h264mi_capture_stats.restype = i32
+    L.h264mi_capture_ref_lines.argtypes = [vp, i32, C.POINTER(C.c_uint64)]
+    L.h264mi_capture_ref_lines.restype = i32
     L.h264mi_capture_free.argtypes = [vp]
     L.h264mi_capture_free.restype = None
     L.h264mi_device_alloc.argtypes = [sz]

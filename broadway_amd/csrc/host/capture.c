@@ -15,6 +15,7 @@ typedef struct CapPic {
     uint32_t ncoef;
     int      cur_slot;
     uint64_t alg_ref_bytes;
+    uint64_t ref_line_bytes;
     uint32_t n_inter, n_intra, n_coded;
 } CapPic;
 
@@ -29,6 +30,8 @@ struct h264mi_capture {
     int errors;
     int reconfigured;
 };
+
+static uint64_t ref_line_bytes(const MbRec *rec, int w, int h);
 
 static int cap_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
 {
@@ -131,10 +134,70 @@ static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
     p->n_coded = pb->n_coded_blocks;
     memcpy(c->recs + c->nrec, pb->rec, sizeof(MbRec) * nmbs);
     set_ref_rows(c->recs + c->nrec, c->w, c->h);
+    p->ref_line_bytes = ref_line_bytes(c->recs + c->nrec, c->w, c->h);
     if (pb->ncoef) memcpy(c->coefs + c->ncoef * 16, pb->coef, (size_t)pb->ncoef * 32);
     c->nrec += nmbs;
     c->ncoef += pb->ncoef;
     return 0;
+}
+
+/* Distinct 128-B lines of the reference slots that k_wgpp's MC loads touch
+ * for one picture, times 128: the line-granular (compulsory) part of its
+ * reference traffic, beside R_alg's bytes actually used (part_bytes).  The
+ * windows are mc_issue's (recon_kernels.hip): per 4x4 luma block 9 rows of
+ * 12 bytes from (x0 & ~3) clamped to [0, W16 - 12], per 2x2 chroma block and
+ * component 3 rows of 8 bytes from (x0 & ~3) clamped to [0, CW - 8], rows
+ * clamped to the plane.  Slots are frame_bytes = 384 B per MB apart, a
+ * multiple of 128, so line ids never straddle slots. */
+static uint64_t ref_line_bytes(const MbRec *rec, int w, int h)
+{
+    const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2;
+    const size_t lines = (size_t)w * h * 3;             /* 384 B per MB / 128 */
+    int maxslot = -1;
+    for (int i = 0; i < w * h; i++)
+        if (rec[i].type == MBT_INTER || rec[i].type == MBT_SKIP)
+            for (int k = 0; k < 4; k++) maxslot = rec[i].ref[k] > maxslot ? rec[i].ref[k] : maxslot;
+    if (maxslot < 0) return 0;
+    uint8_t *mark = (uint8_t *)calloc((size_t)(maxslot + 1) * lines, 1);
+    if (!mark) return 0;
+    uint64_t n = 0;
+#define MARK(slot, off, len) do {                                                   \
+        const size_t a_ = (off) / 128, b_ = ((off) + (len) - 1) / 128;             \
+        for (size_t l_ = a_; l_ <= b_; l_++) {                                     \
+            uint8_t *m_ = mark + (size_t)(slot) * lines + l_;                      \
+            if (!*m_) { *m_ = 1; n++; }                                            \
+        }                                                                          \
+    } while (0)
+    for (int i = 0; i < w * h; i++) {
+        const MbRec *r = &rec[i];
+        if (r->type != MBT_INTER && r->type != MBT_SKIP) continue;
+        const int mbx = i % w, mby = i / w;
+        for (int b = 0; b < 16; b++) {
+            const int bx = ((b >> 2) & 1) * 2 + (b & 1), by = ((b >> 3) & 1) * 2 + ((b >> 1) & 1);
+            const int slot = r->ref[b >> 2];
+            const int mvx = r->mv[b][0], mvy = r->mv[b][1];
+            int x0 = mbx * 16 + bx * 4 + (mvx >> 2) - 2, y0 = mby * 16 + by * 4 + (mvy >> 2) - 2;
+            int ax = x0 & ~3;
+            ax = ax < 0 ? 0 : ax > W16 - 12 ? W16 - 12 : ax;
+            for (int k = 0; k < 9; k++) {
+                int y = y0 + k;
+                y = y < 0 ? 0 : y > H16 - 1 ? H16 - 1 : y;
+                MARK(slot, (size_t)y * W16 + ax, 12);
+            }
+            int cx0 = mbx * 8 + bx * 2 + (mvx >> 3), cy0 = mby * 8 + by * 2 + (mvy >> 3);
+            int cax = cx0 & ~3;
+            cax = cax < 0 ? 0 : cax > CW - 8 ? CW - 8 : cax;
+            for (int comp = 0; comp < 2; comp++)
+                for (int k = 0; k < 3; k++) {
+                    int y = cy0 + k;
+                    y = y < 0 ? 0 : y > CH - 1 ? CH - 1 : y;
+                    MARK(slot, (size_t)W16 * H16 + (size_t)comp * CW * CH + (size_t)y * CW + cax, 8);
+                }
+        }
+    }
+#undef MARK
+    free(mark);
+    return n * 128;
 }
 
 static int cap_read(void *vctx, int slot, uint8_t *dst)
@@ -201,6 +264,13 @@ int h264mi_capture_picture(const h264mi_capture *c, int i, const void **rec, con
     if (ncoef) *ncoef = p->ncoef;
     if (cur_slot) *cur_slot = p->cur_slot;
     if (alg_ref_bytes) *alg_ref_bytes = p->alg_ref_bytes;
+    return 0;
+}
+
+int h264mi_capture_ref_lines(const h264mi_capture *c, int i, uint64_t *ref_line_bytes)
+{
+    if (!c || i < 0 || i >= c->npics || !ref_line_bytes) return -1;
+    *ref_line_bytes = c->pics[i].ref_line_bytes;
     return 0;
 }
 

@@ -30,6 +30,7 @@ class CapturedPicture:
     n_inter: int
     n_intra: int
     n_coded: int
+    ref_line_bytes: int = 0     # distinct 128-B reference lines the MC windows touch, x 128
 
 
 class Capture:
@@ -53,8 +54,10 @@ class Capture:
                                        C.byref(alg))
         a, b, c = C.c_uint32(), C.c_uint32(), C.c_uint32()
         self._L.h264mi_capture_stats(self._h, i, C.byref(a), C.byref(b), C.byref(c))
+        lb = C.c_uint64()
+        self._L.h264mi_capture_ref_lines(self._h, i, C.byref(lb))
         return CapturedPicture(rec.value or 0, coef.value or 0, nc.value, slot.value, alg.value,
-                               a.value, b.value, c.value)
+                               a.value, b.value, c.value, lb.value)
 
     def records_bytes(self, i: int) -> bytes:
         p = self.pictures[i]

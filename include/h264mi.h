@@ -267,6 +267,11 @@ int  h264mi_capture_info(const h264mi_capture *c, int *w_mbs, int *h_mbs, int *n
 int  h264mi_capture_picture(const h264mi_capture *c, int i, const void **rec, const int16_t **coef,
                             uint32_t *ncoef, int *cur_slot, uint64_t *alg_ref_bytes);
 int  h264mi_capture_stats(const h264mi_capture *c, int i, uint32_t *n_inter, uint32_t *n_intra, uint32_t *n_coded);
+/* picture i's reference footprint in whole 128-B lines (distinct lines of
+ * each reference slot the k_wgpp MC windows touch, x 128): the line-granular
+ * reference traffic beside alg_ref_bytes' bytes used (measurement helper; no
+ * reference counterpart) */
+int  h264mi_capture_ref_lines(const h264mi_capture *c, int i, uint64_t *ref_line_bytes);
 void h264mi_capture_free(h264mi_capture *c);
 
 /* Device memory helpers for the device-resident path (HIP device pointers).

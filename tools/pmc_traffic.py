@@ -157,7 +157,7 @@ def main(tag):
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
-    if os.path.exists(os.path.join(src, "bytes_bench_rd")) and not os.path.exists(os.path.join(src, "prof")):
+    if not os.path.exists(os.path.join(src, "prof")):         # tools/pmc_bytes.sh alone
         return bytes_report(tag, src, dst)
     shutil.copy(os.path.join(src, "prof", "bench_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     fetch = per_launch(os.path.join(src, "pmc_fetch", "bench_counter_collection.csv"), "FETCH_SIZE")
@@ -195,6 +195,8 @@ def main(tag):
     if os.path.exists(os.path.join(src, "bench.json")):
         shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{tag}_bench.json"))
     print(json.dumps(out, indent=1))
+    if os.path.exists(os.path.join(src, "bytes_bench_rd")):
+        bytes_report(tag, src, dst)
 
 
 if __name__ == "__main__":
