@@ -52,7 +52,7 @@ static int block_in_range(const int16_t *lv, uint32_t sum, int start, int32_t dc
     return idct_in_range(d);
 }
 
-int mb_residual_in_range(const int16_t (*blk)[16], const uint32_t *bsum, uint32_t cbits, int is_i16,
+int mb_residual_in_range(const int16_t *const *blk, const uint32_t *bsum, uint32_t cbits, int is_i16,
                          int qp, int qpc)
 {
     /* whole-MB bound first: every block's DC and AC magnitudes are at most

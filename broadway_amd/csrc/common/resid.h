@@ -18,7 +18,7 @@
  * DC, [25]/[26] Cb/Cr DC (4 levels); only blocks whose cbits bit is set are
  * read.  bsum[b]: sum of |level| of block b (from the CAVLC decode).
  * Returns 1 if every processed block stays in range. */
-int mb_residual_in_range(const int16_t (*blk)[16], const uint32_t *bsum, uint32_t cbits, int is_i16,
+int mb_residual_in_range(const int16_t *const *blk, const uint32_t *bsum, uint32_t cbits, int is_i16,
                          int qp, int qpc);
 
 #endif

@@ -345,24 +345,33 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     m->qp = (uint8_t)*qp;
     r->qp = (uint8_t)*qp;
 
-    /* residual(), §7.3.5.3 */
-    int16_t blk[27][16];
+    /* residual(), §7.3.5.3.  Coded blocks are decoded straight into the
+     * picture's coefficient pool in bit order (luma 0..15, chroma AC 16..23,
+     * then the DC blocks 24..26, which the syntax sends first and which go
+     * through a local copy); a block with TotalCoeff 0 leaves no entry. */
+    const uint32_t base = pb->ncoef;
+    if (!picbuild_coef_alloc(pb, 27)) return -1;     /* room for every block */
+    pb->ncoef = base;
+    int16_t *nxt = pb->coef + (size_t)base * 16;
+    int16_t dcb[3][16];
+    memset(dcb, 0, sizeof(dcb));                     /* chroma DC fills 4 of 16 */
+    const int16_t *blk[27];
     uint32_t bsum[27];
     uint32_t cbits = 0;
     if (is_i16) {
-        int tc = cavlc_decode_block_sum(br, mbctx_nc_luma(&pb->pc, cur, 0), 16, blk[24], &bsum[24]);
+        int tc = cavlc_decode_block_sum(br, mbctx_nc_luma(&pb->pc, cur, 0), 16, dcb[0], &bsum[24]);
         if (tc < 0) return -1;
-        if (tc) cbits |= 1u << 24;
+        if (tc) { cbits |= 1u << 24; blk[24] = dcb[0]; }
     }
     for (int b = 0; b < 16; b++) {
         if (cbp & (1 << (b >> 2))) {
             int nc = mbctx_nc_luma(&pb->pc, cur, b);
             int tc;
-            if (is_i16) { blk[b][0] = 0; tc = cavlc_decode_block_sum(br, nc, 15, blk[b] + 1, &bsum[b]); }
-            else tc = cavlc_decode_block_sum(br, nc, 16, blk[b], &bsum[b]);
+            if (is_i16) { nxt[0] = 0; tc = cavlc_decode_block_sum(br, nc, 15, nxt + 1, &bsum[b]); }
+            else tc = cavlc_decode_block_sum(br, nc, 16, nxt, &bsum[b]);
             if (tc < 0) return -1;
             m->tc[b] = (uint8_t)tc;
-            if (tc) cbits |= 1u << b;
+            if (tc) { cbits |= 1u << b; blk[b] = nxt; nxt += 16; }
         } else {
             m->tc[b] = 0;
         }
@@ -370,20 +379,20 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     int cc = cbp >> 4;
     if (cc) {
         for (int comp = 0; comp < 2; comp++) {
-            int tc = cavlc_decode_block_sum(br, -1, 4, blk[25 + comp], &bsum[25 + comp]);
+            int tc = cavlc_decode_block_sum(br, -1, 4, dcb[1 + comp], &bsum[25 + comp]);
             if (tc < 0) return -1;
-            if (tc) cbits |= 1u << (25 + comp);
+            if (tc) { cbits |= 1u << (25 + comp); blk[25 + comp] = dcb[1 + comp]; }
         }
     }
     for (int comp = 0; comp < 2; comp++)
         for (int b = 0; b < 4; b++) {
             int idx = 16 + comp * 4 + b;
             if (cc & 2) {
-                blk[idx][0] = 0;
-                int tc = cavlc_decode_block_sum(br, mbctx_nc_chroma(&pb->pc, cur, comp, b), 15, blk[idx] + 1, &bsum[idx]);
+                nxt[0] = 0;
+                int tc = cavlc_decode_block_sum(br, mbctx_nc_chroma(&pb->pc, cur, comp, b), 15, nxt + 1, &bsum[idx]);
                 if (tc < 0) return -1;
                 m->tcc[comp * 4 + b] = (uint8_t)tc;
-                if (tc) cbits |= 1u << idx;
+                if (tc) { cbits |= 1u << idx; blk[idx] = nxt; nxt += 16; }
             } else {
                 m->tcc[comp * 4 + b] = 0;
             }
@@ -391,16 +400,15 @@ static int parse_mb(PicBuild *pb, BitReader *br, int cur, const SliceHdr *sh, co
     if (br->err) return -1;
     /* h264bsdDecodeMacroblock -> ProcessResidual: a residual outside
      * [-512, 511] fails the MB, hence the slice (resid.h) */
-    if (cbits && !mb_residual_in_range((const int16_t (*)[16])blk, bsum, cbits, is_i16, *qp,
+    if (cbits && !mb_residual_in_range(blk, bsum, cbits, is_i16, *qp,
                                        kQpChroma[clip3(0, 51, *qp + pps->chroma_qp_offset)]))
         pb->mb_decode_err = 1;
-    int nblk = __builtin_popcount(cbits);
-    int16_t *dst = picbuild_coef_alloc(pb, (uint32_t)nblk);
-    if (!dst) return -1;
-    r->coef = pb->ncoef - (uint32_t)nblk;
+    for (int k = 0; k < 3; k++)
+        if (cbits & (1u << (24 + k))) { memcpy(nxt, dcb[k], 32); nxt += 16; }
+    const int nblk = __builtin_popcount(cbits);
+    r->coef = base;
     r->cbits = cbits;
-    for (int bit = 0; bit < 27; bit++)
-        if (cbits & (1u << bit)) { memcpy(dst, blk[bit], 32); dst += 16; }
+    pb->ncoef = base + (uint32_t)nblk;
     pb->n_coded_blocks += (uint32_t)nblk;
     return br->err ? -1 : 0;
 }
