@@ -390,6 +390,8 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     static const int mc_lead = getenv("H264MI_MC_LEAD") ? std::max(4, atoi(getenv("H264MI_MC_LEAD"))) : 0;
     a.mc_lead0 = mc_lead0;
     a.mc_lead = mc_lead;
+    static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 0;
+    a.row_prio_split = row_prio;
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;

@@ -67,6 +67,10 @@ struct ReconArgs {
     // until the row's chain has taken its first MB, lead after that; 0 = the
     // ring depth (H264MI_MC_LEAD0 / H264MI_MC_LEAD, engine.hip)
     int mc_lead0, mc_lead;
+    // study knob (H264MI_ROW_PRIO=1): row waves at s_setprio 1 outside the
+    // chain (slot waits, copy-in, frame stores) and 3 on it (hdone wait ..
+    // publish); 0 = 3 throughout
+    int row_prio_split;
 };
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -1367,6 +1371,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     }
 
     for (int c = w; c < W; c += 2) {
+        if (a.row_prio_split) __builtin_amdgcn_s_setprio(1);
         if (prof) tc0 = clock64();
         // per-MB stamps (100 MHz wall clock): [0] row-above entry c in hand (H(c)
         // may start); [1] V(c) start (after the hdone wait and halo copy) in
@@ -1411,6 +1416,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             *(uint32_t *)(Lb + db_lds) = od;
         }
         PPT(0);
+        if (a.row_prio_split) __builtin_amdgcn_s_setprio(3);
         // ---- the chain: MB c-1's H pass done -> its columns 12..15
         if (c > 0) {
             unsigned spins = 0;
@@ -1503,6 +1509,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             if (prof && lane == 0) pmb[2] = (wall_clock64() & 0xFFFFFFFFull) | (tvd << 32);
         }
         // ---- off the chain again: frame stores, once per sample
+        if (a.row_prio_split) __builtin_amdgcn_s_setprio(1);
         if (!last_row && c != W - 1) {
             const uint32_t va = *(const uint32_t *)(Lb + sa_lds);
             const uint32_t vb = *(const uint32_t *)(Lb + sb_lds);

@@ -4,7 +4,8 @@
 # per variant and round: GOP-mix frames/s and k_wgpp us (bench, no verify);
 # then one FETCH_SIZE and one WRITE_SIZE pass (k_wgpp average per launch, KiB:
 # read = 2 x FETCH_SIZE on gfx950, profiles/r54_bytes.json); VERIFY=1 adds a
-# verified bench run per variant (480 frames vs the reference MD5s).
+# verified bench run per variant (480 frames vs the reference MD5s); NO_PMC=1
+# skips the counter passes.
 set -o pipefail
 mkdir -p gpurun_out/abt
 export TMPDIR=/tmp
@@ -16,6 +17,7 @@ for i in $(seq 1 ${ROUNDS:-2}); do
   done
 done
 for spec in "$@"; do
+  [ -n "$NO_PMC" ] && break
   name=${spec%%:*}; envs=${spec#*:}
   for c in FETCH_SIZE WRITE_SIZE; do
     ( [ -n "$envs" ] && export $envs; timeout -s KILL 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/abt/${name}_$c -o bench -- python3 bench.py --no-cpu-baseline --no-verify --no-e2e --no-legs --no-rgba > /dev/null 2> gpurun_out/abt/pmc.err ) || { tail -20 gpurun_out/abt/pmc.err; exit 1; }
