@@ -539,6 +539,9 @@ class _DryEngine:
     def timing_report(self):
         return 0.0, 0.0, 0
 
+    def timing_list(self, cap=4096):
+        return []
+
     def errors(self):
         return 0
 
@@ -691,12 +694,12 @@ class DeviceRun:
         self.close_engine()
 
 
-def timed_run(run, dist, torch, sync, stride):
+def timed_run(run, dist, torch, sync, stride=1):
     """Pre-roll + warmup launches untimed, then the timed launches bracketed
     by a barrier and device syncs; HIP events on every stride-th timed
-    launch, carried by k_wgpp's own dispatch packet.  Returns (wall seconds
-    max over ranks, avg k_wgpp us of the sampled launches, sampled launch
-    indices)."""
+    launch (default: every one), carried by k_wgpp's own dispatch packet.
+    Returns (wall seconds max over ranks, avg k_wgpp us of the sampled
+    launches, sampled launch indices, per-launch us of those launches)."""
     for i in range(run.n_warm):
         run.launch(i)
     run.eng.sync()
@@ -715,9 +718,21 @@ def timed_run(run, dist, torch, sync, stride):
         dist.barrier()
     t1 = time.perf_counter()
     dt = max_over_ranks(dist, torch, t1 - t0)
+    per = run.eng.timing_list(ntimed) or []
     _, us, nb = run.eng.timing_report()
     sampled = [run.n_warm + j for j in range(0, ntimed, stride)][:nb]
-    return dt, us / max(nb, 1), sampled
+    return dt, us / max(nb, 1), sampled, per
+
+
+def launch_split(run, sampled, per):
+    """Sampled launches split by whether one of their pictures is an IDR
+    (I picture): {"i": (n, avg us), "p": (n, avg us)}."""
+    out = {}
+    for key, want in (("i", True), ("p", False)):
+        v = [u for i, u in zip(sampled, per)
+             if any(run.is_i[k][s] for step in run.launches[i] for s, k in enumerate(step)) == want]
+        out[key] = (len(v), round(sum(v) / len(v), 2) if v else None)
+    return out
 
 
 def alg_bytes(run, launch_ids):
@@ -766,7 +781,7 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0):
         os.environ.pop("H264MI_MC_WAVES", None)
         os.environ.pop("H264MI_RPW", None)
     try:
-        dt, launch_us, sampled = timed_run(run, None, torch, torch.cuda.synchronize, 1)
+        dt, launch_us, sampled, _ = timed_run(run, None, torch, torch.cuda.synchronize, 1)
         r_alg = alg_bytes(run, sampled) / max(len(sampled), 1)
         refs = [golden_frames(config, sd, {}) for sd in seeds]
         ok, n, missing, _ = run.verify(refs)
@@ -832,9 +847,13 @@ def main(argv=None):
     eng, P, resident = run.eng, run.P, run.resident
     t_prep = time.perf_counter() - t_prep
     sync = (lambda: None) if a.dry_run else torch.cuda.synchronize
-    stride = int(os.environ.get("BENCH_TIMING_STRIDE", "4"))
+    # HIP events on every timed launch by default: they ride k_wgpp's own
+    # dispatch packet (no extra launch or sync), and every launch -- those
+    # holding an IDR included -- enters the roofline's kernel time
+    stride = int(os.environ.get("BENCH_TIMING_STRIDE", "1"))
 
-    dt, step_us, sampled = timed_run(run, dist, torch, sync, stride)
+    dt, step_us, sampled, per_launch = timed_run(run, dist, torch, sync, stride)
+    split = launch_split(run, sampled, per_launch) if per_launch else None
     launches_timed = len(run.launches) - run.n_warm
     errors = eng.errors()
     timed = run.timed_pictures()
@@ -859,7 +878,7 @@ def main(argv=None):
     if staggered:
         kp = max(1, min(a.steps, run.N - 1 - a.warmup))     # pictures 1+W .. W+kp: no IDR
         run.set_plan(a.warmup, kp, [1] * S)
-        dt_p, us_p, _ = timed_run(run, dist, torch, sync, stride)
+        dt_p, us_p, _, _ = timed_run(run, dist, torch, sync, stride)
         tp = run.timed_pictures()
         p_only = {"value": round(S * kp * world / dt_p, 2), "unit": "frames/s", "steps": kp,
                   "avg_launch_kernel_us": round(us_p, 2),
@@ -940,8 +959,13 @@ def main(argv=None):
                          "ref_line_bytes_per_launch": int(launch_ref_lines),
                          "traffic_by_request_size": (traffic.get("request_size_accounting") or {}).get(
                              "dram_bytes_per_step") if traffic else None,
+                         # over the whole timed window (every launch by default),
+                         # with the launches holding an IDR and the P-only ones apart
                          "avg_launch_kernel_us": round(step_us, 2),
                          "timed_launches_sampled": len(sampled),
+                         "sampling_stride": stride,
+                         "launches_with_idr": {"n": split["i"][0], "avg_launch_kernel_us": split["i"][1]} if split else None,
+                         "launches_p_only": {"n": split["p"][0], "avg_launch_kernel_us": split["p"][1]} if split else None,
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
             "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S * P,
@@ -951,7 +975,7 @@ def main(argv=None):
                                    # rocprofv3 kernel-trace order): the timed window and
                                    # the launches the HIP events sampled
                                    "trace_window": [run.n_warm, len(run.launches)],
-                                   "trace_sampled": sampled,
+                                   "trace_sampled": sampled if len(sampled) != launches_timed else "all",
                                    "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}},
             "p_only": p_only,
             "wall_read_GBs": round(frame_read_gbs, 2),

@@ -63,12 +63,12 @@ static inline void br_init(BitReader *br, const uint8_t *buf, size_t size)
     br_refill_(br);
 }
 
-/* peek up to 32 bits (zero-padded past the end).  Logically const: only the
- * cache moves. */
-static inline uint32_t br_peek(const BitReader *cbr, int n)
+/* peek up to 32 bits (zero-padded past the end).  The position does not
+ * move, but the reader's cache may be refilled: the reader is written, so a
+ * reader shared between threads (or a const one) must be copied first */
+static inline uint32_t br_peek(BitReader *br, int n)
 {
     if (n == 0) return 0;
-    BitReader *br = (BitReader *)cbr;
     size_t off = br->pos - br->cbase;
     if (off + (size_t)n > 64) {        /* also pos < cbase: off wraps to a huge value */
         br_refill_(br);
@@ -130,7 +130,7 @@ static inline uint32_t br_te(BitReader *br, uint32_t cmax)
  * h264bsd_util.c): data remain unless at most 8 bits are left and they are
  * exactly the rbsp_stop_one_bit pattern 1 0..0 -- which is what decides
  * where a damaged (truncated) slice stops */
-static inline int br_more_rbsp_data(const BitReader *br)
+static inline int br_more_rbsp_data(BitReader *br)
 {
     if (br->pos >= br->size * 8) return br->pos > br->size * 8;   /* past the end: reference reads on */
     const size_t bits = br->size * 8 - br->pos;

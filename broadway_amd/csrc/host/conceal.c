@@ -104,7 +104,7 @@ static void conceal_plane(uint8_t *plane, int stride, int n, int x0, int y0, int
 }
 
 /* ConcealMb, neighbour-based branch, on an I420 picture of w x h MBs */
-static void conceal_mb_intra(uint8_t *img, int w, int h, int row, int col, const uint8_t *dec)
+void h264dec_conceal_mb_intra(uint8_t *img, int w, int h, int row, int col, const uint8_t *dec)
 {
     const int mb = row * w + col;
     const int A = row && dec[mb - w], B = row != h - 1 && dec[mb + w];
@@ -240,7 +240,7 @@ int h264dec_conceal(H264Dec *d, int is_i)
     }
     for (int k = 0; k < n; k++) {
         const int mb = order[k];
-        conceal_mb_intra(img, w, h, mb / w, mb % w, dec);
+        h264dec_conceal_mb_intra(img, w, h, mb / w, mb % w, dec);
         dec[mb] = 1;
     }
     /* pass 2 records: the concealed samples as I_PCM */

@@ -3,6 +3,7 @@
 #include "../common/tables.h"
 
 #include <stdlib.h>
+#include <stdatomic.h>
 #include <string.h>
 
 #include <stdio.h>
@@ -15,7 +16,17 @@ double h264dec_now(void)
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
 }
 
-static int dbg_enabled(void) { static int e = -1; if (e < 0) e = getenv("H264MI_DEBUG") != NULL; return e; }
+/* H264MI_DEBUG, read once; instances on several threads may ask first */
+static int dbg_enabled(void)
+{
+    static _Atomic int e = -1;
+    int v = atomic_load_explicit(&e, memory_order_relaxed);
+    if (v < 0) {
+        v = getenv("H264MI_DEBUG") != NULL;
+        atomic_store_explicit(&e, v, memory_order_relaxed);
+    }
+    return v;
+}
 #define DEC_FAIL(code) (dbg_enabled() ? (fprintf(stderr, "h264mi: %s:%d -> %d\n", __FILE__, __LINE__, (code)), (code)) : (code))
 #define SPS_FORCE (MAX_SPS + 1)
 #define PPS_FORCE (MAX_PPS + 1)

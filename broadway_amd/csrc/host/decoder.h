@@ -14,6 +14,10 @@
 #include "dpb.h"
 #include "picbuild.h"
 
+#ifdef __cplusplus
+extern "C" {
+#endif
+
 /* Reconstruction backend interface (the device boundary). */
 typedef struct H264Backend {
     void *ctx;
@@ -126,6 +130,10 @@ int  h264dec_valid_param_sets(const H264Dec *d);
 /* conceal the current picture's missing MBs (conceal.c); returns their
  * number or -1 */
 int  h264dec_conceal(H264Dec *d, int is_i);
+/* ConcealMb's neighbour path for the MB at (row, col) of an I420 picture of
+ * w x h MBs in host memory, reading the MBs flagged in dec (the host
+ * restatement of k_conceal; conceal.c) */
+void h264dec_conceal_mb_intra(uint8_t *img, int w, int h, int row, int col, const uint8_t *dec);
 
 /* Annex-B NAL unit location and emulation-prevention removal (decoder.c) */
 int  nal_scan(const uint8_t *bs, uint32_t len, uint32_t *init, uint32_t *size, uint32_t *read_bytes, int *emul);
@@ -142,5 +150,9 @@ int  spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes
 void spec_launch_ahead(SpecPool *sp, const H264Dec *d, const uint8_t *buf, uint32_t len);
 int  spec_active_for(const SpecPool *sp, const uint8_t *buf);
 const Sps *h264dec_active_sps(const H264Dec *d);
+
+#ifdef __cplusplus
+}
+#endif
 
 #endif

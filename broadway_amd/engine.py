@@ -198,6 +198,14 @@ class Engine:
         if self._L.h264mi_engine_set_timing_stride(self._h, int(stride)) != 0:
             raise RuntimeError("h264mi_engine_set_timing_stride failed")
 
+    def timing_list(self, cap: int = 4096):
+        """k_wgpp duration (us) of every recorded launch, in order."""
+        v = (C.c_double * cap)()
+        n = self._L.h264mi_engine_timing_list(self._h, v, int(cap))
+        if n < 0:
+            return None
+        return [float(v[i]) for i in range(n)]
+
     def timing_report(self):
         a, b, n = C.c_double(), C.c_double(), C.c_int()
         if self._L.h264mi_engine_timing_report(self._h, C.byref(a), C.byref(b), C.byref(n)) != 0:

@@ -194,6 +194,13 @@ unsigned long long h264mi_conceal_launches(void);
 /* diagnostics: engines of H264SwDec* instances taken from the pool of
  * released ones (H264MI_ENGINE_POOL) / newly created, in this process */
 void h264mi_engine_pool_stats(unsigned long long *reused, unsigned long long *created);
+/* frees every released engine and pinned output frame the pools hold (what
+ * instances still use is not touched; the library also drains at unload);
+ * returns the engines freed.  The pinned-frame pool keeps at most
+ * H264MI_HOST_POOL_MB (default 256) MB. */
+int  h264mi_pool_drain(void);
+/* pooled engines / pinned bytes held now */
+void h264mi_pool_held(int *engines, size_t *pinned_bytes);
 
 /* Device-resident variant (records already in HBM; kernel-only timing):
  * d_recs = npics*w*h MbRec in batch order with coefficient offsets relative
@@ -248,6 +255,10 @@ int  h264mi_engine_set_timing(h264mi_engine *e, int max_batches);
 /* time only every stride-th launch (default 1) */
 int  h264mi_engine_set_timing_stride(h264mi_engine *e, int stride);
 int  h264mi_engine_timing_report(h264mi_engine *e, double *inter_us, double *wave_us, int *nbatches);
+/* the recorded launches' k_wgpp durations one by one (us[i], in recording
+ * order, at most cap); returns how many (call before timing_report, which
+ * resets the record) */
+int  h264mi_engine_timing_list(h264mi_engine *e, double *us, int cap);
 /* diagnostics: per k_wgpp workgroup (row r of batch picture p at index
  * r * npics + p) 16 u64: wall-clock start/end (100 MHz) and shader-clock sums
  * of its phases, then 4 u64 per MB (chain stamps); enable != 0 allocates and

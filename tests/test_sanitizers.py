@@ -14,6 +14,7 @@ import hashlib
 import os
 import random
 import subprocess
+import shutil
 import tempfile
 
 import pytest
@@ -116,3 +117,67 @@ def test_fuzzed_streams_clean(sanitized, kind):
     concealment are expected; memory errors, UB and races are not)."""
     for i, s in enumerate(_fuzz_set(40 if kind == "asan" else 16)):
         _check_clean(_run(sanitized[kind], s), f"fuzz #{i}")
+
+
+# ---------------------------------------------------------------------------
+# The product's own threading: the H264Backend adapter of the HIP engine
+# (broadway_amd/csrc/host/hipback.cpp -- per-GPU shared engines with their
+# batch collection, 1 ms launch timeout, per-instance events and per-batch
+# result ring; the pool of released engines; the pinned output-frame pool;
+# blocking waits) with the product host path and the h264mi_dec CLI
+# (TestBenchMultipleInstance.c's N concurrent instances, one thread each),
+# built on oracle/null_device.cpp, a CPU stand-in for the GPU (HIP runtime
+# calls on host memory; engines that reconstruct with the CPU oracle, so
+# the output is still the reference's), under ThreadSanitizer and
+# AddressSanitizer + UBSan.
+
+NULL_SET = ["err_drop_slice_11x9", "err_trunc_slice_11x9", "err_range_p_11x9", "err_drop_pic_gaps_11x9",
+            "err_range_i_9x6", "ref_mmco_lt_12x8", "ref_mod_alias_12x8", "small_ip_8x6_2sl"]
+NULL_MODES = {
+    # 8 instances on one 4-lane shared engine per picture size (two 11x9
+    # engines' worth of instances: the extra ones take private engines)
+    "share4": (["-S4"], {}),
+    # private engines, released ones pooled and reused (-r2)
+    "private_pool": ([], {"H264MI_ENGINE_POOL": "1"}),
+    "private_nopool": ([], {"H264MI_ENGINE_POOL": "0"}),
+    # device concealment off: the host path reads pictures back
+    "share4_hostconceal": (["-S4"], {"H264MI_HOST_CONCEAL": "1"}),
+}
+
+
+@pytest.fixture(scope="module")
+def nulldev():
+    subprocess.check_call(["make", "-s", "nulldev"], cwd=os.path.join(ROOT, "oracle"))
+    return {k: os.path.join(BUILD, f"h264mi_dec_null_{k}") for k in ("tsan", "asan")}
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", sorted(NULL_MODES))
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_hip_backend_threads_clean(nulldev, kind, mode):
+    """8 concurrent H264SwDec instances (damaged and reference-management
+    streams of four picture sizes), each stream decoded twice, through the
+    HIP backend adapter on the null device: no sanitizer report, every
+    picture output, and the first stream's frames == the reference's."""
+    flags, extra = NULL_MODES[mode]
+    td = tempfile.mkdtemp(prefix="nulldev")
+    try:
+        paths = []
+        for i, n in enumerate(NULL_SET):
+            p = os.path.join(td, f"s{i}.h264")
+            with open(p, "wb") as f:
+                f.write(stream(CASES[n]))
+            paths.append(p)
+        out = os.path.join(td, "s0.yuv")
+        env = dict(os.environ, H264MI_PARSE_THREADS="2", H264MI_BLOCKING_SYNC="1",
+                   TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0",
+                   ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1", **extra)
+        p = subprocess.run([nulldev[kind], f"-O{out}", "-r2"] + flags + paths, capture_output=True, text=True,
+                           timeout=600, env=env)
+        _check_clean(p, f"{kind}/{mode}")
+        want = 2 * sum(len(CASES[n]["frames"]) for n in NULL_SET)
+        assert f"pictures {want} " in p.stdout, p.stdout
+        c = CASES[NULL_SET[0]]
+        assert _frames(out, c["width"] * c["height"] * 3 // 2) == c["frames"]
+    finally:
+        shutil.rmtree(td, ignore_errors=True)

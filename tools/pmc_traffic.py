@@ -66,7 +66,8 @@ def trace_window(src):
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     a, b = k["trace_window"]
     win = dur[a:b]
-    smp = [dur[i] for i in k["trace_sampled"] if i < len(dur)]
+    ts = k["trace_sampled"]
+    smp = win if ts == "all" else [dur[i] for i in ts if i < len(dur)]
     return {"k_wgpp_dispatches_in_trace": len(dur), "timed_window": [a, b],
             "rocprof_timed_window_avg_us": round(sum(win) / max(len(win), 1), 2),
             "rocprof_sampled_avg_us": round(sum(smp) / max(len(smp), 1), 2),

@@ -32,15 +32,28 @@ S = int(os.environ.get("PROF_S", "8"))
 CFG = int(os.environ.get("PROF_CONFIG", "3"))
 PIC = int(os.environ.get("PROF_PIC", "5"))
 seeds = [(100 if CFG == 3 else 1) + i for i in range(S)]
-streams, caps = bench.prepare(CFG, seeds, PIC + 1)
+# PROF_MIX=1: the bench's own GOP mix (IDRs staggered over the streams,
+# bench.gop_phases); the profiled launch is the first one in which stream
+# S-1 decodes its IDR while the others decode P pictures -- a configs[3]
+# launch that holds one I picture.  Stats below then cover that I picture
+# (PROF_SEL=i) or the P pictures of the launch (PROF_SEL=p)
+MIX = os.environ.get("PROF_MIX") == "1"
+streams, caps = bench.prepare(CFG, seeds, bench.GOP if MIX else PIC + 1)
 w, h = caps[0].w_mbs, caps[0].h_mbs
-run = bench.DeviceRun(L, caps, 0, PIC + 1, 1)
+if MIX:
+    ph = bench.gop_phases(S, min(c.npics for c in caps))
+    v_idr = (caps[0].npics - ph[S - 1]) % caps[0].npics
+    run = bench.DeviceRun(L, caps, 0, v_idr + 1, 1, phases=ph)
+else:
+    run = bench.DeviceRun(L, caps, 0, PIC + 1, 1)
 eng = run.eng
 L.h264mi_engine_profile(eng._h, 1, None, 0)
 for i in range(len(run.launches)):
     run.launch(i)
     eng.sync()
-print("kernel", eng.kernel_name(), "config", CFG, "picture", PIC, "intra" if run.is_i[PIC][0] else "inter")
+pics = list(run.launches[-1][0])          # picture of each stream in the profiled launch
+print("kernel", eng.kernel_name(), "config", CFG, "pictures", pics,
+      "types", "".join("I" if run.is_i[k][s] else "P" for s, k in enumerate(pics)))
 n = S * h * 16 + S * w * h * 8
 buf = (C.c_uint64 * n)()
 L.h264mi_engine_profile(eng._h, 1, buf, n)
@@ -55,6 +68,17 @@ m3 = lo(m[..., 3])
 base = min(Cst[Cst > 0].min(), m3[m3 > 0].min())
 us = lambda x: ((x - base) % (1 << 32)) / 100.0
 A, B, Cst, D, E = us(A), us(B), us(Cst), us(D), us(E)
+print("per picture: row 0 end / row h-2 end (us):",
+      " ".join(f"{'I' if run.is_i[k][s] else 'P'}{s}:{D[s, 0, w - 1]:.0f}/{D[s, h - 2, w - 1]:.0f}" for s, k in enumerate(pics)))
+SEL = os.environ.get("PROF_SEL", "i" if MIX else "")
+if SEL:
+    keep = [s for s, k in enumerate(pics) if run.is_i[k][s] == (SEL == "i")]
+    print(f"stats below: pictures {keep} ({'I' if SEL == 'i' else 'P'} only)")
+    m = m[keep]
+    A, B, Cst, D, E = A[keep], B[keep], Cst[keep], D[keep], E[keep]
+    pics = [pics[s] for s in keep]
+    caps = [caps[s] for s in keep]
+    S = len(keep)
 
 rows = slice(8, h - 1)        # deep rows, not the last (no publish)
 cols = slice(2, w - 2)
@@ -118,7 +142,7 @@ print(f"  row 0 end (us, mean over pictures): {D[:, 0, w - 1].mean():.1f}; row {
 # slot (left, LDS flag) and the row above's unfiltered bottom row up to
 # column c+1 (mailbox dwords 24..31 through L2).
 M0, M1 = us(lo(m[..., 3])), us(hi(m[..., 3]))
-types = np.stack([np.frombuffer(caps[s].records_bytes(PIC), np.uint8).reshape(h, w, 96)[..., 0] for s in range(S)])
+types = np.stack([np.frombuffer(caps[s].records_bytes(pics[s]), np.uint8).reshape(h, w, 96)[..., 0] for s in range(S)])
 intra = (types == 2) | (types == 3)     # I4x4 / I16x16 (I_PCM is a copy)
 print(f"MC: {intra.mean() * 100:.1f} % intra MBs; MC slot-final of row 0's last MB {M1[:, 0, w - 1].mean():.1f} us, "
       f"of row {h - 1}'s {M1[:, h - 1, w - 1].mean():.1f} us")

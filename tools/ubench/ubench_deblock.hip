@@ -1,47 +1,82 @@
-// Micro-benchmark: cycles of one deblock_dir() pass (k_rows' per-MB filter)
-// for one wave, on an LDS region filled with pseudo-random samples and a
-// P-frame-like deblocking record.  Diagnostics only.
+// Micro-benchmark (diagnostics only): shader cycles of one lone wave's
+// deblocking passes, deblock_dir() of recon_kernels.hip on a PPRegion in LDS
+// filled with pseudo-random samples, and of the bare filter arithmetic
+// (filt_line on registers, 4 edges), per bS mode:
+//   0: MB edge bS 2, internal edges 0      (skip-like P MBs)
+//   1: every edge bS 2                     (coded P MBs)
+//   2: MB edge bS 4, internal edges 3      (intra MBs)
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 ubench_deblock.hip -o ubench_deblock
 #include "../../broadway_amd/csrc/hip/recon_kernels.hip"
 #include <stdio.h>
 
 __global__ __launch_bounds__(64) void k_ub(unsigned long long *out, int iters, int bsmode)
 {
-    __shared__ RowLds L;
+    __shared__ PPRegion G;
+    __shared__ uint8_t junk[256];
     const int lane = threadIdx.x;
-    for (int i = lane; i < (int)sizeof(RowLds); i += 64) ((uint8_t *)&L)[i] = (uint8_t)(100 + ((i * 37) & 15));
+    for (int i = lane; i < (int)sizeof(PPRegion); i += 64) ((uint8_t *)&G)[i] = (uint8_t)(100 + ((i * 37) & 15));
     __syncthreads();
-    if (lane < 16) {
-        // bS: mode 0 = MB edges 2, internal 0; mode 1 = all 2; mode 2 = MB edge 4, internal 3
-        uint16_t w = bsmode == 0 ? 0x0002 : bsmode == 1 ? 0x2222 : 0x3334;
-        ((uint16_t *)L.db)[lane] = w;
+    if (lane < 8) {
+        const uint16_t w = bsmode == 0 ? 0x0002 : bsmode == 1 ? 0x2222 : 0x3334;
+        ((uint16_t *)G.db)[lane] = w;
     }
     if (lane < 6) {
-        uint8_t *o = L.db + 16 + lane * 8;
+        uint8_t *o = G.db + 16 + lane * 8;
         o[0] = 40; o[1] = 10; o[2] = 1; o[3] = 2; o[4] = 3; o[5] = 30; o[6] = o[7] = 0;
     }
     __syncthreads();
     unsigned long long t0 = clock64();
     for (int it = 0; it < iters; it++) {
-        deblock_dir(0, L.db, L.ry, L.ru, L.rv, lane, true);
+        deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, true);
         wave_sync();
     }
     unsigned long long t1 = clock64();
     for (int it = 0; it < iters; it++) {
-        deblock_dir(1, L.db, L.ry, L.ru, L.rv, lane, true);
+        deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, true);
         wave_sync();
     }
     unsigned long long t2 = clock64();
-    if (lane == 0) { out[0] = (t1 - t0) / iters; out[1] = (t2 - t1) / iters; out[2] = L.ry[100]; }
+    // the filter arithmetic alone: 4 dependent edges on a register line
+    int v[20];
+    for (int j = 0; j < 20; j++) v[j] = 100 + ((lane * 7 + j * 13) & 15);
+    const int bS0 = bsmode == 2 ? 4 : 2, bSi = bsmode == 0 ? 0 : bsmode == 1 ? 2 : 3;
+    for (int it = 0; it < iters; it++) {
+        filt_line<true>(v, 0, bS0, 40, 10, 10, 0x03020100u);
+        for (int k = 1; k < 4; k++) filt_line<false>(v, k, bSi, 40, 10, 10, 0x03020100u);
+    }
+    unsigned long long t3 = clock64();
+    int acc = 0;
+    for (int j = 0; j < 20; j++) acc += v[j];
+    if (lane == 0) {
+        out[0] = (t1 - t0) / iters; out[1] = (t2 - t1) / iters; out[2] = (t3 - t2) / iters;
+        out[3] = G.ry[100] + acc;
+    }
+}
+
+// wall-clock (100 MHz) against shader clock over the same loop: the clock
+// the passes ran at
+__global__ void k_clk(unsigned long long *out)
+{
+    const unsigned long long w0 = wall_clock64(), c0 = clock64();
+    unsigned long long w1;
+    do { w1 = wall_clock64(); } while (w1 - w0 < 100000);
+    const unsigned long long c1 = clock64();
+    if (threadIdx.x == 0) { out[0] = w1 - w0; out[1] = c1 - c0; }
 }
 
 int main()
 {
-    unsigned long long *d, h[3];
-    hipMalloc(&d, 64);
+    unsigned long long *d, h[4];
+    (void)hipMalloc(&d, 64);
+    hipLaunchKernelGGL(k_clk, dim3(1), dim3(64), 0, 0, d);
+    (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+    const double mhz = (double)h[1] / (double)h[0] * 100.0;
+    printf("shader clock %.0f MHz\n", mhz);
     for (int mode = 0; mode < 3; mode++) {
-        hipLaunchKernelGGL(k_ub, dim3(1), dim3(64), 0, 0, d, 200, mode);
-        hipMemcpy(h, d, 24, hipMemcpyDeviceToHost);
-        printf("bsmode %d: V %llu cycles, H %llu cycles\n", mode, h[0], h[1]);
+        hipLaunchKernelGGL(k_ub, dim3(1), dim3(64), 0, 0, d, 2000, mode);
+        (void)hipMemcpy(h, d, 32, hipMemcpyDeviceToHost);
+        printf("bsmode %d: V %llu cycles (%.3f us), H %llu cycles (%.3f us), filt x4 %llu cycles\n", mode,
+               h[0], h[0] / mhz, h[1], h[1] / mhz, h[2]);
     }
     return 0;
 }
