@@ -359,14 +359,84 @@ def rgba_leg(torch, L, eng, S, w_mbs, h_mbs, reps=50):
                     "MALL, the RGBA output is written with non-temporal stores"}
 
 
-def end_to_end(streams, nframes, reps=3):
+def parse_cpulist(text: str):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]"""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def format_cpulist(cpus) -> str:
+    """[0, 1, 2, 3, 8] -> '0-3,8'"""
+    cpus, parts, i = sorted(set(cpus)), [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        parts.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(parts)
+
+
+def gpu_numa_node(torch, dev: int) -> int:
+    """NUMA node of HIP device `dev`, from sysfs of its PCI function; -1 when
+    unknown (no GPU, no sysfs entry)."""
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        path = f"/sys/bus/pci/devices/{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0/numa_node"
+        with open(path) as f:
+            return int(f.read().strip())
+    except (OSError, ValueError, AttributeError, RuntimeError, AssertionError):
+        return -1
+
+
+def node_cpus(node: int):
+    """Host cores of NUMA node `node` (sysfs), or None."""
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            return parse_cpulist(f.read())
+    except (OSError, ValueError):
+        return None
+
+
+def e2e_core_plan(local: int, numa, allowed):
+    """Host cores for each local rank's end-to-end decoder processes
+    (each GPU has its own host parse threads on a NUMA-local core
+    set): rank j gets an equal, disjoint share of the cores it may use on its
+    GPU's NUMA node (numa[j], -1 = unknown), split among the local ranks whose
+    GPUs sit on that node; a node without usable cores falls back to an equal
+    share of every allowed core.  Returns (this rank's cores, the plan of
+    every local rank)."""
+    allowed = sorted(set(allowed))
+    plan = []
+    for j, n in enumerate(numa):
+        pool = None
+        if n >= 0:
+            nc = node_cpus(n)
+            pool = sorted(set(nc) & set(allowed)) if nc else None
+            peers = [k for k, m in enumerate(numa) if m == n]
+        if not pool:
+            pool, peers = allowed, list(range(len(numa)))
+        k, m = peers.index(j), len(peers)
+        share = len(pool) // m
+        plan.append(pool[k * share:(k + 1) * share] if share else pool[k % len(pool):k % len(pool) + 1])
+    return plan[local], plan
+
+
+def end_to_end(streams, nframes, reps=3, device=0, cpus=None):
     """End-to-end decode through the product C-ABI: one
     broadway_amd/lib/h264mi_dec process per stream (at most MAX_E2E_PROCS),
     all in parallel (one host thread each), each decoding its stream `reps`
     times -- host CAVLC parse, H2D of the MB records, k_prep + k_wgpp, D2H of
     every output picture.  Rate = all pictures / the slowest process's decode
     time (HIP start-up of each process excluded; it is paid before its timed
-    loop)."""
+    loop).  The processes decode on GPU `device` (H264MI_DEVICE) and, given
+    `cpus`, run pinned to those host cores (h264mi_dec -A: the process and
+    every thread it starts)."""
     from broadway_amd import _lib
     exe = os.path.join(_lib.LIB_DIR, "h264mi_dec")      # H264MI_LIB_DIR: an A/B build's
     if not os.path.exists(exe):
@@ -380,6 +450,8 @@ def end_to_end(streams, nframes, reps=3):
     # 2 slice workers each (profiles/r51_host_ab.txt: 5.9 vs 6.4 ms host CPU
     # per picture with 3 workers, same rate); the library default stays 3
     env.setdefault("H264MI_PARSE_THREADS", "2")
+    env["H264MI_DEVICE"] = str(device)
+    pin = [f"-A{format_cpulist(cpus)}"] if cpus else []
     td = tempfile.mkdtemp(prefix="h264e2e")
     try:
         procs = []
@@ -387,7 +459,7 @@ def end_to_end(streams, nframes, reps=3):
             pth = os.path.join(td, f"s{i}.h264")
             with open(pth, "wb") as f:
                 f.write(s)
-            procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T", pth], stdout=subprocess.PIPE,
+            procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T"] + pin + [pth], stdout=subprocess.PIPE,
                                           stderr=subprocess.PIPE, text=True, env=env))
         secs, pics, parts, cpu_s, sys_s = [], 0, {}, 0.0, 0.0
         for pr in procs:
@@ -410,6 +482,9 @@ def end_to_end(streams, nframes, reps=3):
                     sys_s += float(f[1])
         t = max(secs)
         res = {"value": round(pics / t, 2), "unit": "frames/s", "host_threads": len(streams),
+               "pictures": pics, "seconds": round(t, 6), "device": device,
+               "host_cores_assigned": len(cpus) if cpus else None,
+               "cpus": format_cpulist(cpus) if cpus else None,
                "sample": f"{len(streams)} x {nframes}-frame 1080p streams x {reps} passes, one h264mi_dec process "
                          f"(H264SwDec* C-ABI) per stream: host parse + H2D + kernels + D2H of every picture; "
                          f"{pics} frames in {t:.2f} s"}
@@ -427,7 +502,7 @@ def end_to_end(streams, nframes, reps=3):
         # the same streams in ONE process, one thread (H264SwDec instance) per
         # stream, sharing one batched engine (h264mi_set_share, -S)
         paths = [os.path.join(td, f"s{i}.h264") for i in range(len(streams))]
-        o = subprocess.run([exe, "-Onone", f"-r{reps}", "-T", f"-S{len(streams)}"] + paths, capture_output=True,
+        o = subprocess.run([exe, "-Onone", f"-r{reps}", "-T", f"-S{len(streams)}"] + pin + paths, capture_output=True,
                            text=True, timeout=600, env=env)
         if o.returncode == 0:
             d = {}
@@ -910,9 +985,32 @@ def main(argv=None):
     legs = None
     if rank == 0 and world == 1 and not a.no_legs and not a.dry_run:
         legs = config_legs(L, torch)
+    # end-to-end drop-in path on every rank: its own h264mi_dec processes on
+    # its own GPU, pinned to a disjoint, NUMA-local host-core share
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    numa = [-1 if a.dry_run else gpu_numa_node(torch, j) for j in range(local_world)]
+    my_cpus, _ = e2e_core_plan(local, numa, os.sched_getaffinity(0))
+    e2e_plan = {"rank": rank, "device": local, "numa_node": numa[local] if local < len(numa) else -1,
+                "cpus": format_cpulist(my_cpus), "host_cores": len(my_cpus)}
     e2e = None
-    if rank == 0 and world == 1 and not a.no_e2e and not a.dry_run:
-        e2e = end_to_end(streams, nframes)
+    if not a.no_e2e and not a.dry_run:
+        if dist:
+            dist.barrier()
+        e2e = end_to_end(streams, nframes, device=local, cpus=my_cpus if world > 1 else None)
+    if dist:
+        plans, e2es = [None] * world, [None] * world
+        dist.all_gather_object(plans, e2e_plan)
+        dist.all_gather_object(e2es, e2e)
+        if e2e is not None and all(x is not None for x in e2es):
+            # all ranks decoded at once: every rank's pictures over the slowest rank's time
+            e2e = {"value": round(sum(x["pictures"] for x in e2es) / max(x["seconds"] for x in e2es), 2),
+                   "unit": "frames/s", "n_gpus": world,
+                   "host_cores_total": sum(x["host_cores_assigned"] or 0 for x in e2es),
+                   "host_cpu_ms_per_picture": round(sum(x.get("host_cpu_ms_per_picture", 0) * x["pictures"] for x in e2es)
+                                                    / max(sum(x["pictures"] for x in e2es), 1), 3),
+                   "per_rank": e2es}
+    else:
+        plans = [e2e_plan]
 
     if rank == 0:
         mix = (f"IDRs staggered: stream s enters the timed window s*{run.N}/{S} pictures into its GOP "
@@ -981,6 +1079,7 @@ def main(argv=None):
             "wall_read_GBs": round(frame_read_gbs, 2),
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "end_to_end_plan": plans,
             "rgba_output": rgba,
             "config_legs": legs,
             "bitexact_check": {"ok": ok_all, "frames_checked": n_checked_all,

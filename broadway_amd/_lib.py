@@ -178,8 +178,13 @@ def mi() -> C.CDLL:
     L.h264mi_engine_set_timing_stride.restype = i32
     L.h264mi_engine_timing_report.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i32)]
     L.h264mi_engine_timing_report.restype = i32
-    L.h264mi_engine_timing_list.argtypes = [vp, C.POINTER(C.c_double), i32]
-    L.h264mi_engine_timing_list.restype = i32
+    # (round-4 additions; absent from older builds loaded for A/B timing)
+    if hasattr(L, "h264mi_engine_error_bits"):
+        L.h264mi_engine_error_bits.argtypes = [vp]
+        L.h264mi_engine_error_bits.restype = C.c_uint32
+    if hasattr(L, "h264mi_engine_timing_list"):
+        L.h264mi_engine_timing_list.argtypes = [vp, C.POINTER(C.c_double), i32]
+        L.h264mi_engine_timing_list.restype = i32
     L.h264mi_engine_profile.argtypes = [vp, i32, C.POINTER(C.c_uint64), sz]
     L.h264mi_engine_profile.restype = i32
     L.h264mi_engine_frame_ptr.argtypes = [vp, i32, i32]

@@ -77,6 +77,9 @@ struct h264mi_engine {
     uint8_t *d_rgba;          // h264mi_engine_read_rgba staging (w*h*4 B, allocated on first use)
     int steps;                // pictures per stream per launch (h264mi_engine_set_steps)
     unsigned *d_done;         // per picture row of a launch: epoch tag once the row is final in its slot
+    int check;                // H264MI_CHECK=1: the dependency-checker kernels (recon_kernels.hip CHK_*)
+    int check_inject;         // H264MI_CHECK_INJECT: test hook (ReconArgs::chk_inject)
+    uint32_t err_bits;        // OR of every picture's device flags since the last h264mi_engine_error_bits
 };
 
 // per-picture buffers of one launch (deblocking records, residuals, row
@@ -122,6 +125,8 @@ static void engine_config(h264mi_engine *e)
     const char *mw = getenv("H264MI_MC_WAVES");
     e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
     e->launch_intra = -1;
+    e->check = getenv("H264MI_CHECK") && atoi(getenv("H264MI_CHECK"));
+    e->check_inject = getenv("H264MI_CHECK_INJECT") ? atoi(getenv("H264MI_CHECK_INJECT")) : 0;
     const char *rp = getenv("H264MI_RPW");
     e->rpw_env = rp ? atoi(rp) : 0;
     if (e->rpw_env < 0 || e->rpw_env > 3) e->rpw_env = 0;
@@ -146,6 +151,16 @@ static void engine_config(h264mi_engine *e)
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 1, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 2, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 2, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 3, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
     e->rpw_max = e->mc_waves == 2 ? 2 : 3;
@@ -326,6 +341,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     a.mc_lead = mc_lead;
     static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 0;
     a.row_prio_split = row_prio;
+    a.chk_inject = e->check ? e->check_inject : 0;
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;
@@ -369,6 +385,17 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         else if (rpw == 2) hipLaunchKernelGGL((k_wgpp<3, true, true, 2>), grid, dim3(640), lmbx, e->st, a);
         else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, true, true, 1>), grid, dim3(256), lmbx, e->st, a);
         else hipLaunchKernelGGL((k_wgpp<3, true, true, 1>), grid, dim3(320), lmbx, e->st, a);
+        if (rec) (void)hipEventRecord(t2, e->st);
+    } else if (e->check) {
+        // dependency checker (H264MI_CHECK=1): every hand-off verified at
+        // its consumer, violations in the pictures' error words
+        e->last_kernel = "k_wgpp_check";
+        if (rec) (void)hipEventRecord(t0, e->st);
+        if (rpw == 3) hipLaunchKernelGGL((k_wgpp<3, false, true, 3, true>), grid, dim3(960), lmbx, e->st, a);
+        else if (rpw == 2 && nmc == 2) hipLaunchKernelGGL((k_wgpp<2, false, true, 2, true>), grid, dim3(512), lmbx, e->st, a);
+        else if (rpw == 2) hipLaunchKernelGGL((k_wgpp<3, false, true, 2, true>), grid, dim3(640), lmbx, e->st, a);
+        else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, false, true, 1, true>), grid, dim3(256), lmbx, e->st, a);
+        else hipLaunchKernelGGL((k_wgpp<3, false, true, 1, true>), grid, dim3(320), lmbx, e->st, a);
         if (rec) (void)hipEventRecord(t2, e->st);
     } else if (nmc == 2) {
         // sizing study (H264MI_MC_WAVES=2): two MC waves per row workgroup
@@ -558,7 +585,10 @@ extern "C" int h264mi_engine_sync(h264mi_engine *e)
     // a blocking-sync event: the waiting thread sleeps whatever the device's
     // scheduling flags (which take effect only before the first context)
     if (engine_wait(e)) return -1;
-    for (int i = 0; i < e->pipe_cap; i++) e->err_accum += e->h_err[i] ? 1 : 0;
+    for (int i = 0; i < e->pipe_cap; i++) {
+        e->err_accum += e->h_err[i] ? 1 : 0;
+        e->err_bits |= e->h_err[i];
+    }
     return 0;
 }
 
@@ -572,6 +602,14 @@ extern "C" uint32_t h264mi_engine_errors(h264mi_engine *e)
     if (!e) return 0;
     uint32_t v = e->err_accum;
     e->err_accum = 0;
+    return v;
+}
+
+extern "C" uint32_t h264mi_engine_error_bits(h264mi_engine *e)
+{
+    if (!e) return 0;
+    const uint32_t v = e->err_bits;
+    e->err_bits = 0;
     return v;
 }
 

@@ -71,7 +71,29 @@ struct ReconArgs {
     // chain (slot waits, copy-in, frame stores) and 3 on it (hdone wait ..
     // publish); 0 = 3 throughout
     int row_prio_split;
+    // dependency-checker builds (k_wgpp<..., CHK = true>): test hook that
+    // deliberately breaks one hand-off so the tests can see the checker fire
+    // (0: none; 1: MB 5 of every row hands the row waves a wrong ring tag)
+    int chk_inject;
 };
+
+// Dependency checker (the reference's compile-time
+// _ASSERT_USED / _RANGE_CHECK knobs, h264bsd_util.h:35-123): in the CHK
+// instantiations of k_wgpp every hand-off is verified at the consumer, each
+// kind of violation setting its own bit of the picture's error word:
+//   CHK_RING    the MC ring slot the row waves read holds another MB's data
+//   CHK_RING_WR an MC wave writes a slot the row waves have not released
+//   CHK_REGION  the partner row wave's region holds another MB than the one
+//               whose H pass its hdone announced
+//   CHK_PROG    an intra progress word names another MB than the left one
+//   CHK_REFROW  (frame-pipelined launches) a reference line is read from a
+//               picture of the same launch before every row holding a byte
+//               of it was tagged final -- checks the host's set_ref_rows
+#define CHK_RING    64u
+#define CHK_RING_WR 128u
+#define CHK_REGION  256u
+#define CHK_PROG    512u
+#define CHK_REFROW  1024u
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 __constant__ uint8_t cLevelScale[6][3] = {
@@ -639,14 +661,18 @@ struct LeftNb {
     int *my_lprog, *my_cprog;       // this MB's
     int ltag, mytag;                // (c - 1) << 4, c << 4
     unsigned *perr;
+    bool chk;                       // dependency checker: the word must name the left MB
 };
-__device__ __forceinline__ void prog_wait(const int *p, int want, int lane, unsigned *perr)
+__device__ __forceinline__ void prog_wait(const int *p, int want, int lane, unsigned *perr, bool chk = false)
 {
     unsigned spins = 0;
-    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < want) {
+    int v;
+    while ((v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) < want) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }   // bounded wait
     }
+    // a later MB in the same ring slot also passes `< want`
+    if (chk && (v >> 4) != (want >> 4) && lane == 0) atomicOr(perr, CHK_PROG);
     wave_sync();
 }
 __device__ __forceinline__ void prog_set(int *p, int v, int lane)
@@ -673,7 +699,7 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
     const bool aA = avail & AV_A, aB = avail & AV_B;
     {   // chroma: lane -> (comp, row, pair), straight into the slot
         if (aA) {
-            prog_wait(N.cprog, N.ltag | 1, lane, N.perr);
+            prog_wait(N.cprog, N.ltag | 1, lane, N.perr, N.chk);
             if (lane < 16) {
                 const int k = lane & 7, comp = lane >> 3;
                 (comp ? tv : tu)[(k + 1) * TC_STRIDE + TX0 - 1] = N.lp[256 + comp * 64 + k * 8 + 7];
@@ -728,7 +754,7 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
     }
     if (mbtype == MBT_I16) {
         if (aA) {
-            prog_wait(N.lprog, N.ltag | 10, lane, N.perr);
+            prog_wait(N.lprog, N.ltag | 10, lane, N.perr, N.chk);
             if (lane < 16) ty[(lane + 1) * TY_STRIDE + TX0 - 1] = N.lp[lane * 16 + 15];
             wave_sync();
         }
@@ -816,7 +842,7 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
             // the left MB's block beside it (5, 7, 13, 15: its steps 3, 5, 7, 9)
             if ((s & 1) == 0 && s <= 6 && aA) {
                 const int by = s == 0 ? 0 : s == 2 ? 1 : s == 4 ? 2 : 3;
-                prog_wait(N.lprog, N.ltag | (s + 4), lane, N.perr);
+                prog_wait(N.lprog, N.ltag | (s + 4), lane, N.perr, N.chk);
                 if (lane < 4) ty[(by * 4 + lane + 1) * TY_STRIDE + TX0 - 1] = N.lp[(by * 4 + lane) * 16 + 15];
                 wave_sync();
             }
@@ -1081,6 +1107,7 @@ struct __attribute__((aligned(16))) MbRing {
     // I4x4 steps whose samples are in px (10: all luma), cprog n = 1 once its
     // chroma is -- the next MB's intra reads its left neighbours as they land
     int lprog[RK], cprog[RK];
+    int tag[RK];            // dependency checker: the MB whose data the slot holds
     int consumed;
 };
 
@@ -1111,7 +1138,7 @@ template <bool UPL, int RK>
 __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigned long long *mbx_up, g_u32 *perr_g,
                                                    int W, int c, uint32_t tag, bool has_up, int lane, lds_McScratch *Ml,
                                                    __attribute__((address_space(3))) MbRing<RK> *Rl, lds_cu32 *i4tab_l,
-                                                   __attribute__((address_space(1))) unsigned long long *pst)
+                                                   __attribute__((address_space(1))) unsigned long long *pst, bool chk)
 {
     // pst (profiling build): [0] left ready | top ready, [1] prediction done | slot written
     unsigned long long st0 = 0, st1 = 0;
@@ -1177,6 +1204,7 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     N.my_lprog = &R.lprog[slot]; N.my_cprog = &R.cprog[slot];
     N.ltag = (c - 1) << 4; N.mytag = c << 4;
     N.perr = perr;
+    N.chk = chk;
     intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
     if (pst) st1 = wall_clock64();
     if (pst && lane == 0) { pst[0] = st0; pst[1] = (st1 & 0xFFFFFFFFull) | (wall_clock64() << 32); }
@@ -1210,6 +1238,7 @@ struct __attribute__((aligned(16))) PPRegion {
     uint8_t ry[20 * RY_S];      // rows -4..15, cols -4..15
     uint8_t ru[10 * RC_S];      // rows -2..7, cols -4..7
     uint8_t rv[10 * RC_S];
+    int tag[4];                 // dependency checker: the MB in the region (after its H pass)
 };
 struct __attribute__((aligned(16))) PPLds {
     PPRegion G[2];
@@ -1222,7 +1251,7 @@ struct __attribute__((aligned(16))) PPLds {
 // UPL / MEL: the row above's mailbox (mbx_up) / this row's (mbx_me) is the
 // workgroup's LDS one (k_wgpp RPW = 2: the upper row of the pair publishes to
 // LDS, the lower one reads from there)
-template <bool PROF, bool UPL, bool MEL, int RK>
+template <bool PROF, bool UPL, bool MEL, int RK, bool CHK>
 __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing<RK> *R,
                        const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
@@ -1407,6 +1436,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         }
         wave_sync();
         PPT(7);
+        if (CHK && __builtin_amdgcn_readfirstlane(lds_ld(&R->tag[slot])) != c && lane == 0) atomicOr(perr, CHK_RING);
         {
             const uint32_t oy = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
             const uint32_t oc = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
@@ -1426,6 +1456,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             }
             wave_sync();
             PPT(3);
+            if (CHK && __builtin_amdgcn_readfirstlane(lds_ld(&Gp.tag[0])) != c - 1 && lane == 0) atomicOr(perr, CHK_REGION);
             if (prof && lane == 0) tva = wall_clock64();
             const uint32_t hv = *(const uint32_t *)((const uint8_t *)&Gp + cp_src);
             *(uint32_t *)(Lb + cp_dst) = hv;
@@ -1464,6 +1495,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_TOP);
             wave_sync();
         }
+        if (CHK && lane == 0) lds_st(&G.tag[0], c);
         if (lane == 0) lds_st(&L.hdone, c + 1);
         if (prof && lane == 0) tvd = wall_clock64();
         PPT(2);
@@ -1491,6 +1523,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                     qdw = *(const uint32_t *)&R->px[s1][pq_off];
                     bsw = dbn[1]; t0 = dbn[pchroma ? 12 : 6]; t1 = dbn[pchroma ? 13 : 7];
                 }
+                if (CHK && __builtin_amdgcn_readfirstlane(lds_ld(&R->tag[s1])) != c + 1 && lane == 0) atomicOr(perr, CHK_RING);
                 const uint32_t pdw = ent;
                 int v[20];
 #pragma unroll
@@ -1833,10 +1866,74 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
         prep_mb(pa, g, lane, wid < NM ? M[wid] : Mx[wid - NM], R.db[wid], T);
 }
 
+// Dependency checker, frame-pipelined launches: the rows of the in-launch
+// producer picture that MB mb's reference loads need final, from the loads'
+// own geometry (mc_issue's windows, at 128-B line granularity, each line's
+// first and last byte and the last byte before a plane boundary it crosses),
+// must all be among the leading rows dep_wait saw done (D.known) -- i.e. the
+// host's set_ref_rows (capture.c) covered every line the kernel reads.  Rows
+// 0..R+1 done make MB row R's bytes final (row R+1 stores R's rows 12..15).
+__device__ __forceinline__ int chk_need_of(uint32_t o, uint32_t ysz, uint32_t csz, int W16, int CW, int h)
+{
+    // MB rows whose workgroups must be done for byte o of a slot to be final
+    const int R = o < ysz ? (int)(o / (uint32_t)W16) >> 4
+                          : (int)(((o < ysz + csz ? o - ysz : o - ysz - csz)) / (uint32_t)CW) >> 3;
+    return min(R + 2, h);
+}
+__device__ __forceinline__ int chk_line_need(uint32_t off, uint32_t len, uint32_t ysz, uint32_t csz, int W16, int CW, int h)
+{
+    const uint32_t l0 = off & ~127u, l1 = min(((off + len - 1) | 127u), ysz + 2 * csz - 1);
+    int n = max(chk_need_of(l0, ysz, csz, W16, CW, h), chk_need_of(l1, ysz, csz, W16, CW, h));
+    if (l0 < ysz && l1 >= ysz) n = max(n, chk_need_of(ysz - 1, ysz, csz, W16, CW, h));
+    if (l0 < ysz + csz && l1 >= ysz + csz) n = max(n, chk_need_of(ysz + csz - 1, ysz, csz, W16, CW, h));
+    return n;
+}
+// (out of line, plain-value arguments: see mc_intra)
+__device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *perr, int mb, uint32_t v0, int lane, int dslot,
+                                                       int known)
+{
+    const uint32_t d0 = rec_dw(v0, 0), refs = rec_dw(v0, 6);
+    if ((d0 & 255) >= MBT_I4x4) return;
+    struct { int w, h; } a = {aw, ah};
+    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
+    const uint32_t ysz = (uint32_t)W16 * H16, csz = (uint32_t)CW * CH;
+    const int mbx = mb % a.w, mby = mb / a.w;
+    int need = 0;
+    {   // luma: lane -> block lb, window rows lsub + 4k (mc_issue)
+        const int lb = lane >> 2, lsub = lane & 3;
+        const uint32_t mvl = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + lb) << 2, (int)v0);
+        if ((int)((refs >> ((lb >> 2) * 8)) & 255) == dslot) {
+            const int mvx = (int)(int16_t)(mvl & 0xFFFF), mvy = (int)(int16_t)(mvl >> 16);
+            const int x0 = clip3(0, W16 - 12, (mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2) & ~3);
+            const int y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int y = clip3(0, H16 - 1, y0 + min(lsub + 4 * k, 8));
+                need = max(need, chk_line_need((uint32_t)(y * W16 + x0), 12, ysz, csz, W16, CW, a.h));
+            }
+        }
+    }
+    {   // chroma: lane -> block cb, component
+        const int cb = (lane & 31) >> 1, ccomp = lane & 1;
+        const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
+        if ((int)((refs >> ((cb >> 2) * 8)) & 255) == dslot) {
+            const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
+            const int x0 = clip3(0, CW - 8, (mbx * 8 + blk_x(cb) * 2 + (cmx >> 3)) & ~3);
+            const int y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3);
+#pragma unroll
+            for (int wy = 0; wy < 3; wy++) {
+                const int y = clip3(0, CH - 1, y0 + wy);
+                need = max(need, chk_line_need(ysz + (uint32_t)ccomp * csz + (uint32_t)(y * CW + x0), 8, ysz, csz, W16, CW, a.h));
+            }
+        }
+    }
+    if (__builtin_amdgcn_ballot_w64(need > known) != 0 && lane == 0) atomicOr((unsigned *)perr, CHK_REFROW);
+}
+
 // MC waves of one row (picture p, MB row r): walk the row's MBs c0, c0 + NMC,
 // ... into the row's LDS ring.  UPL / MEL as row_pp: where the row above's
 // unfiltered bottom rows come from (intra) / where this row's go.
-template <int NMC, bool PROF, bool UPL, bool MEL, int RK>
+template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK>
 __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing<RK> &R,
                                        const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
@@ -1859,6 +1956,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     uint32_t v0 = c0 < a.w ? recrow[(size_t)c0 * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
     if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
+    if (CHK && c0 < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c0, v0, lane, (int)D.slot[0], D.known[0]);
     if (c0 < a.w) mc_issue(a, pd, p, r * a.w + c0, v0, lane, ld);
     const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
     const int lead0 = a.mc_lead0 > 0 && a.mc_lead0 < lead ? a.mc_lead0 : lead;
@@ -1879,6 +1977,9 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             }
             wave_sync();
         }
+        // the slot held MB c - RK: the row waves must have released it
+        if (CHK && c >= RK && __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < c - RK + 1 && lane == 0)
+            atomicOr(a.err + p, CHK_RING_WR);
         const unsigned long long t0 = PROF ? wall_clock64() : 0;      // MB c's MC start (ring slot free)
         if (NMC == 2) {
             // urgency (2-MC-wave workgroups, 3 per CU): an MC wave whose row
@@ -1898,7 +1999,8 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             mc_intra<UPL, RK>((g_MbRec *)(a.rec + pd.rec_base + r * a.w + c), mbx_up, (g_u32 *)(a.err + p), a.w, c, a.epoch,
                               r > 0, lane, (lds_McScratch *)&Mw, (__attribute__((address_space(3))) MbRing<RK> *)&R,
                               (lds_cu32 *)i4tab,
-                              (__attribute__((address_space(1))) unsigned long long *)(PROF ? a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4 : nullptr));
+                              (__attribute__((address_space(1))) unsigned long long *)(PROF ? a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4 : nullptr),
+                              CHK);
         }
         wave_sync();
         {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
@@ -1911,12 +2013,14 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         if (PROF && lane == 0)
             a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 3] = (t0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
         if (lane == 0) {
+            if (CHK) lds_st(&R.tag[slot], c ^ (a.chk_inject == 1 && c == 5 ? 1 : 0));
             lds_st(&R.lprog[slot], (c << 4) | 10);
             lds_st(&R.cprog[slot], (c << 4) | 1);
             lds_st(&R.flag[slot], c + 1);
         }
         v0 = nv0;
         if (more && D.n) dep_wait(a, p, v0, lane, D);
+        if (CHK && more && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c + NMC, v0, lane, (int)D.slot[0], D.known[0]);
         if (more) mc_issue(a, pd, p, r * a.w + c + NMC, v0, lane, ld);
     }
 }
@@ -1950,7 +2054,7 @@ struct WgppLds {
 #define WGPP_WAVES_PER_EU 4
 #endif
 
-template <int NMC, bool PROF, bool PREP, int RPW>
+template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false>
 __global__ __launch_bounds__(64 * (NMC + 2) * RPW)
 __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : 3))) void k_wgpp(ReconArgs a)
 {
@@ -1975,8 +2079,14 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
     const int j = jg / hg, g = jg - j * hg, p = j * S + s;
     for (int q = 0; q < RPW; q++) {
-        if (threadIdx.x < RK) { R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1; }
-        if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
+        if (threadIdx.x < RK) {
+            R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1;
+            R[q].tag[threadIdx.x] = -1;
+        }
+        if (threadIdx.x == 0) {
+            R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0;
+            L[q].G[0].tag[0] = L[q].G[1].tag[0] = -1;
+        }
     }
     for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
         L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
@@ -1997,10 +2107,10 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     unsigned long long *const me = mel ? lmbx + q * W32 : a.mbx + ((size_t)p * a.h + r) * W32;
     if (wid < 2) {
         __builtin_amdgcn_s_setprio(3);
-        if (!upl && !mel) row_pp<PROF, false, false, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
-        else if (!upl) row_pp<PROF, false, true, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
-        else if (mel) row_pp<PROF, true, true, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
-        else row_pp<PROF, true, false, RK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        if (!upl && !mel) row_pp<PROF, false, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else if (!upl) row_pp<PROF, false, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else if (mel) row_pp<PROF, true, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        else row_pp<PROF, true, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         // row finished: progress for the tail workgroups' start
         if (wid == 0 && lane == 0 && a.rows_done)
             __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2022,10 +2132,10 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
     McScratch &Mw = M[q * NMC + wid - 2];
-    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (!upl) mc_row<NMC, PROF, false, true, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (mel) mc_row<NMC, PROF, true, true, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else mc_row<NMC, PROF, true, false, RK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else mc_row<NMC, PROF, true, false, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
 }
 template __global__ void k_wgpp<3, false, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 1>(ReconArgs);
@@ -2035,3 +2145,9 @@ template __global__ void k_wgpp<3, false, true, 3>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 2>(ReconArgs);
 template __global__ void k_wgpp<2, true, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 3>(ReconArgs);
+// dependency-checker instantiations (H264MI_CHECK=1)
+template __global__ void k_wgpp<3, false, true, 1, true>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 1, true>(ReconArgs);
+template __global__ void k_wgpp<3, false, true, 2, true>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 2, true>(ReconArgs);
+template __global__ void k_wgpp<3, false, true, 3, true>(ReconArgs);

@@ -67,6 +67,11 @@ static int clampi(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v;
  * 2x2 block and plane, windows clamped as in the kernel's mc_issue) */
 static void set_ref_rows(MbRec *recs, int w, int h)
 {
+    /* test hook of the dependency checker (tests/test_depcheck.py): record
+     * this many rows fewer than the loads need, which the CHK kernels must
+     * report (CHK_REFROW) */
+    const char *inj = getenv("H264MI_CHECK_INJECT_REFROWS");
+    const int short_by = inj ? atoi(inj) : 0;
     static const int bx[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
     static const int by[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
     const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2;
@@ -93,6 +98,7 @@ static void set_ref_rows(MbRec *recs, int w, int h)
                 }
             if (n > rows[b >> 2]) rows[b >> 2] = (uint16_t)n;
         }
+        for (int q = 0; q < 4 && short_by > 0; q++) rows[q] = (uint16_t)(rows[q] > short_by ? rows[q] - short_by : 0);
         memcpy(r->i4, rows, 8);
     }
 }

@@ -39,8 +39,20 @@ static int env_blocking()
 // and pinned allocations, a stream, events and a frame clear.  A pooled
 // engine is idle (its stream drained) and is handed out as a fresh one would
 // be: frames cleared, no batch prepped, settings re-read.  H264MI_ENGINE_POOL=0
-// turns it off; h264mi_pool_drain() frees what the pools hold (also run when
-// the library is unloaded).
+// turns it off; h264mi_pool_drain() frees what the pools hold (also run at
+// process exit).
+// at process exit the pools are drained by an atexit handler registered
+// when something is first pooled -- after the HIP runtime initialised, so
+// it runs before the runtime's own teardown (a library destructor would run
+// too late in a process that loaded the runtime first, e.g. through torch)
+extern "C" int h264mi_pool_drain(void);
+static void pool_drain_at_exit() { (void)h264mi_pool_drain(); }
+static void register_drain_once()
+{
+    static std::once_flag once;
+    std::call_once(once, [] { atexit(pool_drain_at_exit); });
+}
+
 #define ENGINE_POOL_MAX 4
 static std::mutex g_pool_mu;
 static h264mi_engine *g_pool[ENGINE_POOL_MAX];
@@ -94,7 +106,7 @@ static void engine_put(h264mi_engine *e)
         hipStreamSynchronize(engine_stream(e)) == hipSuccess) {
         std::lock_guard<std::mutex> g(g_pool_mu);
         for (int i = 0; i < ENGINE_POOL_MAX; i++)
-            if (!g_pool[i]) { g_pool[i] = e; return; }
+            if (!g_pool[i]) { g_pool[i] = e; register_drain_once(); return; }
     }
     h264mi_engine_destroy(e);
 }
@@ -506,7 +518,7 @@ static void hb_host_free(void *vctx, void *p)
         for (int i = 0; i < HOST_POOL_N; i++) kept += g_hpool[i].p ? g_hpool[i].bytes : 0;
         if (bytes && engine_pool_on() && kept + bytes <= host_pool_cap())
             for (int i = 0; i < HOST_POOL_N; i++)
-                if (!g_hpool[i].p) { g_hpool[i].p = p; g_hpool[i].bytes = bytes; return; }
+                if (!g_hpool[i].p) { g_hpool[i].p = p; g_hpool[i].bytes = bytes; register_drain_once(); return; }
     }
     (void)hipHostFree(p);
 }
@@ -599,9 +611,8 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
 }
 
 // Frees every engine and pinned frame the pools hold (engines and frames in
-// use are not touched); returns how many engines were freed.  Run when the
-// library is unloaded, so that a decoder process hands its device memory and
-// pinned pages back however its instances ended.
+// use are not touched); returns how many engines were freed.  Also run at
+// process exit (register_drain_once).
 extern "C" int h264mi_pool_drain(void)
 {
     h264mi_engine *eng[ENGINE_POOL_MAX];
@@ -640,6 +651,3 @@ extern "C" void h264mi_pool_held(int *engines, size_t *pinned_bytes)
     if (pinned_bytes) *pinned_bytes = b;
 }
 
-// (the HIP runtime outlives this destructor: libamdhip64 is a dependency of
-// this library, so the loader finalises it after us)
-__attribute__((destructor)) static void pool_drain_at_unload() { (void)h264mi_pool_drain(); }

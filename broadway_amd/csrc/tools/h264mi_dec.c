@@ -4,16 +4,21 @@
  * D2H of every output picture.  Call protocol of the reference testbench
  * (Decoder/src/DecTestBench.c:230-410): decode, drain NextPicture after each
  * PIC_RDY, flush at end of stream.
- *   h264mi_dec [-R] [-Oout.yuv|-Onone] [-rN] [-T] [-SN] in.h264 [in2.h264 ...]
+ *   h264mi_dec [-R] [-Oout.yuv|-Onone] [-rN] [-T] [-SN] [-Acpus] in.h264 [in2.h264 ...]
  * -rN decodes the stream N times (one instance each; HIP start-up is paid
  * once, before the timed loop); -T prints the wall time of the decode loops.
  * Several inputs: one thread per input, each with its own instances
  * (TestBenchMultipleInstance.c's N instances, concurrently); -SN lets them
  * share one N-lane engine per GPU (h264mi_set_share); -O applies to the
- * first input. */
+ * first input.  -Acpus (a cpulist: "0-7,16,18") pins the process and every
+ * thread it starts (parse workers included) to those host cores before
+ * anything else runs -- one GPU's decoder processes on cores of that GPU's
+ * NUMA node (bench.py end_to_end); the GPU is H264MI_DEVICE (default 0). */
+#define _GNU_SOURCE
 #include "../../../include/h264mi.h"
 
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -25,6 +30,28 @@ static double now_s(void)
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
     return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* "0-3,8,10-11" -> cpu set; 0 on success */
+static int parse_cpulist(const char *s, cpu_set_t *set)
+{
+    CPU_ZERO(set);
+    int n = 0;
+    while (*s) {
+        char *e;
+        long a = strtol(s, &e, 10), b = a;
+        if (e == s || a < 0 || a >= CPU_SETSIZE) return -1;
+        if (*e == '-') {
+            s = e + 1;
+            b = strtol(s, &e, 10);
+            if (e == s || b < a || b >= CPU_SETSIZE) return -1;
+        }
+        for (long c = a; c <= b; c++) { CPU_SET((int)c, set); n++; }
+        if (*e == ',') e++;
+        else if (*e) return -1;
+        s = e;
+    }
+    return n ? 0 : -1;
 }
 
 static double g_t[4];   /* parse, submit, wait, copy (H264SwDecGetTiming), summed over instances */
@@ -119,17 +146,27 @@ int main(int argc, char **argv)
     const char *out = NULL;
     const char *ins[256];
     int nin = 0, no_reorder = 0, timing = 0, reps = 1, share = 0;
+    const char *cpus = NULL;
     for (int i = 1; i < argc; i++) {
         if (!strncmp(argv[i], "-O", 2)) out = argv[i] + 2;
         else if (!strcmp(argv[i], "-R")) no_reorder = 1;
         else if (!strcmp(argv[i], "-T")) timing = 1;
         else if (!strncmp(argv[i], "-r", 2)) reps = atoi(argv[i] + 2);
         else if (!strncmp(argv[i], "-S", 2)) share = atoi(argv[i] + 2);
+        else if (!strncmp(argv[i], "-A", 2)) cpus = argv[i] + 2;
         else if (nin < 256) ins[nin++] = argv[i];
     }
     if (!nin || reps < 1) {
-        fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] [-SN] in.h264 [in2.h264 ...]\n");
+        fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] [-SN] [-Acpus] in.h264 [in2.h264 ...]\n");
         return 2;
+    }
+    if (cpus) {
+        /* before any thread or GPU context exists: everything started later inherits it */
+        cpu_set_t set;
+        if (parse_cpulist(cpus, &set) || sched_setaffinity(0, sizeof(set), &set)) {
+            fprintf(stderr, "bad -A cpu list '%s'\n", cpus);
+            return 2;
+        }
     }
     Job *jobs = (Job *)calloc((size_t)nin, sizeof(Job));
     for (int i = 0; i < nin; i++) {
@@ -178,6 +215,8 @@ int main(int argc, char **argv)
         unsigned long long nb = 0, np = 0;
         h264mi_share_stats(0, &nb, &np);
         if (share) printf("share_batches %llu\nshare_pictures %llu\n", nb, np);
+        cpu_set_t now;
+        if (!sched_getaffinity(0, sizeof(now), &now)) printf("cpus_allowed %d\n", CPU_COUNT(&now));
     }
     for (int i = 0; i < nin; i++) { free(jobs[i].buf); free(jobs[i].work); }
     free(jobs);

@@ -181,6 +181,10 @@ class Engine:
     def errors(self) -> int:
         return int(self._L.h264mi_engine_errors(self._h))
 
+    def error_bits(self) -> int:
+        """OR of the device flags of the pictures synced since the last call."""
+        return int(self._L.h264mi_engine_error_bits(self._h))
+
     def rows_per_workgroup(self, npics: int) -> int:
         """MB rows per k_wgpp workgroup for a batch of npics pictures."""
         return int(self._L.h264mi_engine_rows_per_workgroup(self._h, npics))
@@ -200,6 +204,8 @@ class Engine:
 
     def timing_list(self, cap: int = 4096):
         """k_wgpp duration (us) of every recorded launch, in order."""
+        if not hasattr(self._L, "h264mi_engine_timing_list"):
+            return None
         v = (C.c_double * cap)()
         n = self._L.h264mi_engine_timing_list(self._h, v, int(cap))
         if n < 0:

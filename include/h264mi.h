@@ -241,6 +241,11 @@ int  h264mi_engine_sync(h264mi_engine *e);
  * range errors (reference transform.c:181) or a bounded wait that expired;
  * flags accumulate over every launch and are collected by h264mi_engine_sync */
 uint32_t h264mi_engine_errors(h264mi_engine *e);
+/* the OR of the device flag words of every picture synced since the last
+ * call (1 residual range, 2 / 16 / 32 bounded waits expired; with
+ * H264MI_CHECK=1 the dependency checker's 64 ring data, 128 ring overwrite,
+ * 256 partner region, 512 intra progress, 1024 reference rows not final) */
+uint32_t h264mi_engine_error_bits(h264mi_engine *e);
 /* MB rows per k_wgpp workgroup the engine launches for a batch of npics
  * pictures (1..3: by batch size, H264MI_RPW, the LDS budget) */
 int  h264mi_engine_rows_per_workgroup(h264mi_engine *e, int npics);

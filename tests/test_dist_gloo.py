@@ -107,6 +107,34 @@ def test_bench_dry_run_two_ranks():
     for r in (0, 1):
         assert place[r]["device"] == r
         assert [d for _, d in place[r]["buffers"]] == [r, r, r]
+    # the end-to-end drop-in leg of every rank: its own GPU and a host-core
+    # share disjoint from every other rank's
+    import bench
+    plan = {p["rank"]: p for p in line["end_to_end_plan"]}
+    assert sorted(plan) == [0, 1]
+    cores = {r: set(bench.parse_cpulist(plan[r]["cpus"])) for r in (0, 1)}
+    for r in (0, 1):
+        assert plan[r]["device"] == r
+        assert cores[r] and len(cores[r]) == plan[r]["host_cores"]
+        assert cores[r] <= os.sched_getaffinity(0)
+    assert not cores[0] & cores[1]
+
+
+def test_e2e_core_plan_numa():
+    """Ranks whose GPUs share a NUMA node split that node's cores; a node
+    with no usable cores falls back to an equal share of all allowed cores."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    assert bench.parse_cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert bench.format_cpulist([11, 0, 1, 2, 3, 8, 10]) == "0-3,8,10-11"
+    allowed = list(range(16))
+    mine, plan = bench.e2e_core_plan(1, [-1, -1, -1, -1], allowed)
+    assert mine == [4, 5, 6, 7] and len(plan) == 4
+    assert sorted(c for p in plan for c in p) == allowed
+    # a NUMA node the sysfs does not know: the fallback
+    mine, plan = bench.e2e_core_plan(0, [99, 99], allowed)
+    assert mine == list(range(8)) and plan[1] == list(range(8, 16))
 
 
 def test_bench_gpus_mismatch_refused(monkeypatch):

@@ -53,6 +53,37 @@ __global__ __launch_bounds__(64) void k_ub(unsigned long long *out, int iters, i
     }
 }
 
+// intra_tile (the MC wave's intra MB) of a lone wave, no left neighbour
+// (nothing to wait for): mbtype 2 = I4x4 with modes cycling 0..8, 3 = I16x16
+// plane, chroma plane
+__global__ __launch_bounds__(64) void k_intra(unsigned long long *out, int iters, int mbtype)
+{
+    __shared__ McScratch M;
+    __shared__ uint32_t i4tab[I4TAB_N];
+    __shared__ uint8_t px[384];
+    __shared__ int prog[4];
+    const int lane = threadIdx.x;
+    for (int e = lane; e < I4TAB_N; e += 64) i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
+    for (int i = lane; i < (int)sizeof(McScratch); i += 64) ((uint8_t *)&M)[i] = (uint8_t)(90 + ((i * 29) & 31));
+    for (int i = lane; i < 384; i += 64) M.res[i] = (int16_t)((i * 7) % 9 - 4);
+    if (lane < 4) prog[lane] = 0;
+    __syncthreads();
+    uint64_t i4 = 0;
+    for (int b = 0; b < 16; b++) i4 |= (uint64_t)(b % 9) << (4 * b);
+    LeftNb N;
+    N.lp = nullptr; N.lprog = &prog[0]; N.cprog = &prog[1]; N.my_lprog = &prog[2]; N.my_cprog = &prog[3];
+    N.ltag = 0; N.mytag = 0; N.perr = nullptr; N.chk = false;
+    const int avail = AV_B | AV_C | AV_D;
+    unsigned long long t0 = clock64();
+    for (int it = 0; it < iters; it++) {
+        intra_tile(mbtype, avail, mbtype == MBT_I16 ? 3 | (3 << 4) : (3 << 4), i4, M.res, true, M.ty, M.tu, M.tv,
+                   i4tab, M.junk, px, lane, N);
+        wave_sync();
+    }
+    unsigned long long t1 = clock64();
+    if (lane == 0) { out[0] = (t1 - t0) / iters; out[1] = px[17]; }
+}
+
 // wall-clock (100 MHz) against shader clock over the same loop: the clock
 // the passes ran at
 __global__ void k_clk(unsigned long long *out)
@@ -77,6 +108,11 @@ int main()
         (void)hipMemcpy(h, d, 32, hipMemcpyDeviceToHost);
         printf("bsmode %d: V %llu cycles (%.3f us), H %llu cycles (%.3f us), filt x4 %llu cycles\n", mode,
                h[0], h[0] / mhz, h[1], h[1] / mhz, h[2]);
+    }
+    for (int t = 2; t <= 3; t++) {
+        hipLaunchKernelGGL(k_intra, dim3(1), dim3(64), 0, 0, d, 500, t);
+        (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+        printf("intra_tile %s: %llu cycles (%.3f us)\n", t == 2 ? "I4x4" : "I16x16 plane", h[0], h[0] / mhz);
     }
     return 0;
 }
