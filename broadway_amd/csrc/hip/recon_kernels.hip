@@ -89,6 +89,12 @@ struct ReconArgs {
 //   CHK_REFROW  (frame-pipelined launches) a reference line is read from a
 //               picture of the same launch before every row holding a byte
 //               of it was tagged final -- checks the host's set_ref_rows
+// The checker's MB tags ride in bytes 22..23 of the 64-B deblocking record
+// (class 0's threshold entry {alpha, beta, tc0[3], indexA} leaves them
+// unused): the MC wave writes MB c's index there with the record it puts in
+// the ring slot; the row wave's copy-in carries it into its region.  No LDS
+// layout changes for the normal kernels.
+#define CHK_TAG_OFF 22
 #define CHK_RING    64u
 #define CHK_RING_WR 128u
 #define CHK_REGION  256u
@@ -1107,7 +1113,6 @@ struct __attribute__((aligned(16))) MbRing {
     // I4x4 steps whose samples are in px (10: all luma), cprog n = 1 once its
     // chroma is -- the next MB's intra reads its left neighbours as they land
     int lprog[RK], cprog[RK];
-    int tag[RK];            // dependency checker: the MB whose data the slot holds
     int consumed;
 };
 
@@ -1134,11 +1139,11 @@ typedef __attribute__((address_space(3))) McScratch lds_McScratch;
 typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
 typedef const __attribute__((address_space(1))) MbRec g_MbRec;
 typedef __attribute__((address_space(1))) unsigned g_u32;
-template <bool UPL, int RK>
+template <bool UPL, int RK, bool CHK>
 __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigned long long *mbx_up, g_u32 *perr_g,
                                                    int W, int c, uint32_t tag, bool has_up, int lane, lds_McScratch *Ml,
                                                    __attribute__((address_space(3))) MbRing<RK> *Rl, lds_cu32 *i4tab_l,
-                                                   __attribute__((address_space(1))) unsigned long long *pst, bool chk)
+                                                   __attribute__((address_space(1))) unsigned long long *pst)
 {
     // pst (profiling build): [0] left ready | top ready, [1] prediction done | slot written
     unsigned long long st0 = 0, st1 = 0;
@@ -1204,7 +1209,7 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     N.my_lprog = &R.lprog[slot]; N.my_cprog = &R.cprog[slot];
     N.ltag = (c - 1) << 4; N.mytag = c << 4;
     N.perr = perr;
-    N.chk = chk;
+    N.chk = CHK;
     intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
     if (pst) st1 = wall_clock64();
     if (pst && lane == 0) { pst[0] = st0; pst[1] = (st1 & 0xFFFFFFFFull) | (wall_clock64() << 32); }
@@ -1238,7 +1243,6 @@ struct __attribute__((aligned(16))) PPRegion {
     uint8_t ry[20 * RY_S];      // rows -4..15, cols -4..15
     uint8_t ru[10 * RC_S];      // rows -2..7, cols -4..7
     uint8_t rv[10 * RC_S];
-    int tag[4];                 // dependency checker: the MB in the region (after its H pass)
 };
 struct __attribute__((aligned(16))) PPLds {
     PPRegion G[2];
@@ -1436,7 +1440,8 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         }
         wave_sync();
         PPT(7);
-        if (CHK && __builtin_amdgcn_readfirstlane(lds_ld(&R->tag[slot])) != c && lane == 0) atomicOr(perr, CHK_RING);
+        if (CHK && __builtin_amdgcn_readfirstlane(*(const uint16_t *)&R->db[slot][CHK_TAG_OFF]) != c && lane == 0)
+            atomicOr(perr, CHK_RING);
         {
             const uint32_t oy = *(const uint32_t *)&R->px[slot][orow * 16 + oq * 4];
             const uint32_t oc = *(const uint32_t *)&R->px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
@@ -1456,7 +1461,8 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             }
             wave_sync();
             PPT(3);
-            if (CHK && __builtin_amdgcn_readfirstlane(lds_ld(&Gp.tag[0])) != c - 1 && lane == 0) atomicOr(perr, CHK_REGION);
+            if (CHK && __builtin_amdgcn_readfirstlane(*(const uint16_t *)&Gp.db[CHK_TAG_OFF]) != c - 1 && lane == 0)
+                atomicOr(perr, CHK_REGION);
             if (prof && lane == 0) tva = wall_clock64();
             const uint32_t hv = *(const uint32_t *)((const uint8_t *)&Gp + cp_src);
             *(uint32_t *)(Lb + cp_dst) = hv;
@@ -1495,7 +1501,6 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_TOP);
             wave_sync();
         }
-        if (CHK && lane == 0) lds_st(&G.tag[0], c);
         if (lane == 0) lds_st(&L.hdone, c + 1);
         if (prof && lane == 0) tvd = wall_clock64();
         PPT(2);
@@ -1523,7 +1528,8 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                     qdw = *(const uint32_t *)&R->px[s1][pq_off];
                     bsw = dbn[1]; t0 = dbn[pchroma ? 12 : 6]; t1 = dbn[pchroma ? 13 : 7];
                 }
-                if (CHK && __builtin_amdgcn_readfirstlane(lds_ld(&R->tag[s1])) != c + 1 && lane == 0) atomicOr(perr, CHK_RING);
+                if (CHK && __builtin_amdgcn_readfirstlane(*(const uint16_t *)&R->db[s1][CHK_TAG_OFF]) != c + 1 && lane == 0)
+                    atomicOr(perr, CHK_RING);
                 const uint32_t pdw = ent;
                 int v[20];
 #pragma unroll
@@ -1996,11 +2002,10 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             ((uint32_t *)R.px[slot])[lane] = src[lane];
             if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
         } else if (type >= MBT_I4x4) {
-            mc_intra<UPL, RK>((g_MbRec *)(a.rec + pd.rec_base + r * a.w + c), mbx_up, (g_u32 *)(a.err + p), a.w, c, a.epoch,
+            mc_intra<UPL, RK, CHK>((g_MbRec *)(a.rec + pd.rec_base + r * a.w + c), mbx_up, (g_u32 *)(a.err + p), a.w, c, a.epoch,
                               r > 0, lane, (lds_McScratch *)&Mw, (__attribute__((address_space(3))) MbRing<RK> *)&R,
                               (lds_cu32 *)i4tab,
-                              (__attribute__((address_space(1))) unsigned long long *)(PROF ? a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4 : nullptr),
-                              CHK);
+                              (__attribute__((address_space(1))) unsigned long long *)(PROF ? a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4 : nullptr));
         }
         wave_sync();
         {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
@@ -2013,7 +2018,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         if (PROF && lane == 0)
             a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 3] = (t0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
         if (lane == 0) {
-            if (CHK) lds_st(&R.tag[slot], c ^ (a.chk_inject == 1 && c == 5 ? 1 : 0));
+            if (CHK) *(uint16_t *)&R.db[slot][CHK_TAG_OFF] = (uint16_t)(c ^ (a.chk_inject == 1 && c == 5 ? 1 : 0));
             lds_st(&R.lprog[slot], (c << 4) | 10);
             lds_st(&R.cprog[slot], (c << 4) | 1);
             lds_st(&R.flag[slot], c + 1);
@@ -2079,14 +2084,8 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
     const int j = jg / hg, g = jg - j * hg, p = j * S + s;
     for (int q = 0; q < RPW; q++) {
-        if (threadIdx.x < RK) {
-            R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1;
-            R[q].tag[threadIdx.x] = -1;
-        }
-        if (threadIdx.x == 0) {
-            R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0;
-            L[q].G[0].tag[0] = L[q].G[1].tag[0] = -1;
-        }
+        if (threadIdx.x < RK) { R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1; }
+        if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
     for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
         L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
