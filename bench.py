@@ -181,7 +181,8 @@ def pack(caps, npics):
             recs[off:off + rec_bytes] = C.string_at(p.rec, rec_bytes)
             if p.ncoef:
                 coef_parts.append(C.string_at(p.coef, p.ncoef * 32))
-            pics[j * S + s] = ((j * S + s) * nmbs, s * nslots, p.cur_slot, 0, cbase, 0, 0, 0)
+            heavy = 4 if 2 * p.n_intra > nmbs else 0          # PicDesc.flags PD_INTRA_HEAVY
+            pics[j * S + s] = ((j * S + s) * nmbs, s * nslots, p.cur_slot, heavy, cbase, 0, 0, 0)
             cbase += p.ncoef
     coefs = b"".join(coef_parts) + b"\0" * 64
     return recs, coefs, pics, rec_bytes * S, nslots

@@ -342,6 +342,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 0;
     a.row_prio_split = row_prio;
     a.chk_inject = e->check ? e->check_inject : 0;
+
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;
@@ -461,7 +462,12 @@ int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int
         pd.rec_base = (uint32_t)(i * e->nmbs);
         pd.frame_base = (uint32_t)(stream[i] * e->nslots);
         pd.cur_slot = (uint32_t)cur_slot[i];
-        pd.flags = 0;
+        {
+            const MbRec *r = (const MbRec *)recs[i];
+            int n = 0;
+            for (int m = 0; m < e->nmbs; m++) n += r[m].type >= MBT_I4x4;
+            pd.flags = 2 * n > e->nmbs ? PD_INTRA_HEAVY : 0;
+        }
         pd.coef_base = (uint32_t)cbase;
         pd.rsv[0] = pd.rsv[1] = pd.rsv[2] = 0;
         cbase += ncoef[i];
@@ -472,12 +478,7 @@ int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int
     HIPCHECK(hipEventRecord(e->ev_staged, e->st));
     // the batch's shape hint from its records (launch_nmc)
     int heavy = intra_heavy > 0;
-    for (int i = 0; i < npics && !heavy && intra_heavy < 0; i++) {
-        const MbRec *r = (const MbRec *)recs[i];
-        int n = 0;
-        for (int m = 0; m < e->nmbs; m++) n += r[m].type >= MBT_I4x4;
-        heavy = 2 * n > e->nmbs;
-    }
+    for (int i = 0; i < npics && !heavy && intra_heavy < 0; i++) heavy = (e->h_pics[i].flags & PD_INTRA_HEAVY) != 0;
     e->launch_intra = heavy;
     return launch_batch(e, npics, 1, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
 }

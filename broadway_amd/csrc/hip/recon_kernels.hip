@@ -1964,6 +1964,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
     if (CHK && c0 < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c0, v0, lane, (int)D.slot[0], D.known[0]);
     if (c0 < a.w) mc_issue(a, pd, p, r * a.w + c0, v0, lane, ld);
+
     const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
     const int lead0 = a.mc_lead0 > 0 && a.mc_lead0 < lead ? a.mc_lead0 : lead;
     for (int c = c0; c < a.w; c += NMC) {
@@ -1996,7 +1997,17 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             if (c - __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < 8) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
+        // PROF stamps [4] / [5] of inter MBs (intra MBs: mc_intra's): loads
+        // landed (a drain the normal kernel leaves to the loads' first use),
+        // samples reconstructed into the slot
+        unsigned long long t_ld = 0;
+        if (PROF) { drain_vm(); t_ld = wall_clock64(); }
         const int type = mc_finish(a, p, v0, lane, ld, Mw, R.px[slot], Mw.res, R.db[slot]);
+        if (PROF && type < MBT_I4x4 && lane == 0) {
+            unsigned long long *pm = a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB;
+            pm[4] = (t0 & 0xFFFFFFFFull) | (t_ld << 32);
+            pm[5] = wall_clock64() & 0xFFFFFFFFull;
+        }
         if (type == MBT_IPCM) {
             const uint32_t *src = (const uint32_t *)(a.coef + ((size_t)pd.coef_base + a.rec[pd.rec_base + r * a.w + c].coef) * 16);
             ((uint32_t *)R.px[slot])[lane] = src[lane];

@@ -96,9 +96,12 @@ typedef struct PicDesc {
                                contiguous; k_prep outputs are indexed by batch position) */
     uint32_t frame_base;    /* index of this stream's slot 0 in the frame pool */
     uint32_t cur_slot;      /* slot being reconstructed */
-    uint32_t flags;         /* bit0: picture has intra MBs, bit1: deblocking on */
+    uint32_t flags;         /* bit2 (PD_INTRA_HEAVY): more than half the picture's MBs are intra
+                               (a scheduling hint: intra MC waves first); bits 0, 1 unused */
     uint32_t coef_base;     /* added to MbRec.coef (records are picture-relative) */
     uint32_t rsv[3];
 } PicDesc;
+
+enum { PD_INTRA_HEAVY = 4 };
 
 #endif

@@ -183,6 +183,17 @@ if im.any():
     if i16.any():
         st("  I16x16 intra_tile", (P0 - T0)[:, rr, cc][i16])
 
+# inter MBs' MC ([4] lo: MC start, hi: reference loads landed; [5] lo: samples
+# reconstructed into the slot; [3] hi: flag set), top rows vs deep rows
+I4lo, I4hi, I5lo = us(lo(m[..., 4])), us(hi(m[..., 4])), us(lo(m[..., 5]))
+inter = ~intra & (types != 4)
+for name, rs in (("rows 0..3", slice(0, 4)), ("rows 8..h-2", slice(8, h - 1))):
+    sel = inter[:, rs, :] & (m[:, rs, :, 4] != 0)
+    if sel.any():
+        st(f"inter MC {name}: start -> loads landed", (I4hi - I4lo)[:, rs, :][sel])
+        st(f"inter MC {name}: landed -> reconstructed", (I5lo - I4hi)[:, rs, :][sel])
+        st(f"inter MC {name}: reconstructed -> flag", (M1 - I5lo)[:, rs, :][sel])
+
 if os.environ.get("PROF_ROWS"):
     # per row, mean over pictures (us): MC start of MB 0, MC final of MB 2,
     # V(2) start, H(2) start, the row above's entry 2 published, last MB's H end

@@ -84,6 +84,50 @@ __global__ __launch_bounds__(64) void k_intra(unsigned long long *out, int iters
     if (lane == 0) { out[0] = (t1 - t0) / iters; out[1] = px[17]; }
 }
 
+// mc_finish (the MC wave's inter MB: window staging, 6-tap luma, bilinear
+// chroma, residual add) of a lone wave, loads already landed; fx/fy
+// fractional positions cycle over all 16 luma / 64 chroma cases
+__global__ __launch_bounds__(64) void k_mc(unsigned long long *out, int iters, const uint8_t *frame, uint8_t *dbrec,
+                                           int16_t *res, unsigned *err, int fmode)
+{
+    __shared__ McScratch M;
+    __shared__ uint8_t px[384], db[64];
+    const int lane = threadIdx.x;
+    ReconArgs a;
+    memset(&a, 0, sizeof(a));
+    a.frames = (uint8_t *)frame; a.frame_bytes = 120 * 68 * 384; a.w = 120; a.h = 68;
+    a.dbrec = dbrec; a.res = res; a.err = err;
+    PicDesc pd;
+    memset(&pd, 0, sizeof(pd));
+    // MbRec as dwords: type inter, cbits = all luma + chroma AC, refs slot 0,
+    // per 4x4 block a different fractional MV
+    uint32_t v0 = 0;
+    if (lane == 0) v0 = MBT_INTER | (26u << 8) | (26u << 16) | ((uint32_t)(AV_A | AV_B) << 24);
+    if (lane == 2) v0 = 0x00FFFFFFu;
+    if (lane >= 7 && lane < 23) {
+        const int b = lane - 7;
+        // fmode 0: all 16 positions; 1: full-sample only; 2: half-sample
+        // b / h only (no centre j)
+        const int fx = fmode == 1 ? 0 : fmode == 2 ? ((b & 1) ? 2 : 0) : (b & 3);
+        const int fy = fmode == 1 ? 0 : fmode == 2 ? ((b & 1) ? 0 : 2) : ((b >> 2) & 3);
+        const int mvx = 4 * (b - 8) + fx, mvy = 4 * (3 - b) + fy;
+        v0 = (uint32_t)(uint16_t)mvx | ((uint32_t)(uint16_t)mvy << 16);
+    }
+    McLoad L;
+    unsigned long long acc = 0;
+    for (int it = 0; it < iters; it++) {
+        const int mb = 30 * 120 + 40 + (it & 15);
+        mc_issue(a, pd, 0, mb, v0, lane, L);
+        drain_vm();
+        wave_sync();
+        const unsigned long long t0 = clock64();
+        mc_finish(a, 0, v0, lane, L, M, px, M.res, db);
+        wave_sync();
+        acc += clock64() - t0;
+    }
+    if (lane == 0) { out[0] = acc / iters; out[1] = px[5]; }
+}
+
 // wall-clock (100 MHz) against shader clock over the same loop: the clock
 // the passes ran at
 __global__ void k_clk(unsigned long long *out)
@@ -113,6 +157,24 @@ int main()
         hipLaunchKernelGGL(k_intra, dim3(1), dim3(64), 0, 0, d, 500, t);
         (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
         printf("intra_tile %s: %llu cycles (%.3f us)\n", t == 2 ? "I4x4" : "I16x16 plane", h[0], h[0] / mhz);
+    }
+    {
+        uint8_t *frame, *dbrec;
+        int16_t *res;
+        unsigned *err;
+        (void)hipMalloc(&frame, 120 * 68 * 384);
+        (void)hipMemset(frame, 77, 120 * 68 * 384);
+        (void)hipMalloc(&dbrec, 120 * 68 * 64);
+        (void)hipMemset(dbrec, 0, 120 * 68 * 64);
+        (void)hipMalloc(&res, 120 * 68 * 768);
+        (void)hipMemset(res, 0, 120 * 68 * 768);
+        (void)hipMalloc(&err, 64);
+        for (int fm = 0; fm < 3; fm++) {
+            hipLaunchKernelGGL(k_mc, dim3(1), dim3(64), 0, 0, d, 500, frame, dbrec, res, err, fm);
+            (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+            printf("mc_finish inter MB (%s): %llu cycles (%.3f us)\n", fm == 0 ? "16 positions" : fm == 1 ? "full-sample" : "half b/h only",
+                   h[0], h[0] / mhz);
+        }
     }
     return 0;
 }
