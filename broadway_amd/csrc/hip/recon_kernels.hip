@@ -985,27 +985,46 @@ struct NoMid { __device__ __forceinline__ void operator()() const {} };
 // (region cols -4..-1, the left MB's cols 12..15, now final) are written back
 // -- the row hand-off publishes from there without waiting for the internal
 // edges (edges 1..3 touch only this MB's columns 1..14)
-template <class Mid = NoMid>
-__device__ __forceinline__ void deblock_dir(const int dir, const uint8_t *db, uint8_t *ry, uint8_t *ru, uint8_t *rv,
-                                            uint8_t *junk, int lane, bool mb_edge_on, const Mid &mid = Mid())
+// One pass's per-line filter parameters, from the MB's deblocking record:
+// this line's four bS nibbles (chroma: its edges 0, 1 sit on luma edges 0,
+// 2) and the two threshold sets {alpha, beta, tc0(bS 1..3)} of the MB edge
+// and the internal edges.  They depend on nothing the chain produces, so the
+// row waves compute them off the chain (before the hdone / top waits).
+struct DbPar {
+    uint32_t bsw, tcs_e, tcs_i;
+    int alpha_e, beta_e, alpha_i, beta_i;
+};
+__device__ __forceinline__ DbPar dbpar(const int dir, const uint8_t *db, int lane, bool mb_edge_on)
 {
     const int li = lane & 31;
     const bool chroma = li >= 16;
     const int idx = chroma ? (li & 7) : (li & 15);
     const int seg = chroma ? idx >> 1 : idx >> 2;
-    uint8_t *D = chroma ? ((li & 8) ? rv : ru) : ry;
-    // this line's four bS nibbles (chroma: its edges 0, 1 sit on luma edges
-    // 0, 2) and the two threshold sets {alpha, beta, tc0(bS 1..3), indexA}
+    DbPar P;
     uint32_t bsw = *(const uint16_t *)(db + dir * 8 + seg * 2);
     if (chroma) bsw = (bsw & 15) | ((bsw >> 4) & 0xF0);
     if (!mb_edge_on) bsw &= ~15u;
+    P.bsw = bsw;
     const uint8_t *pe = db + 16 + ((chroma ? 3 : 0) + 1 + dir) * 8;    // MB edge class
     const uint8_t *pi = db + 16 + (chroma ? 3 : 0) * 8;                  // internal class
     const uint2 te = *(const uint2 *)pe, ti = *(const uint2 *)pi;
     const uint32_t cplus = chroma ? 0x01010100u : 0u;
-    const int alpha_e = te.x & 255, beta_e = (te.x >> 8) & 255, alpha_i = ti.x & 255, beta_i = (ti.x >> 8) & 255;
-    const uint32_t tcs_e = (((te.x >> 8) & 0xFFFF00u) | (te.y << 24)) + cplus;
-    const uint32_t tcs_i = (((ti.x >> 8) & 0xFFFF00u) | (ti.y << 24)) + cplus;
+    P.alpha_e = te.x & 255; P.beta_e = (te.x >> 8) & 255; P.alpha_i = ti.x & 255; P.beta_i = (ti.x >> 8) & 255;
+    P.tcs_e = (((te.x >> 8) & 0xFFFF00u) | (te.y << 24)) + cplus;
+    P.tcs_i = (((ti.x >> 8) & 0xFFFF00u) | (ti.y << 24)) + cplus;
+    return P;
+}
+
+template <class Mid = NoMid>
+__device__ __forceinline__ void deblock_dir(const int dir, const DbPar &P, uint8_t *ry, uint8_t *ru, uint8_t *rv,
+                                            uint8_t *junk, int lane, const Mid &mid = Mid())
+{
+    const int li = lane & 31;
+    const bool chroma = li >= 16;
+    const int idx = chroma ? (li & 7) : (li & 15);
+    uint8_t *D = chroma ? ((li & 8) ? rv : ru) : ry;
+    const uint32_t bsw = P.bsw, tcs_e = P.tcs_e, tcs_i = P.tcs_i;
+    const int alpha_e = P.alpha_e, beta_e = P.beta_e, alpha_i = P.alpha_i, beta_i = P.beta_i;
     // one stride for both planes (RC_S == RY_S): every access below is
     // base + immediate.  Chroma lines read past their 12/10 samples into
     // neighbouring LDS (values unused) and write back only what they own.
@@ -1450,6 +1469,11 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             *(uint32_t *)(Lb + own_c_lds) = oc;
             *(uint32_t *)(Lb + db_lds) = od;
         }
+        // both passes' filter parameters, off the chain (the record just
+        // copied in; a wave's LDS accesses complete in order)
+        wave_sync();
+        const DbPar Pv = dbpar(0, G.db, lane, avail & DB_LEFT);
+        const DbPar Ph = dbpar(1, G.db, lane, avail & DB_TOP);
         PPT(0);
         if (a.row_prio_split) __builtin_amdgcn_s_setprio(3);
         // ---- the chain: MB c-1's H pass done -> its columns 12..15
@@ -1476,7 +1500,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         // (measured: reading the left halo straight from the partner's region
         // inside V and releasing it after the MB
         // edge was 3 us per launch slower than this copy)
-        if (dbf) deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_LEFT);
+        if (dbf) deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane);
         wave_sync();
         PPT(1);
         if (prof && lane == 0) { if (c == 0) tva = wall_clock64(); pmb[1] = (tva & 0xFFFFFFFFull) | (wall_clock64() << 32); }
@@ -1498,7 +1522,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         if (prof && lane == 0) pmb[0] = wall_clock64();
         PPT(5);
         if (dbf) {
-            deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, avail & DB_TOP);
+            deblock_dir(1, Ph, G.ry, G.ru, G.rv, junk, lane);
             wave_sync();
         }
         if (lane == 0) lds_st(&L.hdone, c + 1);

@@ -25,14 +25,15 @@ __global__ __launch_bounds__(64) void k_ub(unsigned long long *out, int iters, i
         o[0] = 40; o[1] = 10; o[2] = 1; o[3] = 2; o[4] = 3; o[5] = 30; o[6] = o[7] = 0;
     }
     __syncthreads();
+    const DbPar Pv = dbpar(0, G.db, lane, true), Ph = dbpar(1, G.db, lane, true);
     unsigned long long t0 = clock64();
     for (int it = 0; it < iters; it++) {
-        deblock_dir(0, G.db, G.ry, G.ru, G.rv, junk, lane, true);
+        deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane);
         wave_sync();
     }
     unsigned long long t1 = clock64();
     for (int it = 0; it < iters; it++) {
-        deblock_dir(1, G.db, G.ry, G.ru, G.rv, junk, lane, true);
+        deblock_dir(1, Ph, G.ry, G.ru, G.rv, junk, lane);
         wave_sync();
     }
     unsigned long long t2 = clock64();
