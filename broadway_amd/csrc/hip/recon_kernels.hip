@@ -1015,9 +1015,12 @@ __device__ __forceinline__ DbPar dbpar(const int dir, const uint8_t *db, int lan
     return P;
 }
 
+// pre (dir 0): the line's columns 0..15 (dwords 1..4 of its region row),
+// read off the chain; only the left halo (dword 0) is read here
 template <class Mid = NoMid>
 __device__ __forceinline__ void deblock_dir(const int dir, const DbPar &P, uint8_t *ry, uint8_t *ru, uint8_t *rv,
-                                            uint8_t *junk, int lane, const Mid &mid = Mid())
+                                            uint8_t *junk, int lane, const uint32_t *pre = nullptr,
+                                            const Mid &mid = Mid())
 {
     const int li = lane & 31;
     const bool chroma = li >= 16;
@@ -1034,7 +1037,7 @@ __device__ __forceinline__ void deblock_dir(const int dir, const DbPar &P, uint8
         const uint32_t *row = (const uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
 #pragma unroll
         for (int j = 0; j < 5; j++) {
-            const uint32_t w = row[j];
+            const uint32_t w = (pre && j > 0) ? pre[j - 1] : row[j];
             v[4 * j] = w & 255; v[4 * j + 1] = (w >> 8) & 255; v[4 * j + 2] = (w >> 16) & 255; v[4 * j + 3] = w >> 24;
         }
     } else {
@@ -1396,6 +1399,14 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         pq_off = !pchroma ? (12 + pj) * 16 : 256 + comp * 64 + (6 + row) * 8;
     }
     const bool is_patch = le < 8;
+    // the vertical pass's line in the region (deblock_dir dir 0): luma rows
+    // for lanes 0..15, Cb / Cr rows for 16..31 (32..63 mirror)
+    uint32_t vrow_lds;
+    {
+        const int vl = lane & 31, vch = vl >= 16, vidx = vch ? (vl & 7) : (vl & 15);
+        const uint8_t *D = vch ? ((vl & 8) ? G.rv : G.ru) : G.ry;
+        vrow_lds = (uint32_t)((int)(D - Lb) + (vidx + (vch ? 2 : 4)) * RY_S);
+    }
     // own samples from the ring slot: luma all lanes, chroma lanes 0..31
     const uint32_t own_y_lds = (uint32_t)((int)(G.ry - Lb) + (orow + 4) * RY_S + 4 + oq * 4);
     const uint32_t own_c_lds = lane < 32 ? (uint32_t)((int)((ccomp ? G.rv : G.ru) - Lb) + (crow + 2) * RC_S + 4 + cq * 4)
@@ -1474,6 +1485,40 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         wave_sync();
         const DbPar Pv = dbpar(0, G.db, lane, avail & DB_LEFT);
         const DbPar Ph = dbpar(1, G.db, lane, avail & DB_TOP);
+        // the vertical pass's own columns 0..15 of the lane's line (only its
+        // left halo arrives on the chain)
+        uint32_t vpre[4];
+        {
+            const uint32_t *row = (const uint32_t *)(Lb + vrow_lds);
+#pragma unroll
+            for (int j = 0; j < 4; j++) vpre[j] = row[1 + j];
+        }
+        // the hand-off patch's inputs (below): MB c+1's unfiltered columns
+        // 0..3 and its left-edge bS / thresholds, from its ring slot -- its MC
+        // is normally long done, so they are read here, off the chain, and
+        // only re-read after H(c) if its flag was not set yet (one LDS round
+        // trip: the MC wave writes the slot before the flag)
+        const int s1 = (c + 1) & (RK - 1);
+        const bool pmore = has_down && c + 1 < W;
+        bool p_ready = false;
+        int p_bS = 0, p_alpha = 0, p_beta = 0;
+        uint32_t p_q = 0, p_tcs = 0;
+        auto patch_in = [&](int fl) {
+            const uint32_t *dbn = (const uint32_t *)R->db[s1];
+            p_q = *(const uint32_t *)&R->px[s1][pq_off];
+            const uint32_t bsw = dbn[1], t0 = dbn[pchroma ? 12 : 6], t1 = dbn[pchroma ? 13 : 7];
+            const uint32_t avb = avn >> 24;
+            const bool on = (avb & DB_INNER) && (avb & DB_LEFT);
+            p_bS = on ? (int)((bsw >> 16) & 15) : 0;      // byte 6 low nibble: dir 0, seg 3, edge 0
+            p_alpha = t0 & 255; p_beta = (t0 >> 8) & 255;
+            p_tcs = (((t0 >> 8) & 0xFFFF00u) | (t1 << 24)) + (pchroma ? 0x01010100u : 0u);
+            p_ready = __builtin_amdgcn_readfirstlane(fl) == c + 2;
+        };
+        if (pmore) {
+            const int fl = lds_ld(&R->flag[s1]);
+            wave_sync();
+            patch_in(fl);
+        }
         PPT(0);
         if (a.row_prio_split) __builtin_amdgcn_s_setprio(3);
         // ---- the chain: MB c-1's H pass done -> its columns 12..15
@@ -1500,7 +1545,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         // (measured: reading the left halo straight from the partner's region
         // inside V and releasing it after the MB
         // edge was 3 us per launch slower than this copy)
-        if (dbf) deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane);
+        if (dbf) deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane, vpre);
         wave_sync();
         PPT(1);
         if (prof && lane == 0) { if (c == 0) tva = wall_clock64(); pmb[1] = (tva & 0xFFFFFFFFull) | (wall_clock64() << 32); }
@@ -1532,39 +1577,24 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             const bool more = c + 1 < W;
             uint32_t ent = *(const uint32_t *)(Lb + prov_off);
             if (more) {
-                const int s1 = (c + 1) & (RK - 1);
-                // MB c+1's MC output (normally long done): its flag and the
-                // slot data in one LDS round trip.  LDS serves one wave's
-                // accesses in order and the MC wave writes the slot before
-                // the flag, so data read after a ready flag is the slot's.
-                const uint32_t *dbn = (const uint32_t *)R->db[s1];
-                const int fl = lds_ld(&R->flag[s1]);
-                wave_sync();
-                uint32_t qdw = *(const uint32_t *)&R->px[s1][pq_off];
-                uint32_t bsw = dbn[1], t0 = dbn[pchroma ? 12 : 6], t1 = dbn[pchroma ? 13 : 7];
-                if (__builtin_amdgcn_readfirstlane(fl) != c + 2) {
+                if (!p_ready) {
                     unsigned spins = 0;
                     while (__builtin_amdgcn_readfirstlane(lds_ld(&R->flag[s1])) != c + 2) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
                     }
                     wave_sync();
-                    qdw = *(const uint32_t *)&R->px[s1][pq_off];
-                    bsw = dbn[1]; t0 = dbn[pchroma ? 12 : 6]; t1 = dbn[pchroma ? 13 : 7];
+                    patch_in(c + 2);
                 }
                 if (CHK && __builtin_amdgcn_readfirstlane(*(const uint16_t *)&R->db[s1][CHK_TAG_OFF]) != c + 1 && lane == 0)
                     atomicOr(perr, CHK_RING);
                 const uint32_t pdw = ent;
                 int v[20];
 #pragma unroll
-                for (int x = 0; x < 4; x++) { v[x] = (pdw >> (8 * x)) & 255; v[4 + x] = (qdw >> (8 * x)) & 255; }
+                for (int x = 0; x < 4; x++) { v[x] = (pdw >> (8 * x)) & 255; v[4 + x] = (p_q >> (8 * x)) & 255; }
 #pragma unroll
                 for (int x = 8; x < 20; x++) v[x] = 0;
-                const uint32_t avb = avn >> 24;
-                const bool on = (avb & DB_INNER) && (avb & DB_LEFT);
-                const int bS = on ? (int)((bsw >> 16) & 15) : 0;      // byte 6 low nibble: dir 0, seg 3, edge 0
-                const uint32_t tcs = (((t0 >> 8) & 0xFFFF00u) | (t1 << 24)) + (pchroma ? 0x01010100u : 0u);
-                filt_line<true>(v, 0, bS, t0 & 255, (t0 >> 8) & 255, pchroma ? 0 : ((t0 >> 8) & 255), tcs);
+                filt_line<true>(v, 0, p_bS, p_alpha, p_beta, pchroma ? 0 : p_beta, p_tcs);
                 const uint32_t newp = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
                 if (is_patch) ent = newp;
             }
