@@ -1017,10 +1017,13 @@ __device__ __forceinline__ DbPar dbpar(const int dir, const uint8_t *db, int lan
 
 // pre (dir 0): the line's columns 0..15 (dwords 1..4 of its region row),
 // read off the chain; only the left halo (dword 0) is read here
+// use_halo (dir 0): the line's left halo (dword 0) is `halo`, already in a
+// register (passed by value: a pointer chosen at run time would put it in
+// scratch memory)
 template <class Mid = NoMid>
 __device__ __forceinline__ void deblock_dir(const int dir, const DbPar &P, uint8_t *ry, uint8_t *ru, uint8_t *rv,
                                             uint8_t *junk, int lane, const uint32_t *pre = nullptr,
-                                            const Mid &mid = Mid())
+                                            bool use_halo = false, uint32_t halo = 0, const Mid &mid = Mid())
 {
     const int li = lane & 31;
     const bool chroma = li >= 16;
@@ -1037,7 +1040,7 @@ __device__ __forceinline__ void deblock_dir(const int dir, const DbPar &P, uint8
         const uint32_t *row = (const uint32_t *)(D + (idx + (chroma ? 2 : 4)) * RY_S);
 #pragma unroll
         for (int j = 0; j < 5; j++) {
-            const uint32_t w = (pre && j > 0) ? pre[j - 1] : row[j];
+            const uint32_t w = (pre && j > 0) ? pre[j - 1] : (j == 0 && use_halo) ? halo : row[j];
             v[4 * j] = w & 255; v[4 * j + 1] = (w >> 8) & 255; v[4 * j + 2] = (w >> 16) & 255; v[4 * j + 3] = w >> 24;
         }
     } else {
@@ -1345,12 +1348,15 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     }
     // left-halo copy from the partner's region: lanes 0..15 luma rows, 16..31
     // chroma rows (cols 12..15 / 4..7 -> -4..-1); lanes 32..63 into junk
+    // (lanes 32..63 read what lanes 0..31 read -- the vertical pass takes
+    // the copied dword as its line's halo, and its lanes 32..63 mirror)
     uint32_t cp_src, cp_dst;
     {
         int off, step;
         const uint8_t *D;
-        if (lane < 16) { D = Gp.ry; off = (lane + 4) * RY_S; step = 16; }
-        else { const int k = (lane - 16) & 15; D = (k >> 3) ? Gp.rv : Gp.ru; off = ((k & 7) + 2) * RC_S; step = 8; }
+        const int cl = lane & 31;
+        if (cl < 16) { D = Gp.ry; off = (cl + 4) * RY_S; step = 16; }
+        else { const int k = cl - 16; D = (k >> 3) ? Gp.rv : Gp.ru; off = ((k & 7) + 2) * RC_S; step = 8; }
         cp_src = (uint32_t)((int)(D - (const uint8_t *)&Gp) + off + step);
         cp_dst = lane < 32 ? (uint32_t)((int)(D - (const uint8_t *)&Gp) + off) : (uint32_t)((int)(junk - Lb) + lane * 4);
     }
@@ -1522,6 +1528,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         PPT(0);
         if (a.row_prio_split) __builtin_amdgcn_s_setprio(3);
         // ---- the chain: MB c-1's H pass done -> its columns 12..15
+        uint32_t vhalo = 0;     // the vertical pass's left halo (MB c-1's columns 12..15), c > 0
         if (c > 0) {
             unsigned spins = 0;
             while (__builtin_amdgcn_readfirstlane(lds_ld(&L.hdone)) < c) {
@@ -1535,6 +1542,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             if (prof && lane == 0) tva = wall_clock64();
             const uint32_t hv = *(const uint32_t *)((const uint8_t *)&Gp + cp_src);
             *(uint32_t *)(Lb + cp_dst) = hv;
+            vhalo = hv;
             wave_sync();
             if (lane == 0) { lds_st(&L.copied, c); lds_st(&R->consumed, c); }
         } else {
@@ -1545,7 +1553,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         // (measured: reading the left halo straight from the partner's region
         // inside V and releasing it after the MB
         // edge was 3 us per launch slower than this copy)
-        if (dbf) deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane, vpre);
+        if (dbf) deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane, vpre, c > 0, vhalo);
         wave_sync();
         PPT(1);
         if (prof && lane == 0) { if (c == 0) tva = wall_clock64(); pmb[1] = (tva & 0xFFFFFFFFull) | (wall_clock64() << 32); }
