@@ -80,9 +80,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-rgba", action="store_true", help="skip the RGBA output leg")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the SURVEY §8d config 2 (720p I-only) / config 5 (2160p) legs")
-    ap.add_argument("--pipe", type=int, default=int(os.environ.get("BENCH_PIPE", "1")),
-                    help="steps per launch (1 or 2): with 2, a launch reconstructs two consecutive pictures of "
-                         "every stream and the second's rows start as the reference rows they read are final")
+    ap.add_argument("--pipe", type=int, default=int(os.environ.get("BENCH_PIPE", "2")),
+                    help="steps per launch (1 or 2; default 2, profiles/r72_ab_pipe2_gop.txt): with 2, a launch "
+                         "reconstructs two consecutive pictures of every stream and the second's rows start as the "
+                         "reference rows they read are final; a launch that would hold an IDR runs as two one-step "
+                         "launches")
     ap.add_argument("--aligned", action="store_true",
                     help="all streams' GOPs aligned, pictures W .. W+K-1 timed (no IDR in short windows); "
                          "default: GOP phases staggered over the streams")
@@ -540,17 +542,20 @@ def load_traffic():
 GOP = 60                   # configs[3]: 1 I + 59 P per GOP; the bench streams are one GOP long
 
 
-def gop_phases(S: int, gop: int = GOP):
+def gop_phases(S: int, gop: int = GOP, step: int = 1):
     """GOP phase of each stream: stream s is s*gop/S pictures into its GOP
     when the first warmup step starts, so the S streams' IDR pictures are
     spread evenly over the steps (independent streams that did not start
     together) and every window of `gop` steps reconstructs S I pictures out
     of S*gop -- the configs[3] mix of 1 I per 60 in every step window, not
-    only in the one step that happens to hold picture 0."""
-    return [(s * gop) // S for s in range(S)]
+    only in the one step that happens to hold picture 0.  step = P (frame-
+    pipelined launches of P pictures per stream): phases are multiples of
+    P, so with an even GOP no launch pairs a stream's last picture with the
+    IDR after it."""
+    return [((s * gop) // S) // step * step for s in range(S)]
 
 
-def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None):
+def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None, P: int = 1):
     """Per launch, per step of the launch, the picture index of each stream;
     returns (launches, pre-roll launch count).
 
@@ -559,16 +564,29 @@ def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None
     v - warmup) decodes picture (v + phases[s]) % N of stream s: a stream of
     N pictures starting with its IDR is decoded cyclically -- after picture
     N-1 comes picture 0 again, an IDR (no reference is read across it), so
-    the pictures and MD5s are the stream's own.  An untimed pre-roll of
-    max(phases) launches first brings stream s to picture phases[s]: its
-    pictures 0 .. phases[s]-1 in order, preceded by repeats of the IDR
-    picture 0 (which reads no reference, so repeating it is idempotent)."""
+    the pictures and MD5s are the stream's own -- P steps per launch.  An
+    untimed pre-roll of max(phases) one-step launches first brings stream s
+    to picture phases[s]: its pictures 0 .. phases[s]-1 in order, preceded
+    by repeats of the IDR picture 0 (which reads no reference, so repeating
+    it is idempotent)."""
     if phases is None:
         return [[[k] * S for k in range(k0, k0 + P)] for k0, P in sched], 0
     R = max(phases)
     pre = [[[max(0, u - R + ph) for ph in phases]] for u in range(R)]
-    main = [[[(v + ph) % N for ph in phases]] for v in range(warmup + steps)]
+    main = [[[(v + j + ph) % N for ph in phases] for j in range(P)] for v in range(0, warmup + steps, P)]
     return pre + main, R
+
+
+def pairs_ok(recs, pics, S, nmbs, N, P):
+    """The engine's frame-pipelined batch contract for launches of P = 2
+    consecutive pictures k, k+1 (k even) of every stream: the second writes
+    neither the slot the first writes nor one the first reads."""
+    for k in range(0, N - 1, P):
+        for s in range(S):
+            a, b = k * S + s, (k + 1) * S + s
+            if pics[a][2] == pics[b][2] or pics[b][2] in slots_read(recs, nmbs, a):
+                return False
+    return True
 
 
 class _DryEngine:
@@ -605,6 +623,10 @@ class _DryEngine:
 
     def set_steps(self, *a):
         pass
+
+    def decode_device_steps_next(self, *a):
+        self.launches += 1
+        return True
 
     def sync(self):
         pass
@@ -649,16 +671,20 @@ class DeviceRun:
         self.device = device
         packed = pack(caps, N)
         recs_h, _, pics_h, _, nslots = packed
-        if phases is not None:
-            pipe = 1
         self.sched = None
+        if pipe > 1:
+            nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots)
         if phases is None:
             if warmup + steps > N:
                 raise ValueError(f"{warmup}+{steps} steps but the streams hold {N} pictures")
-            if pipe > 1:
-                nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots)
             self.sched = schedule(recs_h, pics_h, S, nmbs, warmup, steps, pipe)
-        self.P = self.sched[0][1] if self.sched else 1
+            self.P = self.sched[0][1]
+        else:
+            # frame-pipelined GOP plan: P-aligned phases, an even GOP, P-aligned
+            # warmup / steps and every (k, k+1) pair within the batch contract
+            ok = (pipe > 1 and N % pipe == 0 and warmup % pipe == 0 and steps % pipe == 0 and
+                  all(ph % pipe == 0 for ph in phases) and pairs_ok(recs_h, pics_h, S, nmbs, N, pipe))
+            self.P = pipe if ok else 1
         self.nslots = nslots
         self.pics_h = pics_h
         self.slot_of = pics_h[:, 2].reshape(N, S).copy()
@@ -672,16 +698,36 @@ class DeviceRun:
         self.set_plan(warmup, steps, phases)
 
     def set_plan(self, warmup, steps, phases=None):
-        """(Re)build the launch plan and its descriptor table in HBM."""
+        """(Re)build the launch plan and its descriptor table in HBM (each
+        launch's steps step-major, launches back to back)."""
         S, P = self.S, self.P
         self.warmup, self.steps, self.phases = warmup, steps, phases
-        self.launches, self.n_pre = launch_plan(self.N, S, warmup, steps, phases, self.sched)
-        self.n_warm = self.n_pre + sum(1 for k0, _ in self.sched if k0 < warmup) if self.sched else self.n_pre + warmup
-        d = np.zeros((len(self.launches) * P * S, 8), dtype=np.uint32)
-        for i, launch in enumerate(self.launches):
-            for j, step in enumerate(launch):
+        if phases is not None and P > 1 and not (warmup % P == 0 and steps % P == 0 and
+                                                 all(ph % P == 0 for ph in phases)):
+            raise ValueError(f"plan of {warmup}+{steps} steps, phases {phases}: not aligned to {P} steps per launch")
+        self.launches, self.n_pre = launch_plan(self.N, S, warmup, steps, phases, self.sched, P)
+        if self.sched:
+            self.n_warm = self.n_pre + sum(1 for k0, _ in self.sched if k0 < warmup)
+        else:
+            # GOP plan, P = 2: a launch that would hold an IDR runs as two one-
+            # step launches -- paired, the IDR's own P picture waits on the
+            # IDR's deblocking chain, the launch's longest (r71 A/B: 809 us
+            # against 434 + 325 us split)
+            main, warm = [], 0
+            for j, x in enumerate(self.launches[self.n_pre:]):
+                parts = [[st] for st in x] if len(x) > 1 and self.holds_idr(x) else [x]
+                main += parts
+                warm += len(parts) if j * P < warmup else 0
+            self.launches = self.launches[:self.n_pre] + main
+            self.n_warm = self.n_pre + warm
+        self.desc_off = np.cumsum([0] + [len(x) * S * 32 for x in self.launches]).tolist()
+        d = np.zeros((sum(len(x) for x in self.launches) * S, 8), dtype=np.uint32)
+        row = 0
+        for launch in self.launches:
+            for step in launch:
                 for s, k in enumerate(step):
-                    d[(i * P + j) * S + s] = self.pics_h[k * S + s]
+                    d[row + s] = self.pics_h[k * S + s]
+                row += S
         if self.d_desc:
             self.eng.free(self.d_desc)
             self.bufs.remove(self.d_desc)
@@ -689,22 +735,32 @@ class DeviceRun:
         self.bufs.append(self.d_desc)
         self.eng.upload(self.d_desc, d.ctypes.data, d.nbytes)
 
+    def holds_idr(self, launch):
+        """Does one of the launch's pictures read no reference (I picture)."""
+        return any(self.is_i[k][s] for step in launch for s, k in enumerate(step))
+
     def placement(self):
         """Device of every HBM buffer of this run: [(name, device)]."""
         names = ["records", "coefficients", "descriptors"]
         return [(n, self.eng.pointer_device(p)) for n, p in zip(names, self.bufs)]
 
     def launch(self, i):
-        """Launch i of the plan: P steps of the S streams; the next launch's
-        k_prep runs in its tail workgroups."""
-        S, P = self.S, self.P
-        desc = self.d_desc + i * P * S * 32
+        """Launch i of the plan: its steps (1 or P) of the S streams; the next
+        launch's k_prep runs in this one's tail workgroups (over the next
+        launch's own step count)."""
+        S = self.S
+        P = len(self.launches[i])
+        desc = self.d_desc + self.desc_off[i]
         # the launch's shape hint: does it hold an intra-heavy picture
         self.eng.hint_intra(any(2 * self.caps[s].pictures[k].n_intra > self.nmbs
                                 for step in self.launches[i] for s, k in enumerate(step)))
         if i + 1 < len(self.launches):
-            self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc,
-                                         self.d_recs, self.d_coef, desc + P * S * 32)
+            nd, nP = self.d_desc + self.desc_off[i + 1], len(self.launches[i + 1])
+            if nP == P:
+                self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc, self.d_recs, self.d_coef, nd)
+            elif not self.eng.decode_device_steps_next(S, P, self.d_recs, self.d_coef, desc,
+                                                       self.d_recs, self.d_coef, nd, nP):
+                self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc)
         else:
             self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc)
 
@@ -802,12 +858,13 @@ def timed_run(run, dist, torch, sync, stride=1):
 
 def launch_split(run, sampled, per):
     """Sampled launches split by whether one of their pictures is an IDR
-    (I picture): {"i": (n, avg us), "p": (n, avg us)}."""
+    (I picture): {"i": (n, avg us, avg us per step), "p": (...)}."""
     out = {}
     for key, want in (("i", True), ("p", False)):
-        v = [u for i, u in zip(sampled, per)
-             if any(run.is_i[k][s] for step in run.launches[i] for s, k in enumerate(step)) == want]
-        out[key] = (len(v), round(sum(v) / len(v), 2) if v else None)
+        v = [(u, len(run.launches[i])) for i, u in zip(sampled, per) if run.holds_idr(run.launches[i]) == want]
+        us = sum(u for u, _ in v)
+        out[key] = (len(v), round(us / len(v), 2) if v else None,
+                    round(us / sum(n for _, n in v), 2) if v else None)
     return out
 
 
@@ -910,13 +967,13 @@ def main(argv=None):
     # GOP phases (the default): every stream is one 60-picture GOP decoded
     # cyclically, IDRs staggered over the steps; --aligned / --pipe 2: the
     # round-2 layout (pictures W .. W+K-1 of every stream, decode order)
-    staggered = not a.aligned and a.pipe == 1
+    staggered = not a.aligned
     nframes = GOP if staggered and not overrides else max(GOP, a.warmup + a.steps)
     t_prep = time.perf_counter()
     streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= min(nframes, GOP) for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    phases = gop_phases(S, min(c.npics for c in caps)) if staggered else None
+    phases = gop_phases(S, min(c.npics for c in caps), a.pipe) if staggered else None
     run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run, phases=phases)
     placement = run.placement()
     assert all(d == local for _, d in placement), f"rank {rank}: buffers not on device {local}: {placement}"
@@ -952,14 +1009,15 @@ def main(argv=None):
     # round-2 headline's mix), beside the configs[3] mix -- not instead
     p_only = None
     if staggered:
-        kp = max(1, min(a.steps, run.N - 1 - a.warmup))     # pictures 1+W .. W+kp: no IDR
-        run.set_plan(a.warmup, kp, [1] * S)
+        # pictures P+W .. P+W+kp-1: no IDR (P = steps per launch)
+        kp = max(P, min(a.steps, run.N - P - a.warmup) // P * P)
+        run.set_plan(a.warmup, kp, [P] * S)
         dt_p, us_p, _, _ = timed_run(run, dist, torch, sync, stride)
         tp = run.timed_pictures()
         p_only = {"value": round(S * kp * world / dt_p, 2), "unit": "frames/s", "steps": kp,
                   "avg_launch_kernel_us": round(us_p, 2),
                   "i_pictures_timed": sum(1 for s, k in tp if run.is_i[k][s]),
-                  "window": f"pictures {1 + a.warmup}..{a.warmup + kp} of every stream (GOPs aligned, no IDR)"}
+                  "window": f"pictures {P + a.warmup}..{P + a.warmup + kp - 1} of every stream (GOPs aligned, no IDR)"}
         run.set_plan(a.warmup, a.steps, phases)
 
     ok, n_checked, n_missing, n_pre = None, 0, 0, 0
@@ -1014,8 +1072,9 @@ def main(argv=None):
         plans = [e2e_plan]
 
     if rank == 0:
-        mix = (f"IDRs staggered: stream s enters the timed window s*{run.N}/{S} pictures into its GOP "
-               f"(pre-roll + warmup untimed), 1 I per {run.N} in every {run.N}-step window"
+        mix = (f"IDRs staggered: stream s enters the timed window {phases} pictures into its GOP "
+               f"(s*{run.N}/{S}, rounded down to whole launches; pre-roll + warmup untimed), "
+               f"1 I per {run.N} in every {run.N}-step window"
                if staggered else "decode order from picture 0 (aligned GOPs)")
         line = {
             "metric": "1080p Baseline frames/s per GPU; bit-exact YUV; % HBM-read roofline",
@@ -1041,7 +1100,8 @@ def main(argv=None):
                        "i_share_timed": round(n_i_all / max(frames_total, 1), 5),
                        "parallelism": f"streams sharded {S}/GPU over {world} rank(s), no collective; "
                                       f"{P} consecutive picture(s) of each stream per launch"},
-            "roofline": {"kernel": f"k_wgpp (one launch = {P} step(s); k_prep of the next launch runs in its tail)",
+            "roofline": {"kernel": f"k_wgpp (one launch = {P} step(s)" + (", one step when it would hold an IDR" if P > 1 and phases else "") +
+                                   "; k_prep of the next launch runs in its tail)",
                          # what limits the kernel: the MB-row deblocking dependency chain
                          # (DESIGN.md §3), not HBM; `frac` is still quoted against the HBM
                          # peak, the metric's axis
@@ -1061,10 +1121,14 @@ def main(argv=None):
                          # over the whole timed window (every launch by default),
                          # with the launches holding an IDR and the P-only ones apart
                          "avg_launch_kernel_us": round(step_us, 2),
+                         "avg_kernel_us_per_step": round(sum(per_launch) / max(1, sum(
+                             len(run.launches[i]) for i in sampled[:len(per_launch)])), 2) if per_launch else None,
                          "timed_launches_sampled": len(sampled),
                          "sampling_stride": stride,
-                         "launches_with_idr": {"n": split["i"][0], "avg_launch_kernel_us": split["i"][1]} if split else None,
-                         "launches_p_only": {"n": split["p"][0], "avg_launch_kernel_us": split["p"][1]} if split else None,
+                         "launches_with_idr": {"n": split["i"][0], "avg_launch_kernel_us": split["i"][1],
+                                               "avg_us_per_step": split["i"][2]} if split else None,
+                         "launches_p_only": {"n": split["p"][0], "avg_launch_kernel_us": split["p"][1],
+                                             "avg_us_per_step": split["p"][2]} if split else None,
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
             "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S * P,

@@ -146,6 +146,9 @@ def mi() -> C.CDLL:
     L.h264mi_engine_decode_device_next.restype = i32
     L.h264mi_engine_decode_device_steps.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp]
     L.h264mi_engine_decode_device_steps.restype = i32
+    if hasattr(L, "h264mi_engine_decode_device_steps_next"):
+        L.h264mi_engine_decode_device_steps_next.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, i32]
+        L.h264mi_engine_decode_device_steps_next.restype = i32
     L.h264mi_engine_set_steps.argtypes = [vp, i32]
     L.h264mi_engine_set_steps.restype = i32
     L.h264mi_set_share.argtypes = [i32]

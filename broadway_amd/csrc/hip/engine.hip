@@ -42,6 +42,7 @@ struct h264mi_engine {
     // a batch prepped by the previous launch's tail workgroups is `prepped`
     int prep_parity;
     const void *prepped_rec, *prepped_pics;
+    int prepped_n;                            // pictures the tail prepped
     unsigned long long *d_rows_done;   // row workgroups finished, all launches (tail-prep trigger)
     // k_conceal inputs (order + decoded flags): pinned staging, device copy,
     // and an event after the upload (the staging's reuse waits for it)
@@ -304,7 +305,7 @@ static int launch_nmc(const h264mi_engine *e, int rpw)
 
 static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, const int16_t *d_coef,
                         const PicDesc *d_pics, const MbRec *next_rec, const int16_t *next_coef,
-                        const PicDesc *next_pics)
+                        const PicDesc *next_pics, int next_npics = -1)
 {
     const int npics = S * P;
     const size_t mbs = (size_t)e->pipe_cap * e->nmbs;
@@ -314,7 +315,9 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     // the next batch's prep work beside the chain
     static const bool no_tail = getenv("H264MI_NO_TAIL_PREP") && atoi(getenv("H264MI_NO_TAIL_PREP"));
     if (no_tail) next_rec = nullptr, next_coef = nullptr, next_pics = nullptr;
-    if (!(e->prepped_rec && e->prepped_rec == (const void *)d_rec && e->prepped_pics == (const void *)d_pics))
+    if (next_npics < 0) next_npics = npics;
+    if (!(e->prepped_rec && e->prepped_rec == (const void *)d_rec && e->prepped_pics == (const void *)d_pics &&
+          e->prepped_n == npics))
         if (launch_prep(e, npics, d_rec, d_coef, d_pics, hb)) return -1;
     ReconArgs a;
     memset(&a, 0, sizeof(a));
@@ -360,7 +363,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         a.n_rec = next_rec; a.n_coef = next_coef; a.n_pics = next_pics;
         a.n_dbrec = e->d_dbrec + (hb ^ 1) * mbs * 64;
         a.n_res = e->d_res + (hb ^ 1) * mbs * 384;
-        a.n_nmbs_total = npics * e->nmbs;
+        a.n_nmbs_total = next_npics * e->nmbs;
     } else {
         a.rows_done = e->d_rows_done;
     }
@@ -422,6 +425,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     e->rows_launched += rows;
     e->prepped_rec = next_rec;
     e->prepped_pics = next_pics;
+    e->prepped_n = next_npics;
     e->prep_parity = hb ^ 1;                  // the half the next batch was (or will be) prepped into
     return 0;
 }
@@ -522,6 +526,21 @@ extern "C" int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P,
     HIPCHECK(hipSetDevice(e->dev));
     return launch_batch(e, S, P, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
                         next_coef, (const PicDesc *)next_pics);
+}
+
+// the same, naming the next batch's steps (1 .. the engine's steps) when it
+// has a different count: its k_prep in this launch's tail covers S * next_P
+// pictures (a plan mixing one- and two-step launches keeps its tail preps)
+extern "C" int h264mi_engine_decode_device_steps_next(h264mi_engine *e, int S, int P, const void *d_recs,
+                                                      const int16_t *d_coef, const void *d_pics,
+                                                      const void *next_recs, const int16_t *next_coef,
+                                                      const void *next_pics, int next_P)
+{
+    if (!e || S < 1 || S > e->nstreams || P < 1 || P > e->steps || !d_recs || !d_pics) return -1;
+    if (!next_recs || !next_pics || next_P < 1 || next_P > e->steps) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    return launch_batch(e, S, P, (const MbRec *)d_recs, d_coef, (const PicDesc *)d_pics, (const MbRec *)next_recs,
+                        next_coef, (const PicDesc *)next_pics, S * next_P);
 }
 
 // diagnostics: resident k_wgpp workgroups per CU the runtime computes for

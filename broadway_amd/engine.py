@@ -130,6 +130,18 @@ class Engine:
                                                      n_recs or None, n_coef or None, n_pics or None) != 0:
             raise RuntimeError("h264mi_engine_decode_device_steps failed")
 
+    def decode_device_steps_next(self, S: int, P: int, d_recs: int, d_coef: int, d_pics: int,
+                                 n_recs: int, n_coef: int, n_pics: int, next_P: int) -> bool:
+        """decode_device_steps with the next batch's step count when it
+        differs (its k_prep over S * next_P pictures in this launch's tail).
+        False: the library predates it (nothing launched)."""
+        if not hasattr(self._L, "h264mi_engine_decode_device_steps_next"):
+            return False
+        if self._L.h264mi_engine_decode_device_steps_next(self._h, S, P, d_recs, d_coef, d_pics,
+                                                          n_recs, n_coef, n_pics, next_P) != 0:
+            raise RuntimeError("h264mi_engine_decode_device_steps_next failed")
+        return True
+
     def read(self, stream: int, slot: int) -> np.ndarray:
         out = np.empty(self.frame_bytes, dtype=np.uint8)
         if self._L.h264mi_engine_read(self._h, stream, slot, out.ctypes.data) != 0:

@@ -225,6 +225,12 @@ int h264mi_engine_decode_device_next(h264mi_engine *e, int npics, const void *d_
 int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P, const void *d_recs, const int16_t *d_coef,
                                       const void *d_pics, const void *next_recs, const int16_t *next_coef,
                                       const void *next_pics);
+/* The same, naming the next batch's step count next_P (1 .. steps) when it
+ * differs from P: the next batch's k_prep runs in this launch's tail over its
+ * S * next_P pictures (a plan mixing one- and two-step launches). */
+int h264mi_engine_decode_device_steps_next(h264mi_engine *e, int S, int P, const void *d_recs,
+                                           const int16_t *d_coef, const void *d_pics, const void *next_recs,
+                                           const int16_t *next_coef, const void *next_pics, int next_P);
 int h264mi_engine_set_steps(h264mi_engine *e, int steps);
 
 int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */

@@ -1,0 +1,90 @@
+"""bench.py's launch plans on the CPU (dry engine): the GOP-staggered plan
+with one and with two steps per launch (frame-pipelined launches, verdict
+r03 #8).  Every stream must see its pictures in cyclic decode order, the
+pre-roll must bring stream s to its phase, a two-step launch must pair
+pictures (k, k+1) of every stream with k even, and the descriptor table must
+hold exactly the plan's pictures."""
+import bench
+from broadway_amd import gen
+from broadway_amd.engine import Capture
+
+
+def _walk(launches, S):
+    """Per stream, the picture sequence the plan decodes."""
+    seq = [[] for _ in range(S)]
+    for launch in launches:
+        for step in launch:
+            for s, k in enumerate(step):
+                seq[s].append(k)
+    return seq
+
+
+def test_gop_phases_whole_launches():
+    assert bench.gop_phases(8, 60) == [0, 7, 15, 22, 30, 37, 45, 52]
+    assert bench.gop_phases(8, 60, 2) == [0, 6, 14, 22, 30, 36, 44, 52]
+    assert all(p % 2 == 0 for p in bench.gop_phases(5, 60, 2))
+
+
+def test_launch_plan_pipe2_cyclic():
+    N, S, W, K = 60, 8, 4, 56
+    ph = bench.gop_phases(S, N, 2)
+    launches, R = bench.launch_plan(N, S, W, K, ph, None, 2)
+    assert R == max(ph)
+    assert all(len(x) == 1 for x in launches[:R]) and all(len(x) == 2 for x in launches[R:])
+    for launch in launches[R:]:
+        for s in range(S):
+            a, b = launch[0][s], launch[1][s]
+            assert a % 2 == 0 and b == a + 1
+    seq = _walk(launches, S)
+    for s in range(S):
+        main = seq[s][R:]
+        assert main == [(v + ph[s]) % N for v in range(W + K)]
+        # pre-roll: repeats of the IDR, then pictures 0 .. phase-1 in order
+        pre = [k for k in seq[s][:R]]
+        tail = pre[R - ph[s]:] if ph[s] else []
+        assert tail == list(range(ph[s])) and all(k == 0 for k in pre[:R - ph[s]])
+
+
+def _caps(n=3, frames=12):
+    streams = [gen.generate(2, 90 + i, nframes=frames, w_mbs=13, h_mbs=7, crop_bottom=0, slices=2, gop=frames)
+               for i in range(n)]
+    return [Capture(s) for s in streams]
+
+
+def test_device_run_pipe2_gop_plan_descriptors():
+    caps = _caps()
+    S, N = len(caps), 12
+    ph = bench.gop_phases(S, N, 2)
+    run = bench.DeviceRun(None, caps, 2, 8, 2, dry=True, phases=ph)
+    assert run.P == 2
+    # launches holding an IDR run one step at a time, the others two
+    main = run.launches[run.n_pre:]
+    assert all(not run.holds_idr(x) for x in main if len(x) == 2)
+    singles = [j for j, x in enumerate(main) if len(x) == 1]
+    assert len(singles) % 2 == 0 and singles
+    for j in singles[::2]:
+        assert len(main[j + 1]) == 1 and run.holds_idr(main[j] + main[j + 1])
+    assert sum(len(x) for x in main) == 10
+    assert sum(len(x) for x in main[:run.n_warm - run.n_pre]) == 2
+    seq = _walk(main, S)
+    assert all(seq[s] == [(v + ph[s]) % N for v in range(10)] for s in range(S))
+    # the table, launch by launch, is the plan's pictures step-major
+    assert run.desc_off[-1] == sum(len(x) for x in run.launches) * S * 32
+    # a two-step launch's pictures write distinct slots
+    for launch in [x for x in main if len(x) == 2]:
+        for s in range(S):
+            assert run.slot_of[launch[0][s]][s] != run.slot_of[launch[1][s]][s]
+    for i in range(len(run.launches)):
+        run.launch(i)
+    assert run.eng.launches == len(run.launches)
+    # the P-only window of bench.main: phases [2]*S, whole launches
+    run.set_plan(2, 6, [2] * S)
+    assert all(not run.is_i[k][s] for s, k in run.timed_pictures())
+    run.free()
+
+
+def test_device_run_odd_plan_falls_back_to_one_step():
+    caps = _caps()
+    run = bench.DeviceRun(None, caps, 3, 8, 2, dry=True, phases=bench.gop_phases(len(caps), 12, 2))
+    assert run.P == 1 and all(len(x) == 1 for x in run.launches)
+    run.free()

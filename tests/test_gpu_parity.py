@@ -183,27 +183,32 @@ def test_engine_bench_streams_vs_reference(rpw, mc, monkeypatch):
     assert eng.errors() == 0
 
 
-@pytest.mark.parametrize("rank,pipe", [(r, 2) for r in range(8)] + [(0, 1), (1, 1)])
-def test_configs3_shard_vs_reference(rank, pipe):
+@pytest.mark.parametrize("rank,pipe,staggered",
+                         [(r, 2, True) for r in range(8)] + [(0, 1, True), (1, 1, True), (0, 2, False), (1, 2, False)])
+def test_configs3_shard_vs_reference(rank, pipe, staggered):
     """configs[3]: 64 streams, 8 per GPU.  Rank r's shard (seeds 100+8r ..
     100+8r+7, bench.shard_seeds) through bench.py's own device-resident path
     (bench.DeviceRun: records in HBM on the rank's engine, the next launch's
-    k_prep in each launch's tail) and its verification pass.  pipe 1: the
-    bench default -- GOP phases staggered over the streams, each 60-picture
-    stream decoded cyclically after an untimed pre-roll; pipe 2: two
-    consecutive pictures of every stream per launch (frame-pipelined
-    batches).  Every picture of every launch vs the reference MD5s, and after
-    the run every frame slot's last picture."""
+    k_prep in each launch's tail) and its verification pass.  staggered: GOP
+    phases staggered over the streams, each 60-picture stream decoded
+    cyclically after an untimed pre-roll -- with pipe 2 (the bench default)
+    two consecutive pictures of every stream per launch, one per launch where
+    a launch would hold an IDR; aligned: decode order from picture 0, every
+    launch two steps (frame-pipelined batches).  Every picture of every
+    launch vs the reference MD5s, and after the run every frame slot's last
+    picture."""
     import bench
     seeds = bench.shard_seeds(rank, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
-    phases = bench.gop_phases(8, n) if pipe == 1 else None
+    phases = bench.gop_phases(8, n, pipe) if staggered else None
     run = bench.DeviceRun(_lib.mi(), caps, 4, n - 4, pipe, phases=phases)
     try:
         assert run.P == pipe and all(d == 0 for _, d in run.placement())
-        if pipe == 1:
-            assert run.n_pre == max(phases) and len(run.launches) == run.n_pre + n
+        if staggered:
+            steps = sum(len(x) for x in run.launches[run.n_pre:])
+            assert run.n_pre == max(phases) and steps == n
+            assert all(not run.holds_idr(x) for x in run.launches[run.n_pre:] if len(x) > 1)
             timed = run.timed_pictures()
             assert sum(run.is_i[k][s] for s, k in timed) == 8 - 1     # stream 0's IDR falls in the warmup
         else:
