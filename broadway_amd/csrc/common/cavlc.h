@@ -15,14 +15,12 @@
  * order (coef[0] is the first coded scan position of the block).  Returns
  * TotalCoeff (>= 0) or -1 on a syntax error. */
 int cavlc_decode_block(BitReader *br, int nC, int maxcoef, int16_t *coef);
-/* same, also returning the sum of |level| (the host residual range bound);
- * inline: the parser's call sites pass constant maxcoef (16, 15, 4), which
- * the compiler folds into the clear, the range checks and the table choice */
-static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, uint32_t *abs_sum)
+/* One block through the BitReader (any position, end of buffer included):
+ * the path for blocks that start within CAVLC_SLACK bytes of the end. */
+static inline int cavlc_block_checked_(BitReader *br, int nC, int maxcoef, int16_t *coef, uint32_t *abs_sum)
 {
     int len;
     *abs_sum = 0;
-    /* constant sizes: inlined stores instead of a library call per block */
     if (maxcoef == 16) memset(coef, 0, 32);
     else if (maxcoef == 15) memset(coef, 0, 30);
     else memset(coef, 0, sizeof(int16_t) * (size_t)maxcoef);
@@ -36,16 +34,14 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
     int level[16];
     int suffix_len = (tc > 10 && t1 < 3) ? 1 : 0;
     int i = 0;
-    if (t1) {                                    /* trailing_ones_sign_flags, one read */
+    if (t1) {
         const uint32_t sg = br_u(br, t1);
         for (; i < t1; i++) level[i] = ((sg >> (t1 - 1 - i)) & 1) ? -1 : 1;
         *abs_sum += (uint32_t)t1;
     }
     for (; i < tc; i++) {
-        /* level_prefix (leading zero bits then a one, §9.2.2.1) and
-         * level_suffix from one 32-bit window: prefix <= 15, suffix <= 12 */
         const uint32_t w = br_peek(br, 32);
-        if ((w >> 16) == 0) return -1;           /* level_prefix > 15 */
+        if ((w >> 16) == 0) return -1;
         const int prefix = __builtin_clz(w);
         int ssize = suffix_len;
         if (prefix == 14 && suffix_len == 0) ssize = 4;
@@ -73,7 +69,7 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
     }
 
     int zeros_left = total_zeros;
-    int pos = tc + total_zeros - 1;              /* scan index of highest coefficient */
+    int pos = tc + total_zeros - 1;
     for (int i = 0; i < tc; i++) {
         coef[pos] = (int16_t)level[i];
         int run = 0;
@@ -90,6 +86,131 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
         pos -= 1 + run;
     }
     if (br->err) return -1;
+    return tc;
+}
+
+/* the longest residual block is 641 bits (coeff_token 16 + 3 sign bits + 15
+ * levels of 28 bits + ... + total_zeros 9 + 14 run_before of 11 bits); a
+ * block starting CAVLC_SLACK bytes or more before the end cannot read past it
+ * even with the 8-byte window below */
+#define CAVLC_SLACK 96
+
+/* 32 stream bits at bit position pos, MSB first (8 readable bytes at pos/8) */
+static inline uint32_t cavlc_bits32_(const uint8_t *buf, size_t pos)
+{
+    uint64_t v;
+    memcpy(&v, buf + (pos >> 3), 8);
+    return (uint32_t)((__builtin_bswap64(v) << (pos & 7)) >> 32);
+}
+
+/* same, also returning the sum of |level| (the host residual range bound);
+ * inline: the parser's call sites pass constant maxcoef (16, 15, 4), which
+ * the compiler folds into the clear, the range checks and the table choice.
+ * Away from the end of the buffer the block is read with a local bit
+ * position and unchecked 8-byte windows (no per-field bounds or cache
+ * checks), packed one-load VLC tables and a branch-free suffixLength update;
+ * the stream position on every return, error returns included, is the one
+ * the checked path leaves. */
+static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, uint32_t *abs_sum)
+{
+    if (__builtin_expect((br->pos >> 3) + CAVLC_SLACK > br->size, 0))
+        return cavlc_block_checked_(br, nC, maxcoef, coef, abs_sum);
+    const uint8_t *const buf = br->buf;
+    size_t pos = br->pos;
+    /* nC -1 .. 16 -> coeff_token table (Table 9-5 columns) */
+    static const uint8_t kClass[18] = {4, 0, 0, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 3};
+    uint32_t e = vlc_pk(&gCoeffTokenPk[kClass[nC + 1]], cavlc_bits32_(buf, pos) >> 16);
+    if (maxcoef == 16) memset(coef, 0, 32);
+    else if (maxcoef == 15) memset(coef, 0, 30);
+    else memset(coef, 0, sizeof(int16_t) * (size_t)maxcoef);
+    if (!e) return -1;
+    pos += e & 31;
+    const int tc = (int)(e >> 7), t1 = (int)(e >> 5) & 3;
+    if (tc == 0) { br->pos = pos; *abs_sum = 0; return 0; }
+    if (tc > maxcoef) { br->pos = pos; return -1; }
+
+    int level[16];
+    uint32_t sum = (uint32_t)t1;
+    int i = 0;
+    {                                            /* trailing_ones_sign_flags: up to 3 */
+        const uint32_t sg = cavlc_bits32_(buf, pos);
+        level[0] = 1 - 2 * (int)(sg >> 31);
+        level[1] = 1 - 2 * (int)((sg >> 30) & 1);
+        level[2] = 1 - 2 * (int)((sg >> 29) & 1);
+        pos += t1;
+        i = t1;
+    }
+    int suffix_len = (tc > 10 && t1 < 3) ? 1 : 0;
+    for (; i < tc; i++) {
+        const uint32_t w = cavlc_bits32_(buf, pos);
+        if (__builtin_expect((w >> 16) == 0, 0)) { br->pos = pos; return -1; }   /* level_prefix > 15 */
+        const int prefix = __builtin_clz(w);
+        int code, used;
+        if (__builtin_expect(prefix < 14, 1)) {
+            /* suffix of suffix_len bits (0: none) */
+            code = (prefix << suffix_len) + (int)(((uint64_t)(w << prefix << 1)) >> (32 - suffix_len));
+            used = prefix + 1 + suffix_len;
+        } else {
+            const int ssize = prefix == 15 ? 12 : (suffix_len ? suffix_len : 4);
+            code = (prefix << suffix_len) + (int)((w << (prefix + 1)) >> (32 - ssize));
+            if (prefix == 15 && suffix_len == 0) code += 15;
+            used = prefix + 1 + ssize;
+        }
+        pos += used;
+        code += (i == t1 && t1 < 3) ? 2 : 0;
+        const int mag = (code + 2) >> 1;
+        const int neg = code & 1;
+        level[i] = neg ? -mag : mag;
+        sum += (uint32_t)mag;
+        suffix_len += suffix_len == 0;
+        suffix_len += (mag > (3 << (suffix_len - 1))) & (suffix_len < 6);
+    }
+
+    int total_zeros = 0;
+    if (tc < maxcoef) {
+        const VlcPk *t = (maxcoef == 4) ? &gTotalZerosDcPk[tc - 1] : &gTotalZerosPk[tc - 1];
+        const uint32_t z = vlc_pk(t, cavlc_bits32_(buf, pos) >> 16);
+        if (!z) { br->pos = pos; return -1; }
+        pos += z & 31;
+        total_zeros = (int)(z >> 5);
+        if (tc + total_zeros > maxcoef) { br->pos = pos; return -1; }
+    }
+
+    /* levels from the highest scan position down, run_before between them
+     * (Table 9-10): zerosLeft 1..6 codes are at most 3 bits (kRunSmall, row
+     * 0 = zerosLeft 0: no code); above 6, 1..3-bit 'run = 7 - code' or
+     * leading zeros then a one, 'run = zeros + 4' -- no branch per field */
+    static const uint8_t kRunSmall[7][8] = {
+        {0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00},
+        {0x11, 0x11, 0x11, 0x11, 0x01, 0x01, 0x01, 0x01},   /* 1: 1 | 0 */
+        {0x22, 0x22, 0x12, 0x12, 0x01, 0x01, 0x01, 0x01},   /* 2: 1 | 01 | 00 */
+        {0x32, 0x32, 0x22, 0x22, 0x12, 0x12, 0x02, 0x02},   /* 3: 11 10 01 00 */
+        {0x43, 0x33, 0x22, 0x22, 0x12, 0x12, 0x02, 0x02},   /* 4: 11 10 01 001 000 */
+        {0x53, 0x43, 0x33, 0x23, 0x12, 0x12, 0x02, 0x02},   /* 5: 11 10 011 010 001 000 */
+        {0x13, 0x23, 0x43, 0x33, 0x63, 0x53, 0x02, 0x02},   /* 6: 11 000 001 011 010 101 100 */
+    };
+    int zeros_left = total_zeros;
+    int at = tc + total_zeros - 1;
+    for (i = 0; i < tc - 1; i++) {
+        coef[at] = (int16_t)level[i];
+        const uint32_t w = cavlc_bits32_(buf, pos);
+        const uint32_t top3 = w >> 29;
+        const int lz = __builtin_clz(w | 1);
+        const int small = kRunSmall[zeros_left < 7 ? zeros_left : 0][top3];
+        const int big = zeros_left > 6;
+        const int run = big ? (top3 ? 7 - (int)top3 : lz + 4) : small >> 4;
+        const int len = big ? (top3 ? 3 : lz + 1) : small & 15;
+        if (__builtin_expect(run > zeros_left || (big & (lz > 10)), 0)) {
+            br->pos = pos + (run > zeros_left && !(big & (lz > 10)) ? len : 0);
+            return -1;
+        }
+        pos += len;
+        zeros_left -= run;
+        at -= 1 + run;
+    }
+    coef[at] = (int16_t)level[tc - 1];           /* the rest of the zeros lie below it */
+    br->pos = pos;
+    *abs_sum = sum;
     return tc;
 }
 

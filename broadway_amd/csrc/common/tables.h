@@ -58,6 +58,26 @@ extern VlcTable gTotalZerosDec[15];
 extern VlcTable gTotalZerosDcDec[3];
 extern VlcTable gRunBeforeDec[7];
 
+/* the same tables packed for the parser's fast path: one 16-bit entry per
+ * 8-bit index, (sym << 5) | len (len 1..16), 0 = invalid, 0x8000 | k = the
+ * k-th 256-entry subtable of the next 8 bits (contiguous in sub) */
+typedef struct {
+    uint16_t t[256];
+    uint16_t *sub;
+} VlcPk;
+extern VlcPk gCoeffTokenPk[5];
+extern VlcPk gTotalZerosPk[15];
+extern VlcPk gTotalZerosDcPk[3];
+extern VlcPk gRunBeforePk[7];
+
+/* entry for a 16-bit window (MSB = next stream bit): len = e & 31, sym = e >> 5 */
+static inline uint32_t vlc_pk(const VlcPk *t, uint32_t peek16)
+{
+    uint32_t e = t->t[peek16 >> 8];
+    if (__builtin_expect(e & 0x8000, 0)) e = t->sub[((e & 0x7FFFu) << 8) | (peek16 & 0xFFu)];
+    return e;
+}
+
 void h264_tables_init(void);   /* idempotent, thread-safe */
 /* returns sym or -1; inline: the CAVLC decode calls it several times per
  * coded block */

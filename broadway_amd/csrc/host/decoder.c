@@ -541,9 +541,14 @@ static int decode_nal(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic
          * there (specparse.c), else parses them itself */
         if (first_slice && !spec_active_for(d->spec, buf))
             spec_launch(d->spec, d, sps, pps, &nh, &sh, buf, *read_bytes, len);
-        if (spec_take(d->spec, d, buf, *read_bytes, &sh, pps, ref_slot)) {
-            /* taken: identical to parsing it here */
-        } else if (parse_slice_data(&d->pb, &br, &sh, pps, ref_slot)) {
+        const int st = spec_stats_on(d->spec);
+        const double c0 = st ? spec_thread_cpu() : 0.0;
+        const int nd0 = d->pb.ndecoded;
+        int taken = 0, perr = 0;
+        if (spec_take(d->spec, d, buf, *read_bytes, &sh, pps, ref_slot)) taken = 1;   /* identical to parsing it here */
+        else perr = parse_slice_data(&d->pb, &br, &sh, pps, ref_slot);
+        if (st && !taken) spec_account_main(d->spec, spec_thread_cpu() - c0, d->pb.ndecoded - nd0);
+        if (perr) {
             /* the slice is un-marked (decoder.c:462-467, slice_data.c:302-358);
              * its MBs are concealed at the next access-unit boundary */
             picbuild_mark_slice_corrupted(&d->pb, sh.first_mb);

@@ -148,6 +148,10 @@ void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps,
 int  spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
                const Pps *pps, const int *ref_slot);
 void spec_launch_ahead(SpecPool *sp, const H264Dec *d, const uint8_t *buf, uint32_t len);
+/* H264MI_SPEC_STATS: thread CPU per MB of worker and caller parses */
+int  spec_stats_on(const SpecPool *sp);
+double spec_thread_cpu(void);
+void spec_account_main(SpecPool *sp, double cpu, int mbs);
 int  spec_active_for(const SpecPool *sp, const uint8_t *buf);
 const Sps *h264dec_active_sps(const H264Dec *d);
 

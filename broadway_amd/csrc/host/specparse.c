@@ -21,6 +21,7 @@
 
 #include <pthread.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -55,6 +56,9 @@ struct SpecPool {
     int              order[SPEC_MAX_JOBS];
     int              running;
     unsigned long    taken, declined;   /* statistics (H264MI_SPEC_STATS) */
+    int              stats;
+    double           w_cpu, c_cpu, m_cpu;   /* thread CPU: worker jobs, commits, the caller's own slices */
+    unsigned long    w_mbs, m_mbs;
     /* snapshot of the picture the jobs belong to */
     Sps              sps;
     Pps              pps;
@@ -64,6 +68,13 @@ struct SpecPool {
     NalHdr           nh;
     int              w, h, cip, cur_slot;
 };
+
+static double thread_cpu(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
 
 static void run_job(SpecPool *sp, SpecJob *j)
 {
@@ -118,8 +129,13 @@ static void *worker(void *arg)
         j->started = 1;
         sp->running++;
         pthread_mutex_unlock(&sp->mu);
+        const double t0 = sp->stats ? thread_cpu() : 0.0;
         run_job(sp, j);
         pthread_mutex_lock(&sp->mu);
+        if (sp->stats) {
+            sp->w_cpu += thread_cpu() - t0;
+            if (j->ok) sp->w_mbs += (unsigned long)j->pb.ndecoded;
+        }
         j->done = 1;
         sp->running--;
         pthread_cond_broadcast(&sp->cv_done);
@@ -133,6 +149,7 @@ SpecPool *spec_create(int nthreads)
     if (nthreads < 1) return NULL;
     SpecPool *sp = (SpecPool *)calloc(1, sizeof(SpecPool));
     if (!sp) return NULL;
+    sp->stats = getenv("H264MI_SPEC_STATS") != NULL;
     pthread_mutex_init(&sp->mu, NULL);
     pthread_cond_init(&sp->cv_work, NULL);
     pthread_cond_init(&sp->cv_done, NULL);
@@ -157,8 +174,12 @@ void spec_drain(SpecPool *sp)
 void spec_destroy(SpecPool *sp)
 {
     if (!sp) return;
-    if (getenv("H264MI_SPEC_STATS"))
-        fprintf(stderr, "h264mi: speculative slices taken %lu, parsed again %lu\n", sp->taken, sp->declined);
+    if (sp->stats)
+        fprintf(stderr, "h264mi: speculative slices taken %lu, parsed again %lu; thread CPU per MB: workers %.3f us "
+                "(%lu MBs), caller %.3f us (%lu MBs), commits %.3f us per taken MB\n", sp->taken, sp->declined,
+                1e6 * sp->w_cpu / (double)(sp->w_mbs ? sp->w_mbs : 1), sp->w_mbs,
+                1e6 * sp->m_cpu / (double)(sp->m_mbs ? sp->m_mbs : 1), sp->m_mbs,
+                1e6 * sp->c_cpu / (double)(sp->w_mbs ? sp->w_mbs : 1));
     pthread_mutex_lock(&sp->mu);
     sp->stop = 1;
     pthread_cond_broadcast(&sp->cv_work);
@@ -312,7 +333,9 @@ int spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes,
         while (!j->done) pthread_cond_wait(&sp->cv_done, &sp->mu);
     }
     pthread_mutex_unlock(&sp->mu);
+    const double t0 = sp->stats ? thread_cpu() : 0.0;
     const int r = j && j->ok && commit(sp, j, d, buf, read_bytes, sh, pps, ref_slot);
+    if (sp->stats) sp->c_cpu += thread_cpu() - t0;
     if (j) { if (r) sp->taken++; else sp->declined++; }
     return r;
 }
@@ -352,4 +375,14 @@ static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint
     pb->n_intra += q->n_intra;
     pb->n_coded_blocks += q->n_coded_blocks;
     return 1;
+}
+
+/* statistics: the calling thread parsed a slice itself */
+int spec_stats_on(const SpecPool *sp) { return sp && sp->stats; }
+double spec_thread_cpu(void) { return thread_cpu(); }
+void spec_account_main(SpecPool *sp, double cpu, int mbs)
+{
+    if (!sp) return;
+    sp->m_cpu += cpu;
+    sp->m_mbs += (unsigned long)mbs;
 }

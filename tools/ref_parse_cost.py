@@ -86,12 +86,12 @@ def side_ref(fn, stem):
     return "other"
 
 
-def gprof_run(binary, paths, args, tmp, env=None):
+def gprof_run(binary, paths, args, tmp, env=None, post=()):
     for g in glob.glob(os.path.join(tmp, "gmon*")):
         os.remove(g)
     e = dict(os.environ, GMON_OUT_PREFIX=os.path.join(tmp, "gmon"), **(env or {}))
     for p in paths:
-        subprocess.run([binary] + args + [p], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+        subprocess.run([binary] + args + [p] + list(post), stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                        check=True, cwd=tmp, env=e)
     files = sorted(glob.glob(os.path.join(tmp, "gmon.*")))
     subprocess.run(["gprof", "-s", binary] + files, check=True, cwd=tmp, capture_output=True)
@@ -172,7 +172,7 @@ def main():
               f"{1e3 * cpu / pics:.2f} ms CPU/picture")
         ours_pg = build_ours(tmp, True)
         omap = func_files(ours_pg)
-        rows = gprof_run(ours_pg, paths, [], tmp, {"H264MI_PARSE_THREADS": "0"})
+        rows = gprof_run(ours_pg, paths, [], tmp, {"H264MI_PARSE_THREADS": "0"}, post=["5"])   # 5 passes: samples
         report("product host parse, gprof split by file", rows, lambda fn: omap.get(fn, "?"), pics, cpu)
 
 
