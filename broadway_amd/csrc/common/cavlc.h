@@ -95,20 +95,22 @@ static inline int cavlc_block_checked_(BitReader *br, int nC, int maxcoef, int16
  * even with the 8-byte window below */
 #define CAVLC_SLACK 96
 
-/* 32 stream bits at bit position pos, MSB first (8 readable bytes at pos/8) */
-static inline uint32_t cavlc_bits32_(const uint8_t *buf, size_t pos)
+/* 64 stream bits at bit position pos, MSB first, the low (pos & 7) of them
+ * zero (8 readable bytes at pos / 8) */
+static inline uint64_t cavlc_load64_(const uint8_t *buf, size_t pos)
 {
     uint64_t v;
     memcpy(&v, buf + (pos >> 3), 8);
-    return (uint32_t)((__builtin_bswap64(v) << (pos & 7)) >> 32);
+    return __builtin_bswap64(v) << (pos & 7);
 }
 
 /* same, also returning the sum of |level| (the host residual range bound);
  * inline: the parser's call sites pass constant maxcoef (16, 15, 4), which
  * the compiler folds into the clear, the range checks and the table choice.
- * Away from the end of the buffer the block is read with a local bit
- * position and unchecked 8-byte windows (no per-field bounds or cache
- * checks), packed one-load VLC tables and a branch-free suffixLength update;
+ * Away from the end of the buffer the block is read through a 64-bit
+ * register cache refilled with unchecked 8-byte loads (a field costs a table
+ * load and a shift on the dependency chain, no per-field bounds checks),
+ * packed one-load VLC tables and a branch-free suffixLength / run_before;
  * the stream position on every return, error returns included, is the one
  * the checked path leaves. */
 static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int16_t *coef, uint32_t *abs_sum)
@@ -116,33 +118,36 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
     if (__builtin_expect((br->pos >> 3) + CAVLC_SLACK > br->size, 0))
         return cavlc_block_checked_(br, nC, maxcoef, coef, abs_sum);
     const uint8_t *const buf = br->buf;
-    size_t pos = br->pos;
+    size_t pos = br->pos;                        /* position of the cache's first bit */
+    uint64_t c = cavlc_load64_(buf, pos);
+    int avail = 64 - (int)(pos & 7);             /* valid bits in c (>= 32 before every field) */
+#define CV_NEED(n) do { if (avail < (n)) { c = cavlc_load64_(buf, pos); avail = 64 - (int)(pos & 7); } } while (0)
+#define CV_SKIP(n) do { const int n_ = (n); c <<= n_; avail -= n_; pos += (size_t)n_; } while (0)
     /* nC -1 .. 16 -> coeff_token table (Table 9-5 columns) */
     static const uint8_t kClass[18] = {4, 0, 0, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3, 3, 3, 3};
-    uint32_t e = vlc_pk(&gCoeffTokenPk[kClass[nC + 1]], cavlc_bits32_(buf, pos) >> 16);
+    const uint32_t e = vlc_pk(&gCoeffTokenPk[kClass[nC + 1]], (uint32_t)(c >> 48));
     if (maxcoef == 16) memset(coef, 0, 32);
     else if (maxcoef == 15) memset(coef, 0, 30);
     else memset(coef, 0, sizeof(int16_t) * (size_t)maxcoef);
     if (!e) return -1;
-    pos += e & 31;
+    CV_SKIP((int)(e & 31));
     const int tc = (int)(e >> 7), t1 = (int)(e >> 5) & 3;
     if (tc == 0) { br->pos = pos; *abs_sum = 0; return 0; }
     if (tc > maxcoef) { br->pos = pos; return -1; }
 
     int level[16];
     uint32_t sum = (uint32_t)t1;
-    int i = 0;
     {                                            /* trailing_ones_sign_flags: up to 3 */
-        const uint32_t sg = cavlc_bits32_(buf, pos);
-        level[0] = 1 - 2 * (int)(sg >> 31);
-        level[1] = 1 - 2 * (int)((sg >> 30) & 1);
-        level[2] = 1 - 2 * (int)((sg >> 29) & 1);
-        pos += t1;
-        i = t1;
+        level[0] = 1 - 2 * (int)(c >> 63);
+        level[1] = 1 - 2 * (int)((c >> 62) & 1);
+        level[2] = 1 - 2 * (int)((c >> 61) & 1);
+        CV_SKIP(t1);
     }
+    int i = t1;
     int suffix_len = (tc > 10 && t1 < 3) ? 1 : 0;
     for (; i < tc; i++) {
-        const uint32_t w = cavlc_bits32_(buf, pos);
+        CV_NEED(32);
+        const uint32_t w = (uint32_t)(c >> 32);
         if (__builtin_expect((w >> 16) == 0, 0)) { br->pos = pos; return -1; }   /* level_prefix > 15 */
         const int prefix = __builtin_clz(w);
         int code, used;
@@ -156,7 +161,7 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
             if (prefix == 15 && suffix_len == 0) code += 15;
             used = prefix + 1 + ssize;
         }
-        pos += used;
+        CV_SKIP(used);
         code += (i == t1 && t1 < 3) ? 2 : 0;
         const int mag = (code + 2) >> 1;
         const int neg = code & 1;
@@ -168,10 +173,11 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
 
     int total_zeros = 0;
     if (tc < maxcoef) {
+        CV_NEED(16);
         const VlcPk *t = (maxcoef == 4) ? &gTotalZerosDcPk[tc - 1] : &gTotalZerosPk[tc - 1];
-        const uint32_t z = vlc_pk(t, cavlc_bits32_(buf, pos) >> 16);
+        const uint32_t z = vlc_pk(t, (uint32_t)(c >> 48));
         if (!z) { br->pos = pos; return -1; }
-        pos += z & 31;
+        CV_SKIP((int)(z & 31));
         total_zeros = (int)(z >> 5);
         if (tc + total_zeros > maxcoef) { br->pos = pos; return -1; }
     }
@@ -193,7 +199,8 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
     int at = tc + total_zeros - 1;
     for (i = 0; i < tc - 1; i++) {
         coef[at] = (int16_t)level[i];
-        const uint32_t w = cavlc_bits32_(buf, pos);
+        CV_NEED(16);
+        const uint32_t w = (uint32_t)(c >> 32);
         const uint32_t top3 = w >> 29;
         const int lz = __builtin_clz(w | 1);
         const int small = kRunSmall[zeros_left < 7 ? zeros_left : 0][top3];
@@ -204,10 +211,12 @@ static inline int cavlc_decode_block_sum(BitReader *br, int nC, int maxcoef, int
             br->pos = pos + (run > zeros_left && !(big & (lz > 10)) ? len : 0);
             return -1;
         }
-        pos += len;
+        CV_SKIP(len);
         zeros_left -= run;
         at -= 1 + run;
     }
+#undef CV_NEED
+#undef CV_SKIP
     coef[at] = (int16_t)level[tc - 1];           /* the rest of the zeros lie below it */
     br->pos = pos;
     *abs_sum = sum;

@@ -34,7 +34,17 @@ static int nn_chroma(const MbInfo *m, int comp, int blk);
 void mbctx_begin_mb(PicCtx *pc, int cur)
 {
     pc->nb_key = 0;
-    for (int n = 0; n < 4; n++) pc->nb[n] = neighbour_of(pc, cur, n);
+    {
+        /* neighbour_of for the four, one division */
+        const int w = pc->w, col = cur % w;
+        const uint16_t sl = pc->mb[cur].slice;
+        const int a = col > 0 ? cur - 1 : -1, b = cur - w;
+        const int c = col < w - 1 ? cur - w + 1 : -1, d = col > 0 ? cur - w - 1 : -1;
+        pc->nb[NB_A] = a >= 0 && pc->mb[a].slice == sl ? a : -1;
+        pc->nb[NB_B] = b >= 0 && pc->mb[b].slice == sl ? b : -1;
+        pc->nb[NB_C] = c >= 0 && pc->mb[c].slice == sl ? c : -1;
+        pc->nb[NB_D] = d >= 0 && pc->mb[d].slice == sl ? d : -1;
+    }
     const MbInfo *A = pc->nb[NB_A] >= 0 ? &pc->mb[pc->nb[NB_A]] : NULL;
     const MbInfo *B = pc->nb[NB_B] >= 0 ? &pc->mb[pc->nb[NB_B]] : NULL;
     for (int i = 0; i < 4; i++) {

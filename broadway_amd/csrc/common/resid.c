@@ -56,13 +56,16 @@ int mb_residual_in_range(const int16_t *const *blk, const uint32_t *bsum, uint32
                          int qp, int qpc)
 {
     /* whole-MB bound first: every block's DC and AC magnitudes are at most
-     * the MB's level sum times the largest scale (DC transforms are sums of
-     * +-levels with smaller scales) */
+     * its component's level sum times that QP's largest scale (DC transforms
+     * are sums of +-levels with the smaller position-0 scale), luma at qp,
+     * chroma at qpc */
     {
-        uint32_t total = 0;
-        for (uint32_t m = cbits & 0x7FFFFFFu; m; m &= m - 1) total += bsum[__builtin_ctz(m)];
-        const int q6 = (qp > qpc ? qp : qpc) / 6;
-        if ((uint64_t)total * (uint64_t)(29 << q6) < 32000) return 1;
+        uint32_t tl = 0, tc = 0;
+        for (uint32_t m = cbits & 0x100FFFFu; m; m &= m - 1) tl += bsum[__builtin_ctz(m)];
+        for (uint32_t m = cbits & 0x6FF0000u; m; m &= m - 1) tc += bsum[__builtin_ctz(m)];
+        const uint64_t bound = (uint64_t)tl * (uint64_t)(kLevelScale[qp % 6][1] << (qp / 6)) +
+                               (uint64_t)tc * (uint64_t)(kLevelScale[qpc % 6][1] << (qpc / 6));
+        if (bound < 32000) return 1;
     }
     /* luma: h264bsdProcessLumaDc (transform.c:252-335) for I16, then one
      * ProcessBlock per block that has a DC or coded AC levels */

@@ -43,10 +43,13 @@ int h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be)
     d->aub_first_call = 1;
     d->cur_slot = -1;
     /* worker threads for speculative slice parsing: H264MI_PARSE_THREADS
-     * (default 3; 0 = off) */
-    const char *pt = getenv("H264MI_PARSE_THREADS");
+     * (default 3; 0 = none).  H264MI_PARSE_HELP (default 1): the calling
+     * thread, about to wait for a picture's reconstruction, parses the next
+     * picture's slices ahead itself (spec_help) -- with no workers too */
+    const char *pt = getenv("H264MI_PARSE_THREADS"), *ph = getenv("H264MI_PARSE_HELP");
     const int nth = pt ? atoi(pt) : 3;
-    d->spec = nth > 0 ? spec_create(nth > 16 ? 16 : nth) : NULL;
+    d->spec_help = ph ? atoi(ph) != 0 : 1;
+    d->spec = nth > 0 || d->spec_help ? spec_create(nth > 16 ? 16 : nth < 0 ? 0 : nth) : NULL;
     return 0;
 }
 
@@ -403,7 +406,10 @@ static int decode_nal(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic
 int h264dec_decode(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic_id, uint32_t *read_bytes)
 {
     const double t0 = h264dec_now(), s0 = d->t_submit;
+    const int st = spec_stats_on(d->spec);
+    const double c0 = st ? spec_thread_cpu() : 0.0;
     const int r = decode_nal(d, buf, len, pic_id, read_bytes);
+    if (st) spec_account_caller(d->spec, spec_thread_cpu() - c0);
     d->t_parse += h264dec_now() - t0 - (d->t_submit - s0);
     return r;
 }
@@ -588,6 +594,14 @@ const uint8_t *h264dec_next_output_rgba(H264Dec *d, uint32_t *pic_id, uint32_t *
     const DpbOut *o = dpb_next_output(&d->dpb);
     if (!o) return NULL;
     uint8_t *dst = rgba ? rgba : d->out_frames + d->frame_bytes * (size_t)o->slot;
+    /* rather than wait for the GPU, parse the next picture's slices that
+     * spec_launch_ahead queued (the buffer already holds them); the core
+     * stays busy and warm, and the decode call that follows takes them */
+    if (d->spec_help) {
+        const double h0 = h264dec_now();
+        spec_help(d->spec);
+        d->t_parse += h264dec_now() - h0;
+    }
     const double t0 = h264dec_now();
     if (d->be.sync && d->be.sync(d->be.ctx)) return NULL;
     const double t1 = h264dec_now();

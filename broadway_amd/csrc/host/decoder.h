@@ -106,6 +106,7 @@ typedef struct H264Dec {
     uint64_t pics_decoded, alg_ref_bytes, coded_blocks;
     /* speculative parallel slice parsing (specparse.c); NULL: off */
     SpecPool *spec;
+    int spec_help;              /* the caller parses ahead instead of waiting (H264MI_PARSE_HELP) */
     /* end-to-end time split (seconds): host parse, record upload + launch,
      * wait for the device, output copy; pictures output */
     double   t_parse, t_submit, t_wait, t_copy;
@@ -148,10 +149,13 @@ void spec_launch(SpecPool *sp, const H264Dec *d, const Sps *sps, const Pps *pps,
 int  spec_take(SpecPool *sp, H264Dec *d, const uint8_t *buf, uint32_t read_bytes, const SliceHdr *sh,
                const Pps *pps, const int *ref_slot);
 void spec_launch_ahead(SpecPool *sp, const H264Dec *d, const uint8_t *buf, uint32_t len);
+/* the calling thread runs the queued jobs no worker has started */
+void spec_help(SpecPool *sp);
 /* H264MI_SPEC_STATS: thread CPU per MB of worker and caller parses */
 int  spec_stats_on(const SpecPool *sp);
 double spec_thread_cpu(void);
 void spec_account_main(SpecPool *sp, double cpu, int mbs);
+void spec_account_caller(SpecPool *sp, double cpu);
 int  spec_active_for(const SpecPool *sp, const uint8_t *buf);
 const Sps *h264dec_active_sps(const H264Dec *d);
 

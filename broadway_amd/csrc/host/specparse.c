@@ -58,6 +58,7 @@ struct SpecPool {
     unsigned long    taken, declined;   /* statistics (H264MI_SPEC_STATS) */
     int              stats;
     double           w_cpu, c_cpu, m_cpu;   /* thread CPU: worker jobs, commits, the caller's own slices */
+    double           a_cpu;                 /* the caller's whole decode calls */
     unsigned long    w_mbs, m_mbs;
     /* snapshot of the picture the jobs belong to */
     Sps              sps;
@@ -146,7 +147,7 @@ static void *worker(void *arg)
 
 SpecPool *spec_create(int nthreads)
 {
-    if (nthreads < 1) return NULL;
+    if (nthreads < 0) return NULL;
     SpecPool *sp = (SpecPool *)calloc(1, sizeof(SpecPool));
     if (!sp) return NULL;
     sp->stats = getenv("H264MI_SPEC_STATS") != NULL;
@@ -156,8 +157,34 @@ SpecPool *spec_create(int nthreads)
     sp->th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
     for (int i = 0; sp->th && i < nthreads; i++)
         if (pthread_create(&sp->th[i], NULL, worker, sp) == 0) sp->nth++;
-    if (!sp->nth) { spec_destroy(sp); return NULL; }
+    if (!sp->nth && nthreads) { spec_destroy(sp); return NULL; }
     return sp;
+}
+
+/* the calling thread as a worker: run every queued job nobody has started */
+void spec_help(SpecPool *sp)
+{
+    if (!sp) return;
+    pthread_mutex_lock(&sp->mu);
+    for (;;) {
+        while (sp->next < sp->njobs && sp->jobs[sp->order[sp->next]].started) sp->next++;
+        if (sp->next >= sp->njobs) break;
+        SpecJob *j = &sp->jobs[sp->order[sp->next++]];
+        j->started = 1;
+        sp->running++;
+        pthread_mutex_unlock(&sp->mu);
+        const double t0 = sp->stats ? thread_cpu() : 0.0;
+        run_job(sp, j);
+        pthread_mutex_lock(&sp->mu);
+        if (sp->stats) {
+            sp->w_cpu += thread_cpu() - t0;
+            if (j->ok) sp->w_mbs += (unsigned long)j->pb.ndecoded;
+        }
+        j->done = 1;
+        sp->running--;
+        pthread_cond_broadcast(&sp->cv_done);
+    }
+    pthread_mutex_unlock(&sp->mu);
 }
 
 /* wait for the workers, then forget every job */
@@ -176,10 +203,12 @@ void spec_destroy(SpecPool *sp)
     if (!sp) return;
     if (sp->stats)
         fprintf(stderr, "h264mi: speculative slices taken %lu, parsed again %lu; thread CPU per MB: workers %.3f us "
-                "(%lu MBs), caller %.3f us (%lu MBs), commits %.3f us per taken MB\n", sp->taken, sp->declined,
+                "(%lu MBs), caller %.3f us (%lu MBs), commits %.3f us per taken MB; caller decode calls %.3f s "
+                "(own slices %.3f, commits %.3f, rest %.3f)\n", sp->taken, sp->declined,
                 1e6 * sp->w_cpu / (double)(sp->w_mbs ? sp->w_mbs : 1), sp->w_mbs,
                 1e6 * sp->m_cpu / (double)(sp->m_mbs ? sp->m_mbs : 1), sp->m_mbs,
-                1e6 * sp->c_cpu / (double)(sp->w_mbs ? sp->w_mbs : 1));
+                1e6 * sp->c_cpu / (double)(sp->w_mbs ? sp->w_mbs : 1), sp->a_cpu, sp->m_cpu, sp->c_cpu,
+                sp->a_cpu - sp->m_cpu - sp->c_cpu);
     pthread_mutex_lock(&sp->mu);
     sp->stop = 1;
     pthread_cond_broadcast(&sp->cv_work);
@@ -380,6 +409,10 @@ static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint
 /* statistics: the calling thread parsed a slice itself */
 int spec_stats_on(const SpecPool *sp) { return sp && sp->stats; }
 double spec_thread_cpu(void) { return thread_cpu(); }
+void spec_account_caller(SpecPool *sp, double cpu)
+{
+    if (sp) sp->a_cpu += cpu;
+}
 void spec_account_main(SpecPool *sp, double cpu, int mbs)
 {
     if (!sp) return;

@@ -24,11 +24,22 @@ REFDEC_SOFTAVC = os.path.join(HERE, "_ref", "refdec_softavc")
 _L = None
 
 
+def make(*targets: str) -> None:
+    """make in oracle/ under a file lock: concurrent test processes (pytest
+    -n) must not rebuild the same outputs at once.  Brings liboracle.so up to
+    date with the product host sources it is built from."""
+    import fcntl
+    os.makedirs(os.path.join(HERE, "_build"), exist_ok=True)
+    with open(os.path.join(HERE, "_build", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", HERE] + list(targets))
+
+
 def lib() -> C.CDLL:
     global _L
     if _L is None:
-        if not os.path.exists(LIB):
-            subprocess.check_call(["make", "-s", "-C", HERE])
+        if os.path.isdir(os.path.join(HERE, "..", "broadway_amd", "csrc")):
+            make()
         L = C.CDLL(LIB)
         L.oracle_decode_stream.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.POINTER(C.c_double)]
         L.oracle_decode_stream.restype = C.c_void_p

@@ -19,6 +19,7 @@ import tempfile
 
 import pytest
 
+import oracle
 from _golden import cases, stream
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -30,7 +31,7 @@ REPORT = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitizer
 
 @pytest.fixture(scope="module")
 def sanitized():
-    subprocess.check_call(["make", "-s", "sanitize"], cwd=os.path.join(ROOT, "oracle"))
+    oracle.make("sanitize")
     return {k: os.path.join(BUILD, f"oracle_dec_{k}") for k in ("tsan", "asan")}
 
 
@@ -142,12 +143,17 @@ NULL_MODES = {
     "private_nopool": ([], {"H264MI_ENGINE_POOL": "0"}),
     # device concealment off: the host path reads pictures back
     "share4_hostconceal": (["-S4"], {"H264MI_HOST_CONCEAL": "1"}),
+    # no slice workers: the calling threads parse the next picture ahead
+    # while they would wait for the device (H264MI_PARSE_HELP, the default),
+    # and with that off too (sequential)
+    "private_help_only": ([], {"H264MI_PARSE_THREADS": "0"}),
+    "private_sequential": ([], {"H264MI_PARSE_THREADS": "0", "H264MI_PARSE_HELP": "0"}),
 }
 
 
 @pytest.fixture(scope="module")
 def nulldev():
-    subprocess.check_call(["make", "-s", "nulldev"], cwd=os.path.join(ROOT, "oracle"))
+    oracle.make("nulldev")
     return {k: os.path.join(BUILD, f"h264mi_dec_null_{k}") for k in ("tsan", "asan")}
 
 
@@ -171,7 +177,8 @@ def test_hip_backend_threads_clean(nulldev, kind, mode):
         out = os.path.join(td, "s0.yuv")
         env = dict(os.environ, H264MI_PARSE_THREADS="2", H264MI_BLOCKING_SYNC="1",
                    TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0",
-                   ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1", **extra)
+                   ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="print_stacktrace=1")
+        env.update(extra)
         p = subprocess.run([nulldev[kind], f"-O{out}", "-r2"] + flags + paths, capture_output=True, text=True,
                            timeout=600, env=env)
         _check_clean(p, f"{kind}/{mode}")

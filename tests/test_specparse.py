@@ -1,6 +1,8 @@
 """Speculative slice parsing (csrc/host/specparse.c) changes nothing: the
-product parser with H264MI_PARSE_THREADS=0 (sequential) and =3 (worker
-threads parsing later slices and the next picture ahead) gives identical
+product parser with H264MI_PARSE_THREADS=0 H264MI_PARSE_HELP=0 (sequential),
+=3 (worker threads parsing later slices and the next picture ahead) and =0
+with the calling thread parsing the next picture's slices while it would wait
+for the device (H264MI_PARSE_HELP=1, no workers) gives identical
 frames on multi-slice streams, on streams whose look-ahead is wrong (frame_num
 gaps, dropped pictures, MMCO, new parameter sets between pictures), and the
 statistics show both taken and declined speculative results.  Runs the oracle
@@ -29,13 +31,14 @@ def _new_param_sets():
     return a + b
 
 
-def _decode(data, threads):
+def _decode(data, threads, helps=0):
     with tempfile.NamedTemporaryFile(suffix=".h264", delete=False) as f:
         f.write(data)
         src = f.name
     out = src + ".yuv"
     try:
-        env = dict(os.environ, H264MI_PARSE_THREADS=str(threads), H264MI_SPEC_STATS="1")
+        env = dict(os.environ, H264MI_PARSE_THREADS=str(threads), H264MI_PARSE_HELP=str(helps),
+                   H264MI_SPEC_STATS="1")
         p = subprocess.run([ODEC, f"-O{out}", src], capture_output=True, text=True, timeout=300, env=env)
         assert p.returncode in (0, 1), p.stderr[-2000:]
         with open(out, "rb") as f:
@@ -44,7 +47,7 @@ def _decode(data, threads):
         for ln in p.stderr.splitlines():
             if "speculative slices taken" in ln:
                 w = ln.split()
-                taken, declined = int(w[4].rstrip(",")), int(w[7])
+                taken, declined = int(w[4].rstrip(",")), int(w[7].rstrip(",;"))
         return frames, taken, declined
     finally:
         os.unlink(src)
@@ -63,7 +66,9 @@ def test_parse_threads_do_not_change_output():
         seq, _, _ = _decode(data, 0)
         spec, taken, declined = _decode(data, 3)
         assert len(seq) > 0 and spec == seq, name
-        total_taken += taken
-        total_declined += declined
+        helped, h_taken, h_declined = _decode(data, 0, 1)
+        assert helped == seq, name
+        total_taken += taken + h_taken
+        total_declined += declined + h_declined
     # both paths of spec_take ran: results committed, and results parsed again
     assert total_taken > 0 and total_declined > 0, (total_taken, total_declined)

@@ -58,28 +58,32 @@ def main():
         print(f"configs[3] 1080p streams, {a.frames} pictures, {a.reps} passes; ms of host CPU per picture "
               f"(all threads, user + sys)")
         for th in ("0", "2", "3"):
-            env = dict(os.environ, H264MI_PARSE_THREADS=th)
+            env = dict(os.environ, H264MI_PARSE_THREADS=th, H264MI_PARSE_HELP="0")
             out, w, c = run([pn, paths[0], str(a.reps)], env)
             n = a.frames * a.reps
             print(f"parse_null  workers {th}: cpu {1e3 * c / n:6.3f}  wall {1e3 * w / n:6.3f}   | {out.strip()}")
-        for th in ("0", "2"):
-            env = dict(os.environ, H264MI_PARSE_THREADS=th, H264MI_BLOCKING_SYNC="1")
+        combos = [("0", "0"), ("0", "1"), ("1", "1"), ("2", "0"), ("2", "1")]   # (workers, caller parses ahead)
+        for th, hp in combos:
+            env = dict(os.environ, H264MI_PARSE_THREADS=th, H264MI_PARSE_HELP=hp, H264MI_BLOCKING_SYNC="1")
             out, w, _ = run([exe, "-Onone", f"-r{a.reps}", "-T", paths[0]], env)
             d = fields(out)
             n = d["pictures"]
-            print(f"h264mi_dec 1 process, workers {th}: cpu {1e3 * d['cpu_seconds'] / n:6.3f} "
+            print(f"h264mi_dec 1 process, workers {th} help {hp}: cpu {1e3 * d['cpu_seconds'] / n:6.3f} "
+                  f"(decode thread {1e3 * d.get('cpu_decode_threads_seconds', 0) / n:6.3f}) "
                   f"(sys {1e3 * d['cpu_sys_seconds'] / n:5.3f})  fps {n / d['decode_seconds']:8.1f}  per picture in the calling "
                   f"thread: parse {1e3 * d['t_parse'] / n:5.3f} submit {1e3 * d['t_submit'] / n:5.3f} "
                   f"wait {1e3 * d['t_wait'] / n:5.3f} copy {1e3 * d['t_copy'] / n:5.3f}")
-        for th in ("0", "2"):
-            env = dict(os.environ, H264MI_PARSE_THREADS=th, H264MI_BLOCKING_SYNC="1")
+        for th, hp in combos:
+            env = dict(os.environ, H264MI_PARSE_THREADS=th, H264MI_PARSE_HELP=hp, H264MI_BLOCKING_SYNC="1")
             procs = [subprocess.Popen([exe, "-Onone", f"-r{a.reps}", "-T", p], stdout=subprocess.PIPE, text=True,
                                       env=env) for p in paths]
             outs = [fields(pr.communicate()[0]) for pr in procs]
             n = sum(d["pictures"] for d in outs)
             cpu = sum(d["cpu_seconds"] for d in outs)
             t = max(d["decode_seconds"] for d in outs)
-            print(f"h264mi_dec 8 processes, workers {th}: cpu {1e3 * cpu / n:6.3f}  fps {n / t:8.1f}  "
+            dthr = sum(d.get("cpu_decode_threads_seconds", 0) for d in outs)
+            print(f"h264mi_dec 8 processes, workers {th} help {hp}: cpu {1e3 * cpu / n:6.3f} (decode threads {1e3 * dthr / n:6.3f})"
+                  f"  fps {n / t:8.1f}  "
                   f"parse {1e3 * sum(d['t_parse'] for d in outs) / n:5.3f} "
                   f"wait {1e3 * sum(d['t_wait'] for d in outs) / n:5.3f} "
                   f"copy {1e3 * sum(d['t_copy'] for d in outs) / n:5.3f}")

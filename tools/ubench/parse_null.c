@@ -22,7 +22,38 @@ static int n_configure(void *ctx, int w, int h, int nslots)
     c->frame = (uint8_t *)calloc(1, c->bytes);
     return c->frame ? 0 : -1;
 }
-static int n_decode(void *ctx, const PicBuild *pb, int slot) { return 0; }
+/* PN_COPY=1: the decode copies the picture's records and coefficient blocks
+ * into a staging buffer with memcpy (what the HIP backend does into pinned
+ * memory), PN_COPY=2: with non-temporal stores -- the host cost of the copy
+ * and of the caches it evicts */
+#include <immintrin.h>
+static uint8_t *g_stage;
+static size_t g_stage_cap;
+static void copy_nt(void *dst, const void *src, size_t n)
+{
+    uint8_t *d = (uint8_t *)dst;
+    const uint8_t *s = (const uint8_t *)src;
+    while (n && ((uintptr_t)d & 31)) { *d++ = *s++; n--; }
+    for (; n >= 128; n -= 128, d += 128, s += 128) {
+        const __m256i a = _mm256_loadu_si256((const __m256i *)s), b = _mm256_loadu_si256((const __m256i *)(s + 32));
+        const __m256i c = _mm256_loadu_si256((const __m256i *)(s + 64)), e = _mm256_loadu_si256((const __m256i *)(s + 96));
+        _mm256_stream_si256((__m256i *)d, a); _mm256_stream_si256((__m256i *)(d + 32), b);
+        _mm256_stream_si256((__m256i *)(d + 64), c); _mm256_stream_si256((__m256i *)(d + 96), e);
+    }
+    memcpy(d, s, n);
+    _mm_sfence();
+}
+static int n_decode(void *ctx, const PicBuild *pb, int slot)
+{
+    static int mode = -1;
+    if (mode < 0) mode = getenv("PN_COPY") ? atoi(getenv("PN_COPY")) : 0;
+    if (!mode) return 0;
+    const size_t rb = (size_t)pb->nmbs * sizeof(MbRec), cb = (size_t)pb->ncoef * 32;
+    if (rb + cb > g_stage_cap) { free(g_stage); g_stage_cap = 2 * (rb + cb); g_stage = (uint8_t *)aligned_alloc(64, g_stage_cap); }
+    if (mode == 1) { memcpy(g_stage, pb->rec, rb); memcpy(g_stage + rb, pb->coef, cb); }
+    else { copy_nt(g_stage, pb->rec, rb); copy_nt(g_stage + rb, pb->coef, cb); }
+    return 0;
+}
 static int n_read(void *ctx, int slot, uint8_t *dst) { return 0; }
 static int n_copy(void *ctx, int d, int s) { return 0; }
 static void n_destroy(void *ctx) { free(((NullCtx *)ctx)->frame); free(ctx); }
