@@ -542,7 +542,7 @@ def load_traffic():
 GOP = 60                   # configs[3]: 1 I + 59 P per GOP; the bench streams are one GOP long
 
 
-def gop_phases(S: int, gop: int = GOP, step: int = 1):
+def gop_phases(S: int, gop: int = GOP, step: int = 1, offset: int = None):
     """GOP phase of each stream: stream s is s*gop/S pictures into its GOP
     when the first warmup step starts, so the S streams' IDR pictures are
     spread evenly over the steps (independent streams that did not start
@@ -550,9 +550,15 @@ def gop_phases(S: int, gop: int = GOP, step: int = 1):
     of S*gop -- the configs[3] mix of 1 I per 60 in every step window, not
     only in the one step that happens to hold picture 0.  step = P (frame-
     pipelined launches of P pictures per stream): phases are multiples of
-    P, so with an even GOP no launch pairs a stream's last picture with the
-    IDR after it."""
-    return [((s * gop) // S) // step * step for s in range(S)]
+    P plus `offset`.  offset 1 with P = 2 (the default, BENCH_IDR_FIRST=1
+    for 0): every pair is (odd k, k + 1), so a stream's IDR is always the
+    second picture of its launch -- (picture gop-1, picture 0): two pictures
+    that do not depend on each other -- instead of the first one, whose
+    successor in the same launch would wait on the IDR's whole deblocking
+    chain."""
+    if offset is None:
+        offset = 0 if step == 1 or os.environ.get("BENCH_IDR_FIRST") == "1" else 1
+    return [((s * gop) // S) // step * step + offset for s in range(S)]
 
 
 def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None, P: int = 1):
@@ -577,13 +583,14 @@ def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None
     return pre + main, R
 
 
-def pairs_ok(recs, pics, S, nmbs, N, P):
+def pairs_ok(recs, pics, S, nmbs, N, P, first=0):
     """The engine's frame-pipelined batch contract for launches of P = 2
-    consecutive pictures k, k+1 (k even) of every stream: the second writes
-    neither the slot the first writes nor one the first reads."""
-    for k in range(0, N - 1, P):
+    consecutive pictures k, k+1 (k = first, first + 2, ..., cyclically: the
+    pair (N-1, 0) included) of every stream: the second writes neither the
+    slot the first writes nor one the first reads."""
+    for k in range(first, N, P):
         for s in range(S):
-            a, b = k * S + s, (k + 1) * S + s
+            a, b = k * S + s, ((k + 1) % N) * S + s
             if pics[a][2] == pics[b][2] or pics[b][2] in slots_read(recs, nmbs, a):
                 return False
     return True
@@ -682,11 +689,12 @@ class DeviceRun:
         else:
             # frame-pipelined GOP plan: P-aligned phases, an even GOP, P-aligned
             # warmup / steps and every (k, k+1) pair within the batch contract
+            par = phases[0] % pipe if pipe > 1 else 0
             ok = (pipe > 1 and N % pipe == 0 and warmup % pipe == 0 and steps % pipe == 0 and
-                  all(ph % pipe == 0 for ph in phases) and pairs_ok(recs_h, pics_h, S, nmbs, N, pipe))
+                  all(ph % pipe == par for ph in phases) and pairs_ok(recs_h, pics_h, S, nmbs, N, pipe, par))
             self.P = pipe if ok else 1
         self.nslots = nslots
-        self.pics_h = pics_h
+        self.pics_h, self.recs_h = pics_h, recs_h
         self.slot_of = pics_h[:, 2].reshape(N, S).copy()
         self.is_i = [[c.pictures[k].n_inter == 0 for c in caps] for k in range(N)]
         self.eng = _DryEngine(device=device) if dry else Engine(w, h, S, nslots, device=device)
@@ -703,19 +711,23 @@ class DeviceRun:
         S, P = self.S, self.P
         self.warmup, self.steps, self.phases = warmup, steps, phases
         if phases is not None and P > 1 and not (warmup % P == 0 and steps % P == 0 and
-                                                 all(ph % P == 0 for ph in phases)):
+                                                 all(ph % P == phases[0] % P for ph in phases)):
             raise ValueError(f"plan of {warmup}+{steps} steps, phases {phases}: not aligned to {P} steps per launch")
+        if phases is not None and P > 1 and not pairs_ok(self.recs_h, self.pics_h, S, self.nmbs, self.N, P,
+                                                         phases[0] % P):
+            raise ValueError(f"phases {phases}: a pair of consecutive pictures breaks the batch contract")
         self.launches, self.n_pre = launch_plan(self.N, S, warmup, steps, phases, self.sched, P)
         if self.sched:
             self.n_warm = self.n_pre + sum(1 for k0, _ in self.sched if k0 < warmup)
         else:
-            # GOP plan, P = 2: a launch that would hold an IDR runs as two one-
-            # step launches -- paired, the IDR's own P picture waits on the
-            # IDR's deblocking chain, the launch's longest (r71 A/B: 809 us
-            # against 434 + 325 us split)
+            # GOP plan, P = 2: a launch whose FIRST step holds an IDR runs as
+            # two one-step launches -- paired, the IDR's own next picture waits
+            # on the IDR's deblocking chain, the launch's longest (r72 A/B: 809
+            # us against 434 + 325 us split).  With the default odd phases an
+            # IDR is always a launch's second picture, and nothing splits.
             main, warm = [], 0
             for j, x in enumerate(self.launches[self.n_pre:]):
-                parts = [[st] for st in x] if len(x) > 1 and self.holds_idr(x) else [x]
+                parts = [[st] for st in x] if len(x) > 1 and self.holds_idr(x[:1]) else [x]
                 main += parts
                 warm += len(parts) if j * P < warmup else 0
             self.launches = self.launches[:self.n_pre] + main
@@ -973,7 +985,10 @@ def main(argv=None):
     streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= min(nframes, GOP) for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    phases = gop_phases(S, min(c.npics for c in caps), a.pipe) if staggered else None
+    # phases for two-step launches only when the window allows them (even
+    # warmup and steps; DeviceRun falls back to one step otherwise)
+    pstep = a.pipe if a.pipe > 1 and a.warmup % a.pipe == 0 and a.steps % a.pipe == 0 else 1
+    phases = gop_phases(S, min(c.npics for c in caps), pstep) if staggered else None
     run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run, phases=phases)
     placement = run.placement()
     assert all(d == local for _, d in placement), f"rank {rank}: buffers not on device {local}: {placement}"
@@ -1110,7 +1125,11 @@ def main(argv=None):
                          "limiter": "latency: the MB-row deblocking dependency chain (DESIGN.md §3), not HBM",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic.get("hbm_bytes_per_step") if traffic else None,
+                         # per timed launch, the unit of `achieved` (launches of 1 or 2 steps)
+                         "traffic": (traffic.get("hbm_bytes_per_timed_launch") or traffic.get("hbm_bytes_per_step"))
+                         if traffic else None,
+                         "traffic_per_step": (traffic.get("hbm_bytes_per_timed_step") or traffic.get("hbm_bytes_per_step"))
+                         if traffic else None,
                          "alg_bytes_per_launch": int(launch_bytes),
                          # reference reads at 128-B line granularity (compulsory for these
                          # windows; R_alg counts only the bytes used) and the PMC traffic by
@@ -1131,13 +1150,16 @@ def main(argv=None):
                                              "avg_us_per_step": split["p"][2]} if split else None,
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
                          "traffic_source": traffic.get("source") if traffic else None},
-            "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2), "pictures_per_launch": S * P,
+            "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2),
+                                   "pictures_per_launch": round(S * a.steps / max(launches_timed, 1), 2),
                                    "steps_per_launch": P,
+                                   "avg_steps_per_timed_launch": round(a.steps / max(launches_timed, 1), 3),
                                    "timed_launches": launches_timed,
                                    # this run's k_wgpp dispatch indices (0-based, in
                                    # rocprofv3 kernel-trace order): the timed window and
                                    # the launches the HIP events sampled
                                    "trace_window": [run.n_warm, len(run.launches)],
+                                   "trace_steps": [len(run.launches[i]) for i in range(run.n_warm, len(run.launches))],
                                    "trace_sampled": sampled if len(sampled) != launches_timed else "all",
                                    "bound": "latency (MB-row deblocking dependency chain); MC waves overlap it"}},
             "p_only": p_only,

@@ -72,6 +72,9 @@ __device__ __forceinline__ void cc_plane_fp(const int32_t (*S)[4], int A, int B,
 
 // frame: the slot (I420, w*16 x h*16); order[0..n): MB addresses in
 // concealment order; dec0: nmbs flags, 1 = decoded (dynamic LDS copy, grows)
+// dynamic LDS bound of k_conceal (one byte per MB): the CU's 160 KB less
+// the static sums and headroom
+#define CONCEAL_LDS_MAX (159 * 1024)
 __global__ __launch_bounds__(64) void k_conceal(uint8_t *frame, int w, int h, const int *order, int n,
                                                const uint8_t *dec0)
 {

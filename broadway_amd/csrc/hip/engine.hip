@@ -41,6 +41,7 @@ struct h264mi_engine {
     // k_prep (deblocking records + residuals) writes buffer half prep_parity;
     // a batch prepped by the previous launch's tail workgroups is `prepped`
     int prep_parity;
+    int conceal_fits;                         // k_conceal's per-MB flags fit its LDS
     const void *prepped_rec, *prepped_pics;
     int prepped_n;                            // pictures the tail prepped
     unsigned long long *d_rows_done;   // row workgroups finished, all launches (tail-prep trigger)
@@ -170,6 +171,12 @@ static void engine_config(h264mi_engine *e)
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev) != hipSuccess || ncu < 1) ncu = 256;
     e->ncu = ncu;
+    // k_conceal keeps one decoded flag per MB in dynamic LDS: up to the CU's
+    // 160 KB less its static part; larger pictures conceal on the host
+    // (engine_conceal_fits -> the backend's conceal_ok)
+    e->conceal_fits = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conceal),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, CONCEAL_LDS_MAX) == hipSuccess &&
+                      (size_t)e->nmbs <= CONCEAL_LDS_MAX;
 }
 
 extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
@@ -776,6 +783,7 @@ extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? e->fr
 static std::atomic<unsigned long long> g_conceal_launches{0};
 // diagnostics: k_conceal launches in this process (tests: the device path ran)
 extern "C" unsigned long long h264mi_conceal_launches(void) { return g_conceal_launches.load(); }
+int engine_conceal_fits(const h264mi_engine *e) { return e && e->conceal_fits; }
 
 extern "C" int h264mi_engine_conceal(h264mi_engine *e, int stream, int slot, const int *order, int n,
                                      const uint8_t *decoded)
@@ -784,6 +792,7 @@ extern "C" int h264mi_engine_conceal(h264mi_engine *e, int stream, int slot, con
         (n && (!order || !decoded)))
         return -1;
     if (!n) return 0;
+    if (!e->conceal_fits) return -2;          // picture too large for k_conceal's LDS
     for (int i = 0; i < n; i++) if (order[i] < 0 || order[i] >= e->nmbs) return -1;
     HIPCHECK(hipSetDevice(e->dev));
     const size_t bytes = (size_t)e->nmbs * (sizeof(int) + 1);

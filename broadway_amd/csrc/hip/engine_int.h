@@ -33,5 +33,8 @@ int engine_poolable(const h264mi_engine *e);
 /* a pooled engine handed to a new decoder instance: settings re-read from the
  * environment, nothing prepped, flags cleared, frames cleared (queued) */
 int engine_reuse(h264mi_engine *e);
+/* k_conceal's per-MB LDS flags fit this engine's picture size (else the
+ * host conceals: h264mi_engine_conceal returns -2) */
+int engine_conceal_fits(const h264mi_engine *e);
 
 #endif

@@ -197,7 +197,7 @@ int h264dec_conceal(H264Dec *d, int is_i)
     }
 
     /* neighbour-based: pass 1 reconstructs the decoded MBs unfiltered */
-    const int on_backend = d->be.conceal != NULL;
+    const int on_backend = d->be.conceal != NULL && (!d->be.conceal_ok || d->be.conceal_ok(d->be.ctx));
     uint8_t *saved = (uint8_t *)malloc((size_t)nmbs);
     uint8_t *img = on_backend ? NULL : (uint8_t *)malloc(d->frame_bytes);
     uint32_t grey = 0;

@@ -44,6 +44,8 @@ typedef struct H264Backend {
      * the MBs order[0..n) in that order; decoded = the w*h decoded flags.
      * NULL: the host conceals a copy of the picture (conceal.c) */
     int  (*conceal)(void *ctx, int slot, const int *order, int n, const uint8_t *decoded);
+    /* optional: whether conceal serves the configured picture size (NULL: it does) */
+    int  (*conceal_ok)(void *ctx);
     /* optional: wait for the reconstructions issued so far (timing split of
      * the output path into device wait and copy) */
     int  (*sync)(void *ctx);

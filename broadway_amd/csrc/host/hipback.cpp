@@ -536,6 +536,12 @@ static int hb_conceal(void *vctx, int slot, const int *order, int n, const uint8
     return h264mi_engine_conceal(c->e, c->lane, slot, order, n, decoded);
 }
 
+static int hb_conceal_ok(void *vctx)
+{
+    const HipBackendCtx *c = (const HipBackendCtx *)vctx;
+    return c->e && engine_conceal_fits(c->e);
+}
+
 static int hb_copy(void *vctx, int dst, int src)
 {
     HipBackendCtx *c = (HipBackendCtx *)vctx;
@@ -604,6 +610,7 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     be.copy = hb_copy;
     // H264MI_HOST_CONCEAL=1: conceal on the host (a copy of the picture, conceal.c)
     be.conceal = getenv("H264MI_HOST_CONCEAL") && atoi(getenv("H264MI_HOST_CONCEAL")) ? NULL : hb_conceal;
+    be.conceal_ok = hb_conceal_ok;
     be.sync = hb_sync;
     be.prefetch = hb_prefetch;
     be.destroy = hb_destroy;

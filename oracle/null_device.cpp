@@ -187,6 +187,7 @@ void engine_shape(const h264mi_engine *e, int *w_mbs, int *h_mbs, int *nstreams,
     *w_mbs = e->w; *h_mbs = e->h; *nstreams = e->nstreams; *nslots = e->nslots; *blocking = e->blocking;
 }
 int engine_poolable(const h264mi_engine *e) { return 1; }
+int engine_conceal_fits(const h264mi_engine *e) { return 1; }
 int engine_reuse(h264mi_engine *e)
 {
     for (int i = 0; i < e->nstreams; i++)

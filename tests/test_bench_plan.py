@@ -21,8 +21,11 @@ def _walk(launches, S):
 
 def test_gop_phases_whole_launches():
     assert bench.gop_phases(8, 60) == [0, 7, 15, 22, 30, 37, 45, 52]
-    assert bench.gop_phases(8, 60, 2) == [0, 6, 14, 22, 30, 36, 44, 52]
-    assert all(p % 2 == 0 for p in bench.gop_phases(5, 60, 2))
+    # two steps per launch: odd phases (a stream's IDR is the second picture
+    # of its launch), or even ones with offset 0
+    assert bench.gop_phases(8, 60, 2) == [1, 7, 15, 23, 31, 37, 45, 53]
+    assert bench.gop_phases(8, 60, 2, 0) == [0, 6, 14, 22, 30, 36, 44, 52]
+    assert all(p % 2 == 1 for p in bench.gop_phases(5, 60, 2))
 
 
 def test_launch_plan_pipe2_cyclic():
@@ -34,7 +37,7 @@ def test_launch_plan_pipe2_cyclic():
     for launch in launches[R:]:
         for s in range(S):
             a, b = launch[0][s], launch[1][s]
-            assert a % 2 == 0 and b == a + 1
+            assert a % 2 == 1 and b == (a + 1) % N          # odd phases: (k, k + 1), k odd; (59, 0) wraps
     seq = _walk(launches, S)
     for s in range(S):
         main = seq[s][R:]
@@ -51,10 +54,27 @@ def _caps(n=3, frames=12):
     return [Capture(s) for s in streams]
 
 
-def test_device_run_pipe2_gop_plan_descriptors():
+def test_device_run_pipe2_odd_phases_never_split():
+    """Odd phases: every IDR is the second picture of its launch, paired with
+    the stream's previous GOP's last picture (no dependency), so every main
+    launch has two steps."""
     caps = _caps()
     S, N = len(caps), 12
     ph = bench.gop_phases(S, N, 2)
+    run = bench.DeviceRun(None, caps, 2, 8, 2, dry=True, phases=ph)
+    assert run.P == 2
+    main = run.launches[run.n_pre:]
+    assert all(len(x) == 2 for x in main) and any(run.holds_idr(x) for x in main)
+    assert not any(run.holds_idr(x[:1]) for x in main)
+    seq = _walk(main, S)
+    assert all(seq[s] == [(v + ph[s]) % N for v in range(10)] for s in range(S))
+    run.free()
+
+
+def test_device_run_pipe2_gop_plan_descriptors():
+    caps = _caps()
+    S, N = len(caps), 12
+    ph = bench.gop_phases(S, N, 2, 0)
     run = bench.DeviceRun(None, caps, 2, 8, 2, dry=True, phases=ph)
     assert run.P == 2
     # launches holding an IDR run one step at a time, the others two
@@ -85,6 +105,6 @@ def test_device_run_pipe2_gop_plan_descriptors():
 
 def test_device_run_odd_plan_falls_back_to_one_step():
     caps = _caps()
-    run = bench.DeviceRun(None, caps, 3, 8, 2, dry=True, phases=bench.gop_phases(len(caps), 12, 2))
+    run = bench.DeviceRun(None, caps, 3, 8, 2, dry=True, phases=bench.gop_phases(len(caps), 12, 2, 0))
     assert run.P == 1 and all(len(x) == 1 for x in run.launches)
     run.free()

@@ -76,6 +76,27 @@ def trace_window(src):
                     "and the P-only leg's; this is the timed window alone"}
 
 
+def window_bytes(src, counter, sub):
+    """Counter values of the k_wgpp dispatches of the bench's timed window
+    (kernels.k_wgpp.trace_window of prof_bench.json, the same command as the
+    --pmc passes), in dispatch order, and the steps each of those launches
+    holds (trace_steps; one step each when the line predates it)."""
+    bj = os.path.join(src, "prof_bench.json")
+    cc = os.path.join(src, sub, "bench_counter_collection.csv")
+    if not (os.path.exists(bj) and os.path.exists(cc)):
+        return None
+    k = json.loads(open(bj).read().strip().splitlines()[-1])["kernels"]["k_wgpp"]
+    if "trace_window" not in k:
+        return None
+    rows = [r for r in csv.DictReader(open(cc)) if kname(r["Kernel_Name"]) == "k_wgpp" and r["Counter_Name"] == counter]
+    if rows and "Dispatch_Id" in rows[0]:
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    a, b = k["trace_window"]
+    vals = [float(r["Counter_Value"]) for r in rows][a:b]
+    steps = k.get("trace_steps") or [1] * len(vals)
+    return vals, steps[:len(vals)]
+
+
 def _counters(path):
     """{kernel: {counter: (mean per launch, launches)}} of one counter-collection CSV"""
     d = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -186,6 +207,20 @@ def main(tag):
     if tw:
         out["trace_window"] = tw
         json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+    # the bench's timed launches alone (a launch holds 1 or 2 steps): bytes
+    # per timed launch -- roofline.traffic, the unit of roofline.achieved --
+    # and per step
+    fw, ww = window_bytes(src, "FETCH_SIZE", "pmc_fetch"), window_bytes(src, "WRITE_SIZE", "pmc_write")
+    if fw and ww and fw[0] and len(fw[0]) == len(ww[0]):
+        tot = sum((2 * f + w) * 1024 for f, w in zip(fw[0], ww[0]))
+        win = {"launches": len(fw[0]), "steps": sum(fw[1]),
+               "hbm_bytes_per_timed_launch": int(tot / len(fw[0])),
+               "hbm_bytes_per_timed_step": int(tot / max(sum(fw[1]), 1))}
+        out["timed_window"] = win
+        json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+        t = json.load(open(os.path.join(dst, "traffic.json")))
+        t.update(win)
+        json.dump(t, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     cal = calibration(src)
     if cal:
         json.dump(cal, open(os.path.join(dst, f"{tag}_fetch_calib.json"), "w"), indent=1)
