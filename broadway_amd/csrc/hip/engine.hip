@@ -302,11 +302,16 @@ static int rows_per_wg(const h264mi_engine *e, int S)
 // urgency priority (recon_kernels.hip mc_row) P pictures gain (measured,
 // configs[3] P-only: 350 vs 355 us per launch; a launch with an I picture:
 // ~40 us slower).  So: 2 unless the launch holds an intra-heavy picture
-// (more than half its MBs intra) or its content is unknown.
-static int launch_nmc(const h264mi_engine *e, int rpw)
+// (more than half its MBs intra) or its content is unknown.  A launch of
+// two steps per stream always takes 2: twice the rows compete for workgroup
+// slots, and 768 of them beat the third wave even with an IDR among the
+// pictures (configs[3] GOP mix: launches holding an IDR 671 vs 754 us,
+// profiles/r75_ab_idr_second.txt).
+static int launch_nmc(const h264mi_engine *e, int rpw, int P)
 {
     if (e->mc_waves) return e->mc_waves;
     if (rpw > 1) return 3;
+    if (P > 1) return 2;
     return e->launch_intra == 0 ? 2 : 3;
 }
 
@@ -385,7 +390,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     e->last_kernel = "k_wgpp";
     const int rpw = rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
-    const int nmc = launch_nmc(e, rpw);
+    const int nmc = launch_nmc(e, rpw, P);
     e->launch_intra = -1;                     // a hint covers one launch
     const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w) : WgppLds<2, 1>::bytes(e->w))
                         : rpw == 3 ? WgppLds<3, 3>::bytes(e->w) : rpw == 2 ? WgppLds<3, 2>::bytes(e->w)
