@@ -192,8 +192,8 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
     k_prep in each launch's tail) and its verification pass.  staggered: GOP
     phases staggered over the streams, each 60-picture stream decoded
     cyclically after an untimed pre-roll -- with pipe 2 (the bench default)
-    two consecutive pictures of every stream per launch, one per launch where
-    a launch would hold an IDR; aligned: decode order from picture 0, every
+    two consecutive pictures of every stream per launch, the phases odd so
+    that an IDR is always the second picture of its launch; aligned: decode order from picture 0, every
     launch two steps (frame-pipelined batches).  Every picture of every
     launch vs the reference MD5s, and after the run every frame slot's last
     picture."""
@@ -208,9 +208,12 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
         if staggered:
             steps = sum(len(x) for x in run.launches[run.n_pre:])
             assert run.n_pre == max(phases) and steps == n
-            assert all(not run.holds_idr(x) for x in run.launches[run.n_pre:] if len(x) > 1)
+            # no two-step launch starts with an IDR (odd phases: IDRs are second)
+            assert all(not run.holds_idr(x[:1]) for x in run.launches[run.n_pre:] if len(x) > 1)
             timed = run.timed_pictures()
-            assert sum(run.is_i[k][s] for s, k in timed) == 8 - 1     # stream 0's IDR falls in the warmup
+            # stream s's IDR is at step (n - phase) % n: those in the timed window
+            want = sum(1 for ph in phases if 4 <= (n - ph) % n)
+            assert sum(run.is_i[k][s] for s, k in timed) == want
         else:
             assert len(run.launches) == n // pipe
         refs = [bench.golden_frames(3, sd, {}) for sd in seeds]
