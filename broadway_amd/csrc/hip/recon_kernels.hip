@@ -1139,6 +1139,7 @@ struct __attribute__((aligned(16))) MbRing {
     // chroma is -- the next MB's intra reads its left neighbours as they land
     int lprog[RK], cprog[RK];
     int consumed;
+    int claim;          // the next MB an MC wave takes (MC_DYN; NMC .. w)
 };
 
 __device__ __forceinline__ int lds_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -1998,9 +1999,22 @@ __device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *pe
     if (__builtin_amdgcn_ballot_w64(need > known) != 0 && lane == 0) atomicOr((unsigned *)perr, CHK_REFROW);
 }
 
-// MC waves of one row (picture p, MB row r): walk the row's MBs c0, c0 + NMC,
-// ... into the row's LDS ring.  UPL / MEL as row_pp: where the row above's
-// unfiltered bottom rows come from (intra) / where this row's go.
+// MC waves of one row (picture p, MB row r): MB c0 first (c0 = the wave's
+// index), then -- in P pictures -- the MBs the waves claim from the row's
+// counter R.claim, in order, into the row's LDS ring: a wave held up by an
+// intra MB (which waits for its left neighbour, then predicts 16 blocks in
+// sequence) no longer holds up the MBs that would statically be the other
+// waves' turn behind it.  A wave claims its next MB when it starts the
+// current one, so its record load is in flight meanwhile.  Intra-heavy
+// pictures (PicDesc PD_INTRA_HEAVY) keep the static c0, c0 + NMC, ... walk:
+// their MBs wait on each other in order anyway, and the claims measured
+// slower there (profiles/r77_ab_mc_claim.txt).  Every wait (ring slot, intra
+// neighbours, reference rows) is on a lower-numbered MB, which some wave
+// already holds.  UPL / MEL as row_pp: where the row above's unfiltered
+// bottom rows come from (intra) / where this row's go.
+#ifndef MC_DYN
+#define MC_DYN 1
+#endif
 template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK>
 __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing<RK> &R,
                                        const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me)
@@ -2020,19 +2034,43 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             D.n++;
         }
     }
-    // MB c0's record (lane i < 24: dword i) and loads; then one MB ahead
-    uint32_t v0 = c0 < a.w ? recrow[(size_t)c0 * 24 + (lane < 24 ? lane : 0)] : 0;
+    // the next MB of this wave: the row counter's (dynamic) or c + NMC.  The
+    // claim is one lane's LDS atomic, exec = lane 0 inside the asm (no
+    // divergent branch in the IR feeding the index; an atomic from all 64
+    // lanes on one address serialises: +35 % per launch).  The static walk
+    // runs the same block with a zero increment: its wait and compiler
+    // barrier at the top of each MB measured 1.4 % faster than without
+    // (r77_ab_mc_claim.txt).
+    const bool dyn = MC_DYN && !(__builtin_amdgcn_readfirstlane(pd.flags) & PD_INTRA_HEAVY);
+    auto next_mb = [&](int c) -> int {
+        const unsigned addr = (unsigned)(size_t)(__attribute__((address_space(3))) int *)&R.claim;
+        const int inc = dyn ? 1 : 0;
+        int u, tmp;
+        unsigned long long saved;
+        asm volatile("s_mov_b64 %1, exec\n\t"
+                     "s_mov_b64 exec, 1\n\t"
+                     "ds_add_rtn_u32 %2, %3, %4\n\t"
+                     "s_waitcnt lgkmcnt(0)\n\t"
+                     "s_mov_b64 exec, %1\n\t"
+                     "v_readfirstlane_b32 %0, %2"
+                     : "=s"(u), "=&s"(saved), "=&v"(tmp) : "v"(addr), "v"(inc) : "memory");
+        return dyn ? u : c + NMC;
+    };
+    // MB c0's record (lane i < 24: dword i) and loads
+    int c = c0;
+    uint32_t v0 = c < a.w ? recrow[(size_t)c * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
-    if (c0 < a.w && D.n) dep_wait(a, p, v0, lane, D);
-    if (CHK && c0 < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c0, v0, lane, (int)D.slot[0], D.known[0]);
-    if (c0 < a.w) mc_issue(a, pd, p, r * a.w + c0, v0, lane, ld);
+    if (c < a.w && D.n) dep_wait(a, p, v0, lane, D);
+    if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, (int)D.slot[0], D.known[0]);
+    if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
 
     const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
     const int lead0 = a.mc_lead0 > 0 && a.mc_lead0 < lead ? a.mc_lead0 : lead;
-    for (int c = c0; c < a.w; c += NMC) {
+    while (c < a.w) {
         const int slot = c & (RK - 1);
-        const bool more = c + NMC < a.w;
-        const uint32_t nv0 = more ? recrow[(size_t)(c + NMC) * 24 + (lane < 24 ? lane : 0)] : 0;
+        // claim the next MB now and fetch its record
+        const int cn = next_mb(c);
+        const uint32_t nv0 = cn < a.w ? recrow[(size_t)cn * 24 + (lane < 24 ? lane : 0)] : 0;
         if (c >= lead0) {
             // slot free (ring depth) and at most lead MBs ahead; before the
             // row's chain has begun (consumed < 1: MB 1 not taken yet) at
@@ -2096,10 +2134,11 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             lds_st(&R.cprog[slot], (c << 4) | 1);
             lds_st(&R.flag[slot], c + 1);
         }
+        c = cn;
         v0 = nv0;
-        if (more && D.n) dep_wait(a, p, v0, lane, D);
-        if (CHK && more && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c + NMC, v0, lane, (int)D.slot[0], D.known[0]);
-        if (more) mc_issue(a, pd, p, r * a.w + c + NMC, v0, lane, ld);
+        if (c < a.w && D.n) dep_wait(a, p, v0, lane, D);
+        if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, (int)D.slot[0], D.known[0]);
+        if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
     }
 }
 
@@ -2158,7 +2197,7 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     const int j = jg / hg, g = jg - j * hg, p = j * S + s;
     for (int q = 0; q < RPW; q++) {
         if (threadIdx.x < RK) { R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1; }
-        if (threadIdx.x == 0) { R[q].consumed = 0; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
+        if (threadIdx.x == 0) { R[q].consumed = 0; R[q].claim = NMC; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
     for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
         L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);

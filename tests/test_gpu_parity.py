@@ -255,7 +255,7 @@ def test_engine_pipelined_steps_vs_oracle(wh):
 
 
 @pytest.mark.parametrize("share", [0, 4])
-def test_swdec_concurrent_instances_vs_reference(share):
+def test_swdec_concurrent_instances_vs_reference(share, monkeypatch):
     """One H264SwDec instance per thread, decoding concurrently (the
     reference's N-instance model, TestBenchMultipleInstance.c:134-305, on
     threads): four 1080p streams -- a damaged one among them, with its
@@ -264,8 +264,12 @@ def test_swdec_concurrent_instances_vs_reference(share):
     (h264mi_set_share; 1080p and 720p each get theirs, the small stream's
     engine is shared by nobody else).  Every output picture, picture id and
     error count equals the reference's, and the lock-step 1080p and 720p
-    instances put several pictures in one launch."""
+    instances put several pictures in one launch (the batching property is
+    timed with the calling threads not parsing ahead, H264MI_PARSE_HELP=0:
+    parsing ahead spreads the instances' submissions; the sanitizer tests run
+    shared engines with it on)."""
     import threading
+    monkeypatch.setenv("H264MI_PARSE_HELP", "0")
     L = _lib.mi()
     names = ["bench_1080p_s100", "bench_1080p_s101", "bench_1080p_s102", "err_1080p_mixed",
              "leg_cfg2_720p_s1", "leg_cfg2_720p_s2", "err_range_p_11x9"]
