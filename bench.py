@@ -579,7 +579,13 @@ def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None
         return [[[k] * S for k in range(k0, k0 + P)] for k0, P in sched], 0
     R = max(phases)
     pre = [[[max(0, u - R + ph) for ph in phases]] for u in range(R)]
-    main = [[[(v + j + ph) % N for ph in phases] for j in range(P)] for v in range(0, warmup + steps, P)]
+    # P-step launches aligned to the timed window's start: warmup % P single
+    # steps first, a shorter launch last when steps % P != 0
+    main, v = [], 0
+    while v < warmup + steps:
+        n = 1 if v < warmup % P else min(P, warmup + steps - v)
+        main.append([[(v + j + ph) % N for ph in phases] for j in range(n)])
+        v += n
     return pre + main, R
 
 
@@ -689,9 +695,12 @@ class DeviceRun:
         else:
             # frame-pipelined GOP plan: P-aligned phases, an even GOP, P-aligned
             # warmup / steps and every (k, k+1) pair within the batch contract
-            par = phases[0] % pipe if pipe > 1 else 0
-            ok = (pipe > 1 and N % pipe == 0 and warmup % pipe == 0 and steps % pipe == 0 and
-                  all(ph % pipe == par for ph in phases) and pairs_ok(recs_h, pics_h, S, nmbs, N, pipe, par))
+            # pairs (k, k + 1) start where the timed window does: k = warmup +
+            # phase (mod 2) -- one parity for every stream, N even so that the
+            # cyclic pair (N - 1, 0) keeps it
+            par = (warmup + phases[0]) % pipe if pipe > 1 else 0
+            ok = (pipe > 1 and N % pipe == 0 and all(ph % pipe == phases[0] % pipe for ph in phases) and
+                  pairs_ok(recs_h, pics_h, S, nmbs, N, pipe, par))
             self.P = pipe if ok else 1
         self.nslots = nslots
         self.pics_h, self.recs_h = pics_h, recs_h
@@ -710,11 +719,10 @@ class DeviceRun:
         launch's steps step-major, launches back to back)."""
         S, P = self.S, self.P
         self.warmup, self.steps, self.phases = warmup, steps, phases
-        if phases is not None and P > 1 and not (warmup % P == 0 and steps % P == 0 and
-                                                 all(ph % P == phases[0] % P for ph in phases)):
-            raise ValueError(f"plan of {warmup}+{steps} steps, phases {phases}: not aligned to {P} steps per launch")
+        if phases is not None and P > 1 and not all(ph % P == phases[0] % P for ph in phases):
+            raise ValueError(f"phases {phases}: not all of one parity")
         if phases is not None and P > 1 and not pairs_ok(self.recs_h, self.pics_h, S, self.nmbs, self.N, P,
-                                                         phases[0] % P):
+                                                         (warmup + phases[0]) % P):
             raise ValueError(f"phases {phases}: a pair of consecutive pictures breaks the batch contract")
         self.launches, self.n_pre = launch_plan(self.N, S, warmup, steps, phases, self.sched, P)
         if self.sched:
@@ -725,11 +733,12 @@ class DeviceRun:
             # on the IDR's deblocking chain, the launch's longest (r72 A/B: 809
             # us against 434 + 325 us split).  With the default odd phases an
             # IDR is always a launch's second picture, and nothing splits.
-            main, warm = [], 0
-            for j, x in enumerate(self.launches[self.n_pre:]):
+            main, warm, v = [], 0, 0
+            for x in self.launches[self.n_pre:]:
                 parts = [[st] for st in x] if len(x) > 1 and self.holds_idr(x[:1]) else [x]
                 main += parts
-                warm += len(parts) if j * P < warmup else 0
+                warm += len(parts) if v < warmup else 0
+                v += len(x)
             self.launches = self.launches[:self.n_pre] + main
             self.n_warm = self.n_pre + warm
         self.desc_off = np.cumsum([0] + [len(x) * S * 32 for x in self.launches]).tolist()
@@ -985,10 +994,12 @@ def main(argv=None):
     streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= min(nframes, GOP) for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    # phases for two-step launches only when the window allows them (even
-    # warmup and steps; DeviceRun falls back to one step otherwise)
-    pstep = a.pipe if a.pipe > 1 and a.warmup % a.pipe == 0 and a.steps % a.pipe == 0 else 1
-    phases = gop_phases(S, min(c.npics for c in caps), pstep) if staggered else None
+    # phases for two-step launches: pairs start at the timed window's first
+    # step, and an IDR is a pair's second picture: warmup + phase odd
+    # (BENCH_IDR_FIRST=1: even, such launches split)
+    pstep = a.pipe if a.pipe > 1 else 1
+    off = None if pstep == 1 else (a.warmup + (0 if os.environ.get("BENCH_IDR_FIRST") == "1" else 1)) % 2
+    phases = gop_phases(S, min(c.npics for c in caps), pstep, off) if staggered else None
     run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run, phases=phases)
     placement = run.placement()
     assert all(d == local for _, d in placement), f"rank {rank}: buffers not on device {local}: {placement}"

@@ -103,8 +103,20 @@ def test_device_run_pipe2_gop_plan_descriptors():
     run.free()
 
 
-def test_device_run_odd_plan_falls_back_to_one_step():
+def test_device_run_odd_warmup_and_steps():
+    """The driver's window (odd warmup, any step count): warmup % 2 single
+    steps first, then pairs starting at the timed window's first step, a
+    single last when the steps are odd; phases of the parity that makes every
+    IDR a pair's second picture."""
     caps = _caps()
-    run = bench.DeviceRun(None, caps, 3, 8, 2, dry=True, phases=bench.gop_phases(len(caps), 12, 2, 0))
-    assert run.P == 1 and all(len(x) == 1 for x in run.launches)
+    S, N, W, K = len(caps), 12, 3, 7
+    ph = bench.gop_phases(S, N, 2, (W + 1) % 2)
+    run = bench.DeviceRun(None, caps, W, K, 2, dry=True, phases=ph)
+    assert run.P == 2
+    main = run.launches[run.n_pre:]
+    assert [len(x) for x in main] == [1, 2, 2, 2, 2, 1]
+    assert run.n_warm - run.n_pre == 2                      # the single + one pair: 3 warmup steps
+    assert not any(run.holds_idr(x[:1]) for x in main if len(x) == 2)
+    seq = _walk(main, S)
+    assert all(seq[s] == [(v + ph[s]) % N for v in range(W + K)] for s in range(S))
     run.free()
