@@ -1081,7 +1081,10 @@ def main(argv=None):
     if not a.no_e2e and not a.dry_run:
         if dist:
             dist.barrier()
-        e2e = end_to_end(streams, nframes, device=local, cpus=my_cpus if world > 1 else None)
+        # pinned at N = 1 too: the GPU's NUMA-local cores (tools/e2e_only.py
+        # E2E_PIN A/B, profiles/r80_e2e_pin.txt: 4.53-4.68 vs 4.97-5.70 ms of
+        # host CPU per picture, and steadier)
+        e2e = end_to_end(streams, nframes, device=local, cpus=my_cpus if my_cpus else None)
     if dist:
         plans, e2es = [None] * world, [None] * world
         dist.all_gather_object(plans, e2e_plan)
