@@ -356,6 +356,9 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     a.mc_lead = mc_lead;
     static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 0;
     a.row_prio_split = row_prio;
+    // study knob: the 2-MC-wave urgency distance (MBs, default 8)
+    static const int mc_urg = getenv("H264MI_MC_URGENCY") ? atoi(getenv("H264MI_MC_URGENCY")) : 8;
+    a.mc_urgency = mc_urg;
     a.chk_inject = e->check ? e->check_inject : 0;
 
     a.pics = d_pics;

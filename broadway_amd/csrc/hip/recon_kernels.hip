@@ -71,6 +71,7 @@ struct ReconArgs {
     // chain (slot waits, copy-in, frame stores) and 3 on it (hdone wait ..
     // publish); 0 = 3 throughout
     int row_prio_split;
+    int mc_urgency;          // MBs ahead of the row's deblocking under which MC waves issue at prio 2 (2-MC shape)
     // dependency-checker builds (k_wgpp<..., CHK = true>): test hook that
     // deliberately breaks one hand-off so the tests can see the checker fire
     // (0: none; 1: MB 5 of every row hands the row waves a wrong ring tag)
@@ -2094,7 +2095,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             // whose deblocking is far off -- the rows sharing a CU all start
             // their MC at once, and the top rows' MC gates their chains
             // (measured: P-only 350 vs 354 us per launch; 3 MC waves: slower)
-            if (c - __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < 8) __builtin_amdgcn_s_setprio(2);
+            if (c - __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < a.mc_urgency) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
         // PROF stamps [4] / [5] of inter MBs (intra MBs: mc_intra's): loads
