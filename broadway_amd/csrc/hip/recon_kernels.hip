@@ -1130,8 +1130,15 @@ template <bool LDSM> __device__ __forceinline__ void st_granT(unsigned long long
 #ifndef RINGG
 #define RINGG 16
 #endif
+// the 2-MC-wave single-row shape's ring (its LDS decides how many of its
+// workgroups share a CU, with WGPP2_WAVES_PER_EU); 32 slots, the 3-MC
+// shape keeps RING1
+#ifndef RING1_2MC
+#define RING1_2MC 32
+#endif
 template <int RK>
 struct __attribute__((aligned(16))) MbRing {
+    static_assert(RK > 0 && (RK & (RK - 1)) == 0, "ring depth must be a power of two: slot = c & (RK - 1)");
     uint8_t px[RK][384];
     uint8_t db[RK][64];
     int flag[RK];
@@ -2161,7 +2168,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
 // MB (396 vs 366 us per launch), so that variant stays a build option.
 template <int NMC, int RPW>
 struct WgppLds {
-    static constexpr int RK = RPW == 1 ? RING1 : RINGG;
+    static constexpr int RK = RPW == 1 ? (NMC == 2 ? RING1_2MC : RING1) : RINGG;
     static constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
     static constexpr size_t offM = a16(sizeof(PPLds) * RPW);
     static constexpr size_t offR = offM + a16(sizeof(McScratch) * RPW * NMC);
@@ -2171,10 +2178,19 @@ struct WgppLds {
 #ifndef WGPP_WAVES_PER_EU
 #define WGPP_WAVES_PER_EU 4
 #endif
+// the 2-MC-wave single-row shape's register budget: 4 waves per SIMD (128
+// VGPRs, no spill) -- with its 32-slot ring (RING1_2MC, ~28 KB of LDS) four
+// four-wave workgroups share a CU: 1,024 row slots, against 768 at 3 (162
+// VGPRs, 64 slots).  A two-step launch's 1,088 rows nearly all start at once:
+// 307 vs 321 us per step on the configs[3] GOP mix, launches holding an IDR
+// 614 vs 669 us (profiles/r82_ab_occupancy.txt); 5 per SIMD spills (448).
+#ifndef WGPP2_WAVES_PER_EU
+#define WGPP2_WAVES_PER_EU 4
+#endif
 
 template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false>
 __global__ __launch_bounds__(64 * (NMC + 2) * RPW)
-__attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : 3))) void k_wgpp(ReconArgs a)
+__attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : WGPP2_WAVES_PER_EU))) void k_wgpp(ReconArgs a)
 {
     using Lay = WgppLds<NMC, RPW>;
     constexpr int RK = Lay::RK;
