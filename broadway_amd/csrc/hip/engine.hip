@@ -354,7 +354,11 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     static const int mc_lead = getenv("H264MI_MC_LEAD") ? std::max(4, atoi(getenv("H264MI_MC_LEAD"))) : 0;
     a.mc_lead0 = mc_lead0;
     a.mc_lead = mc_lead;
-    static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 0;
+    // row waves at s_setprio 1 off the chain (slot waits, copy-in, frame
+    // stores) and 3 on it: on by default since the 4-workgroups-per-CU shape
+    // (profiles/r85_ab_row_prio.txt: 305.3 vs 307.3 us per step, 6 of 6
+    // rounds); H264MI_ROW_PRIO=0 turns it off
+    static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 1;
     a.row_prio_split = row_prio;
     // study knob: the 2-MC-wave urgency distance (MBs, default 8)
     static const int mc_urg = getenv("H264MI_MC_URGENCY") ? atoi(getenv("H264MI_MC_URGENCY")) : 8;
