@@ -80,11 +80,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-rgba", action="store_true", help="skip the RGBA output leg")
     ap.add_argument("--no-legs", action="store_true",
                     help="skip the SURVEY §8d config 2 (720p I-only) / config 5 (2160p) legs")
-    ap.add_argument("--pipe", type=int, default=int(os.environ.get("BENCH_PIPE", "2")),
-                    help="steps per launch (1 or 2; default 2, profiles/r72_ab_pipe2_gop.txt): with 2, a launch "
-                         "reconstructs two consecutive pictures of every stream and the second's rows start as the "
-                         "reference rows they read are final; a launch that would hold an IDR runs as two one-step "
-                         "launches")
+    ap.add_argument("--pipe", type=int, default=int(os.environ.get("BENCH_PIPE", "3")),
+                    help="steps per launch (1..4; default 3, profiles/r91_ab_pipe3.txt): with P > 1, a launch "
+                         "reconstructs P consecutive pictures of every stream and a later picture's rows start as "
+                         "the reference rows they read are final; the GOP phases put every IDR last in its launch")
     ap.add_argument("--aligned", action="store_true",
                     help="all streams' GOPs aligned, pictures W .. W+K-1 timed (no IDR in short windows); "
                          "default: GOP phases staggered over the streams")
@@ -211,58 +210,86 @@ def slots_read(recs, nmbs, i):
     return set(np.unique(r[inter, 24:28]).tolist())
 
 
-def rename_slots(recs, pics, S, nmbs, nslots):
-    """Physical frame slots for frame-pipelined launches: the host parser's
-    DPB slot d of a stream maps to one of nslots + 1 physical slots, and a
-    picture decoded into d gets the physical slot released longest ago --
-    never the one d held before (which the previous picture may still be
-    reading, e.g. the reference the sliding window just dropped).  The
-    mapping is a bijection at every picture, so the records' reference-slot
-    comparisons (bS) are unchanged; MbRec.ref and PicDesc cur_slot /
-    frame_base are rewritten in place.  Returns the physical slot count."""
-    nphys = nslots + 1
+def rename_slots(recs, pics, S, nmbs, nslots, P=2):
+    """Physical frame slots for frame-pipelined launches of P steps: the
+    host parser's DPB slot d of a stream maps to one of nphys >= nslots +
+    P - 1 physical slots, and a picture decoded into d gets the physical
+    slot released longest ago -- P - 1 pictures ago at the latest, so none
+    of the P - 1 pictures before it in its launch still reads it (e.g. the
+    reference the sliding window just dropped) or writes it.  The streams
+    are decoded cyclically (picture 0, an IDR, after the last), so the
+    launches across the wrap must qualify too: nphys grows from nslots +
+    P - 1 until they do (a sliding-window DPB assigns the slots round robin:
+    configs[3]'s 60-picture GOP with 5 DPB slots takes 6 for P = 2, 10 for P
+    = 3 and 4).  The mapping is a bijection at every picture, so the
+    records' reference-slot comparisons (bS) are unchanged; MbRec.ref and
+    PicDesc cur_slot / frame_base are rewritten in place.  Returns the
+    physical slot count."""
     n = len(pics) // S
     arr = np.frombuffer(recs, dtype=np.uint8).reshape(-1, MBREC)
-    for s in range(S):
-        cur = {}                              # DPB slot -> physical slot
-        free = list(range(nphys))             # released order, oldest first
+    refs = [[slots_read(recs, nmbs, k * S + s) for k in range(n)] for s in range(S)]
+
+    def assign(s, nphys):
+        cur, free = {}, list(range(nphys))    # DPB slot -> physical; released order, oldest first
+        luts, phs = [], []
         for k in range(n):
-            i = k * S + s
-            lut = np.arange(256, dtype=np.uint8)
-            for d, ph in cur.items():
-                lut[d] = ph
-            r = arr[i * nmbs:(i + 1) * nmbs]
-            inter = r[:, 0] <= 1
-            r[inter, 24:28] = lut[r[inter, 24:28]]
-            d = int(pics[i][2])
+            luts.append(dict(cur))
+            d = int(pics[k * S + s][2])
             old = cur.get(d)
             ph = next(x for x in free if x != old)
             free.remove(ph)
             if old is not None:
                 free.append(old)
             cur[d] = ph
+            phs.append(ph)
+        reads = [{luts[k].get(x, x) for x in refs[s][k]} for k in range(n)]
+        ok = all(phs[(k + i) % n] != phs[(k + m) % n] and phs[(k + i) % n] not in reads[(k + m) % n]
+                 for k in range(n) for i in range(1, P) for m in range(i))
+        return ok, luts, phs
+
+    for nphys in range(nslots + P - 1, nslots + P + 15):
+        plan = [assign(s, nphys) for s in range(S)]
+        if all(ok for ok, _, _ in plan):
+            break
+    for s, (_, luts, phs) in enumerate(plan):
+        for k in range(n):
+            i = k * S + s
+            lut = np.arange(256, dtype=np.uint8)
+            for d, ph in luts[k].items():
+                lut[d] = ph
+            r = arr[i * nmbs:(i + 1) * nmbs]
+            inter = r[:, 0] <= 1
+            r[inter, 24:28] = lut[r[inter, 24:28]]
             pics[i][1] = s * nphys
-            pics[i][2] = ph
+            pics[i][2] = phs[k]
     return nphys
 
 
 def schedule(recs, pics, S, nmbs, warmup, steps, P):
-    """Launches as (first step, steps in it).  P = 2 pairs steps (2i, 2i+1)
-    when, for every stream, the pair's pictures write different slots and
-    the first does not read the slot the second writes (the engine's
-    frame-pipelined batch contract); otherwise, or when warmup / steps are
-    odd, every launch is one step."""
+    """Launches as (first step, steps in it).  P > 1 groups steps (Pi ..
+    Pi+P-1) when every group meets the engine's frame-pipelined batch
+    contract (batch_ok); otherwise, or when warmup / steps are not multiples
+    of P, every launch is one step."""
     n = warmup + steps
     if P > 1 and warmup % P == 0 and steps % P == 0:
-        ok = True
-        for k0 in range(0, n, P):
-            for s in range(S):
-                a, b = k0 * S + s, (k0 + 1) * S + s
-                if pics[a][2] == pics[b][2] or pics[b][2] in slots_read(recs, nmbs, a):
-                    ok = False
-        if ok:
+        if all(batch_ok(recs, pics, S, nmbs, range(k0, k0 + P)) for k0 in range(0, n, P)):
             return [(k, P) for k in range(0, n, P)]
     return [(k, 1) for k in range(n)]
+
+
+def batch_ok(recs, pics, S, nmbs, ks):
+    """The engine's frame-pipelined batch contract for one launch of the
+    pictures ks (in step order) of every stream: no picture writes the slot
+    an earlier one of the launch writes or reads."""
+    ks = list(ks)
+    for s in range(S):
+        for i, kb in enumerate(ks[1:], 1):
+            b = kb * S + s
+            for ka in ks[:i]:
+                a = ka * S + s
+                if pics[a][2] == pics[b][2] or pics[b][2] in slots_read(recs, nmbs, a):
+                    return False
+    return True
 
 
 def golden_frames(config, seed, overrides):
@@ -542,7 +569,7 @@ def load_traffic():
 GOP = 60                   # configs[3]: 1 I + 59 P per GOP; the bench streams are one GOP long
 
 
-def gop_phases(S: int, gop: int = GOP, step: int = 1, offset: int = None):
+def gop_phases(S: int, gop: int = GOP, step: int = 1, offset: int = None, warmup: int = 0):
     """GOP phase of each stream: stream s is s*gop/S pictures into its GOP
     when the first warmup step starts, so the S streams' IDR pictures are
     spread evenly over the steps (independent streams that did not start
@@ -550,14 +577,15 @@ def gop_phases(S: int, gop: int = GOP, step: int = 1, offset: int = None):
     of S*gop -- the configs[3] mix of 1 I per 60 in every step window, not
     only in the one step that happens to hold picture 0.  step = P (frame-
     pipelined launches of P pictures per stream): phases are multiples of
-    P plus `offset`.  offset 1 with P = 2 (the default, BENCH_IDR_FIRST=1
-    for 0): every pair is (odd k, k + 1), so a stream's IDR is always the
-    second picture of its launch -- (picture gop-1, picture 0): two pictures
-    that do not depend on each other -- instead of the first one, whose
-    successor in the same launch would wait on the IDR's whole deblocking
-    chain."""
+    P plus `offset`.  The default, (1 - warmup) mod P (BENCH_IDR_FIRST=1:
+    -warmup mod P), puts a stream's IDR last in its launch (launches start
+    at warmup mod P): with P = 2 and an even warmup every pair is (odd k,
+    k + 1) -- (picture gop-1, picture 0): pictures that do not depend on
+    each other -- instead of the IDR first, whose successors in the same
+    launch would wait on its whole deblocking chain."""
     if offset is None:
-        offset = 0 if step == 1 or os.environ.get("BENCH_IDR_FIRST") == "1" else 1
+        first = os.environ.get("BENCH_IDR_FIRST") == "1"
+        offset = 0 if step == 1 else ((0 if first else 1) - warmup) % step
     return [((s * gop) // S) // step * step + offset for s in range(S)]
 
 
@@ -590,16 +618,10 @@ def launch_plan(N: int, S: int, warmup: int, steps: int, phases=None, sched=None
 
 
 def pairs_ok(recs, pics, S, nmbs, N, P, first=0):
-    """The engine's frame-pipelined batch contract for launches of P = 2
-    consecutive pictures k, k+1 (k = first, first + 2, ..., cyclically: the
-    pair (N-1, 0) included) of every stream: the second writes neither the
-    slot the first writes nor one the first reads."""
-    for k in range(first, N, P):
-        for s in range(S):
-            a, b = k * S + s, ((k + 1) % N) * S + s
-            if pics[a][2] == pics[b][2] or pics[b][2] in slots_read(recs, nmbs, a):
-                return False
-    return True
+    """The engine's frame-pipelined batch contract (batch_ok) for launches
+    of P consecutive pictures k .. k+P-1 (k = first, first + P, ...,
+    cyclically: with P = 2 the pair (N-1, 0) included) of every stream."""
+    return all(batch_ok(recs, pics, S, nmbs, [(k + i) % N for i in range(P)]) for k in range(first, N, P))
 
 
 class _DryEngine:
@@ -671,7 +693,7 @@ class DeviceRun:
     streams on its own GPU (`device`), every picture's records, coefficient
     blocks and descriptors in that GPU's HBM (engine-scoped allocations,
     placement asserted per buffer), and a launch plan (launch_plan: GOP
-    phases, or P steps per launch with physical slots renamed for P = 2; the
+    phases, or P steps per launch with physical slots renamed for P > 1; the
     next launch's k_prep runs in each launch's tail).  dry: no device calls."""
 
     def __init__(self, L, caps, warmup, steps, pipe=1, device=0, dry=False, phases=None):
@@ -686,7 +708,7 @@ class DeviceRun:
         recs_h, _, pics_h, _, nslots = packed
         self.sched = None
         if pipe > 1:
-            nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots)
+            nslots = rename_slots(recs_h, pics_h, S, nmbs, nslots, pipe)
         if phases is None:
             if warmup + steps > N:
                 raise ValueError(f"{warmup}+{steps} steps but the streams hold {N} pictures")
@@ -728,14 +750,22 @@ class DeviceRun:
         if self.sched:
             self.n_warm = self.n_pre + sum(1 for k0, _ in self.sched if k0 < warmup)
         else:
-            # GOP plan, P = 2: a launch whose FIRST step holds an IDR runs as
-            # two one-step launches -- paired, the IDR's own next picture waits
-            # on the IDR's deblocking chain, the launch's longest (r72 A/B: 809
-            # us against 434 + 325 us split).  With the default odd phases an
-            # IDR is always a launch's second picture, and nothing splits.
+            # GOP plan, P > 1: a launch splits after every step holding an
+            # IDR that is not its last -- in the same launch, the IDR's own
+            # next picture waits on the IDR's deblocking chain, the launch's
+            # longest (r72 A/B, P = 2: 809 us against 434 + 325 us split).
+            # With the default phases an IDR is always a launch's last
+            # picture, and nothing splits.
             main, warm, v = [], 0, 0
             for x in self.launches[self.n_pre:]:
-                parts = [[st] for st in x] if len(x) > 1 and self.holds_idr(x[:1]) else [x]
+                parts, cur = [], []
+                for st in x:
+                    cur.append(st)
+                    if self.holds_idr([st]):
+                        parts.append(cur)
+                        cur = []
+                if cur:
+                    parts.append(cur)
                 main += parts
                 warm += len(parts) if v < warmup else 0
                 v += len(x)
@@ -994,12 +1024,11 @@ def main(argv=None):
     streams, caps = prepare(a.config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= min(nframes, GOP) for c in caps), "stream preparation failed"
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    # phases for two-step launches: pairs start at the timed window's first
-    # step, and an IDR is a pair's second picture: warmup + phase odd
-    # (BENCH_IDR_FIRST=1: even, such launches split)
+    # phases for P-step launches: launches start at the timed window's first
+    # step, and an IDR is its launch's last picture (BENCH_IDR_FIRST=1: the
+    # first, such launches split)
     pstep = a.pipe if a.pipe > 1 else 1
-    off = None if pstep == 1 else (a.warmup + (0 if os.environ.get("BENCH_IDR_FIRST") == "1" else 1)) % 2
-    phases = gop_phases(S, min(c.npics for c in caps), pstep, off) if staggered else None
+    phases = gop_phases(S, min(c.npics for c in caps), pstep, warmup=a.warmup) if staggered else None
     run = DeviceRun(L, caps, a.warmup, a.steps, a.pipe, device=local, dry=a.dry_run, phases=phases)
     placement = run.placement()
     assert all(d == local for _, d in placement), f"rank {rank}: buffers not on device {local}: {placement}"
@@ -1139,7 +1168,7 @@ def main(argv=None):
                          "limiter": "latency: the MB-row deblocking dependency chain (DESIGN.md §3), not HBM",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         # per timed launch, the unit of `achieved` (launches of 1 or 2 steps)
+                         # per timed launch, the unit of `achieved` (launches of 1 .. P steps)
                          "traffic": (traffic.get("hbm_bytes_per_timed_launch") or traffic.get("hbm_bytes_per_step"))
                          if traffic else None,
                          "traffic_per_step": (traffic.get("hbm_bytes_per_timed_step") or traffic.get("hbm_bytes_per_step"))

@@ -164,6 +164,10 @@ static void engine_config(h264mi_engine *e)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 3, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, false, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, true, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
     e->rpw_max = e->mc_waves == 2 ? 2 : 3;
     while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * e->w * 256 + (size_t)e->rpw_max * row_lds > 156 * 1024)
@@ -395,14 +399,25 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     }
     const bool rec = e->timing || rec_tev;
     e->last_kernel = "k_wgpp";
-    const int rpw = rows_per_wg(e, S);
+    // three or more steps: the DEP3 instances (single-row, 2 MC waves)
+    const bool dep3 = P > 2;
+    const int rpw = dep3 ? 1 : rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
-    const int nmc = launch_nmc(e, rpw, P);
+    const int nmc = dep3 ? 2 : launch_nmc(e, rpw, P);
     e->launch_intra = -1;                     // a hint covers one launch
     const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w) : WgppLds<2, 1>::bytes(e->w))
                         : rpw == 3 ? WgppLds<3, 3>::bytes(e->w) : rpw == 2 ? WgppLds<3, 2>::bytes(e->w)
                         : WgppLds<3, 1>::bytes(e->w);
-    if (a.prof) {
+    if (dep3) {
+        // (no profiling build: a profiled engine runs them unstamped)
+        e->last_kernel = e->check ? "k_wgpp_check" : "k_wgpp";
+        if (e->check)
+            hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1, true, true>), grid, dim3(256), lmbx, e->st, rec ? t0 : nullptr,
+                                  rec ? t2 : nullptr, 0, a);
+        else
+            hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1, false, true>), grid, dim3(256), lmbx, e->st, rec ? t0 : nullptr,
+                                  rec ? t2 : nullptr, 0, a);
+    } else if (a.prof) {
         if (rec) (void)hipEventRecord(t0, e->st);
         if (rpw == 3) hipLaunchKernelGGL((k_wgpp<3, true, true, 3>), grid, dim3(960), lmbx, e->st, a);
         else if (rpw == 2) hipLaunchKernelGGL((k_wgpp<3, true, true, 2>), grid, dim3(640), lmbx, e->st, a);
@@ -580,7 +595,9 @@ extern "C" int h264mi_kernel_occupancy(int *blocks_per_cu, int *lds_bytes, int *
 
 extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)
 {
-    if (!e || steps < 1 || steps > 2) return -1;
+    // (frame-pipelined launches name the earlier steps' target slots in a
+    // 32-bit mask: recon_kernels.hip dep_wait)
+    if (!e || steps < 1 || steps > H264MI_MAX_STEPS || (steps > 1 && e->nslots > 32)) return -1;
     if (steps == e->steps) return 0;
     if (h264mi_engine_sync(e)) return -1;
     free_pic_buffers(e);

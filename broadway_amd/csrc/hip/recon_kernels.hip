@@ -1860,18 +1860,22 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
 // is only read once all of its bytes are final, so no CU's L1 and no XCD's
 // L2 ever holds a stale copy of it (the producer's release writes its L2
 // back; lines from earlier launches were dropped at kernel start), and the
-// loads themselves stay plain.  known[k]: leading row workgroups of the
-// step j - k picture seen done by this wave.
-// in-launch producers a picture can wait on: one (steps per launch <= 2);
-// with more, the MC waves' state spills past their 128 VGPRs
-#define DEP_MAX 1
+// loads themselves stay plain.
+//
+// Three or more steps: the done tags are chained -- row r of step j >= 1 tags
+// itself done only once row r of step j - 1 is (k_wgpp), so the step j - 1
+// picture's leading rows seen done imply the same rows of every earlier step
+// done, and one counter covers every in-launch producer: a partition whose
+// reference slot is any earlier step's target (DepState.slot as a mask) waits on step j - 1's
+// tags.  (Per-producer counters would spill the MC waves' 128 VGPRs.)
 struct DepState {
-    int n;                 // in-launch producers of this picture: steps j-1 .. j-n
-    uint32_t slot[DEP_MAX];  // their target slots
-    int pic[DEP_MAX];        // their picture indices
-    int known[DEP_MAX];
+    int n;                 // 1: the picture has in-launch producers
+    uint32_t slot;         // DEP3: their target slots (bit per physical slot, < 32); else step j-1's target slot
+    int pic;               // the step j - 1 picture
+    int known;             // its leading row workgroups seen done by this wave
 };
 
+template <bool DEP3>
 __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0, int lane, DepState &D)
 {
     // the record's dwords 4..6 (wave-uniform): per 8x8 partition the last MB
@@ -1880,29 +1884,54 @@ __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0,
     const uint32_t d0 = rec_dw(v0, 0);
     if ((d0 & 255) >= MBT_I4x4) return;
     const uint32_t rw01 = rec_dw(v0, 4), rw23 = rec_dw(v0, 5), refs = rec_dw(v0, 6);
-#pragma unroll
-    for (int k = 0; k < DEP_MAX; k++) {
-        if (k >= D.n) break;
-        // leading row workgroups of producer k this MB needs done
+    // leading row workgroups of the producers this MB needs done, then the
+    // poll of step j - 1's tags
+    if (DEP3) {
         int need = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t row = ((q < 2 ? rw01 : rw23) >> ((q & 1) * 16)) & 0xFFFF;
-            if (((refs >> (q * 8)) & 255) == D.slot[k]) need = max(need, (int)row + 2);
+            const uint32_t rs = (refs >> (q * 8)) & 255;
+            const uint32_t hit = rs < 32 ? (D.slot >> rs) & 1 : 0;
+            need = max(need, hit ? (int)row + 2 : 0);
         }
         need = min(need, a.h);
         unsigned spins = 0;
-        while (need > D.known[k]) {
-            const int idx = D.known[k] + lane;
-            const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic[k] * a.h + idx) == a.epoch;
+        while (need > D.known) {
+            const int idx = D.known + lane;
+            const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic * a.h + idx) == a.epoch;
             const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
             const int adv = __builtin_amdgcn_readfirstlane(~m ? __builtin_ctzll(~m) : 64);
-            D.known[k] = min(D.known[k] + adv, a.h);
+            D.known = min(D.known + adv, a.h);
             if (adv == 0) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known[k] = a.h; }
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known = a.h; }
             }
         }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 1; k++) {
+        if (k >= D.n) break;
+        int need = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t row = ((q < 2 ? rw01 : rw23) >> ((q & 1) * 16)) & 0xFFFF;
+            if (((refs >> (q * 8)) & 255) == D.slot) need = max(need, (int)row + 2);
+        }
+        need = min(need, a.h);
+        unsigned spins = 0;
+        while (need > D.known) {
+            const int idx = D.known + lane;
+            const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic * a.h + idx) == a.epoch;
+            const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+            const int adv = __builtin_amdgcn_readfirstlane(~m ? __builtin_ctzll(~m) : 64);
+            D.known = min(D.known + adv, a.h);
+            if (adv == 0) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known = a.h; }
+            }
+        }
+      }
     }
     // order the reference loads after the polls (compiler: the polls are
     // relaxed atomics; hardware: the wave issues in order)
@@ -1966,7 +1995,7 @@ __device__ __forceinline__ int chk_line_need(uint32_t off, uint32_t len, uint32_
     return n;
 }
 // (out of line, plain-value arguments: see mc_intra)
-__device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *perr, int mb, uint32_t v0, int lane, int dslot,
+__device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *perr, int mb, uint32_t v0, int lane, uint32_t smask,
                                                        int known)
 {
     const uint32_t d0 = rec_dw(v0, 0), refs = rec_dw(v0, 6);
@@ -1979,7 +2008,7 @@ __device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *pe
     {   // luma: lane -> block lb, window rows lsub + 4k (mc_issue)
         const int lb = lane >> 2, lsub = lane & 3;
         const uint32_t mvl = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + lb) << 2, (int)v0);
-        if ((int)((refs >> ((lb >> 2) * 8)) & 255) == dslot) {
+        if (const uint32_t rs = (refs >> ((lb >> 2) * 8)) & 255; rs < 32 && ((smask >> rs) & 1)) {
             const int mvx = (int)(int16_t)(mvl & 0xFFFF), mvy = (int)(int16_t)(mvl >> 16);
             const int x0 = clip3(0, W16 - 12, (mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2) & ~3);
             const int y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
@@ -1993,7 +2022,7 @@ __device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *pe
     {   // chroma: lane -> block cb, component
         const int cb = (lane & 31) >> 1, ccomp = lane & 1;
         const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
-        if ((int)((refs >> ((cb >> 2) * 8)) & 255) == dslot) {
+        if (const uint32_t rs = (refs >> ((cb >> 2) * 8)) & 255; rs < 32 && ((smask >> rs) & 1)) {
             const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
             const int x0 = clip3(0, CW - 8, (mbx * 8 + blk_x(cb) * 2 + (cmx >> 3)) & ~3);
             const int y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3);
@@ -2023,7 +2052,7 @@ __device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *pe
 #ifndef MC_DYN
 #define MC_DYN 1
 #endif
-template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK>
+template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK, bool DEP3>
 __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing<RK> &R,
                                        const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me)
 {
@@ -2033,13 +2062,22 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     D.n = 0;
     if (a.P > 1) {
         const int S = a.S, j = p / S;
+        if (DEP3) {
+            D.slot = 0; D.pic = 0; D.known = 0;
+            if (j > 0) {
+                D.n = 1;
+                D.pic = p - S;
+                uint32_t m = 0;
 #pragma unroll
-        for (int k = 1; k <= DEP_MAX; k++) {
-            if (k > j) break;
-            D.pic[D.n] = p - k * S;
-            D.slot[D.n] = __builtin_amdgcn_readfirstlane(a.pics[p - k * S].cur_slot);
-            D.known[D.n] = 0;
-            D.n++;
+                for (int k = 1; k < 4; k++)      // 4: H264MI_MAX_STEPS
+                    if (k <= j) m |= 1u << (a.pics[p - k * S].cur_slot & 31);
+                D.slot = __builtin_amdgcn_readfirstlane(m);
+            }
+        } else if (j >= 1) {
+            D.pic = p - S;
+            D.slot = __builtin_amdgcn_readfirstlane(a.pics[p - S].cur_slot);
+            D.known = 0;
+            D.n = 1;
         }
     }
     // the next MB of this wave: the row counter's (dynamic) or c + NMC.  The
@@ -2068,8 +2106,8 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     int c = c0;
     uint32_t v0 = c < a.w ? recrow[(size_t)c * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
-    if (c < a.w && D.n) dep_wait(a, p, v0, lane, D);
-    if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, (int)D.slot[0], D.known[0]);
+    if (c < a.w && D.n) dep_wait<DEP3>(a, p, v0, lane, D);
+    if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, DEP3 ? D.slot : 1u << (D.slot & 31), D.known);
     if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
 
     const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
@@ -2144,8 +2182,8 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         }
         c = cn;
         v0 = nv0;
-        if (c < a.w && D.n) dep_wait(a, p, v0, lane, D);
-        if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, (int)D.slot[0], D.known[0]);
+        if (c < a.w && D.n) dep_wait<DEP3>(a, p, v0, lane, D);
+        if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, DEP3 ? D.slot : 1u << (D.slot & 31), D.known);
         if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
     }
 }
@@ -2188,7 +2226,10 @@ struct WgppLds {
 #define WGPP2_WAVES_PER_EU 4
 #endif
 
-template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false>
+// DEP3: launches of three or more steps (dep_wait's slot mask and the
+// chained row tags); a separate instance, so that the code of launches of
+// one or two steps stays as it was measured
+template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false, bool DEP3 = false>
 __global__ __launch_bounds__(64 * (NMC + 2) * RPW)
 __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : WGPP2_WAVES_PER_EU))) void k_wgpp(ReconArgs a)
 {
@@ -2246,6 +2287,17 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
             // a later step of this launch may read this picture: once both
             // row waves' frame stores have completed, the second wave writes
             // the XCD's L2 back and tags the row done
+            if (DEP3 && j > 0) {
+                // chained tags (dep_wait): with three or more steps, row r of
+                // step j - 1 first -- normally long done, this picture's rows
+                // having waited on it
+                const uint32_t *pd = a.done + (size_t)(p - S) * a.h + r;
+                unsigned spins = 0;
+                while (__builtin_amdgcn_readfirstlane(ld_sc1_u32(pd)) != a.epoch) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); break; }
+                }
+            }
             drain_vm();
             int last = 0;
             if (lane == 0) last = __hip_atomic_fetch_add(&L[q].fin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2260,10 +2312,10 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
     McScratch &Mw = M[q * NMC + wid - 2];
-    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else mc_row<NMC, PROF, true, false, RK, CHK>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    else mc_row<NMC, PROF, true, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
 }
 template __global__ void k_wgpp<3, false, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 1>(ReconArgs);
@@ -2279,3 +2331,6 @@ template __global__ void k_wgpp<2, false, true, 1, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 2, true>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 2, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 3, true>(ReconArgs);
+// three or more steps per launch (single-row, 2 MC waves: launch_batch)
+template __global__ void k_wgpp<2, false, true, 1, false, true>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 1, true, true>(ReconArgs);

@@ -221,7 +221,8 @@ int h264mi_engine_decode_device_next(h264mi_engine *e, int npics, const void *d_
  * to be final (device row tags), so the later picture's top rows overlap the
  * earlier one's bottom rows.  The caller guarantees that no picture of the
  * batch writes a slot an earlier picture of the batch reads or writes.
- * P <= the engine's steps (h264mi_engine_set_steps, 1..2; default 1). */
+ * P <= the engine's steps (h264mi_engine_set_steps, 1..H264MI_MAX_STEPS;
+ * default 1; more than 1 needs at most 32 frame slots per stream). */
 int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P, const void *d_recs, const int16_t *d_coef,
                                       const void *d_pics, const void *next_recs, const int16_t *next_coef,
                                       const void *next_pics);
@@ -231,6 +232,7 @@ int h264mi_engine_decode_device_steps(h264mi_engine *e, int S, int P, const void
 int h264mi_engine_decode_device_steps_next(h264mi_engine *e, int S, int P, const void *d_recs,
                                            const int16_t *d_coef, const void *d_pics, const void *next_recs,
                                            const int16_t *next_coef, const void *next_pics, int next_P);
+#define H264MI_MAX_STEPS 4
 int h264mi_engine_set_steps(h264mi_engine *e, int steps);
 
 int  h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst);   /* D2H I420 */

@@ -120,3 +120,28 @@ def test_device_run_odd_warmup_and_steps():
     seq = _walk(main, S)
     assert all(seq[s] == [(v + ph[s]) % N for v in range(W + K)] for s in range(S))
     run.free()
+
+
+def test_device_run_pipe3_idr_last():
+    """Three steps per launch: physical slots renamed onto enough slots that
+    every launch -- the cyclic one across the GOP wrap included -- meets the
+    batch contract, every IDR the last picture of its launch, the driver's
+    odd warmup as leading single steps."""
+    caps = _caps()
+    S, N = len(caps), 12
+    for W, K in ((3, 9), (4, 8), (5, 7)):
+        ph = bench.gop_phases(S, N, 3, warmup=W)
+        run = bench.DeviceRun(None, caps, W, K, 3, dry=True, phases=ph)
+        assert run.P == 3 and run.nslots >= 3
+        main = run.launches[run.n_pre:]
+        rest = W + K - W % 3
+        assert [len(x) for x in main] == [1] * (W % 3) + [3] * (rest // 3) + ([rest % 3] if rest % 3 else [])
+        assert any(run.holds_idr(x) for x in main) and not any(run.holds_idr(x[:-1]) for x in main)
+        assert bench.pairs_ok(run.recs_h, run.pics_h, S, run.nmbs, N, 3, (W + ph[0]) % 3)
+        seq = _walk(main, S)
+        assert all(seq[s] == [(v + ph[s]) % N for v in range(W + K)] for s in range(S))
+        for launch in main:
+            for s in range(S):
+                slots = [run.slot_of[st[s]][s] for st in launch]
+                assert len(set(slots)) == len(slots)
+        run.free()

@@ -22,19 +22,20 @@ EDGE = sorted(n for n in CASES if n.startswith("edge_"))
 CHK_RING, CHK_RING_WR, CHK_REGION, CHK_PROG, CHK_REFROW = 64, 128, 256, 512, 1024
 
 
-@pytest.mark.parametrize("pipe,staggered", [(1, True), (2, False), (2, True)])
+@pytest.mark.parametrize("pipe,staggered", [(1, True), (2, False), (2, True), (3, True)])
 def test_checker_bench_shard_clean(pipe, staggered, monkeypatch):
     """Rank 0's configs[3] shard (8 x 1080p, 60 pictures each) through
     bench.DeviceRun under the checker: the bench's GOP-staggered plan with 1
-    and 2 steps per launch, and aligned frame-pipelined launches (two
-    pictures of every stream per launch: the reference-row checks run).
+    to 3 steps per launch (the reference-row checks against every earlier
+    step's slot), and aligned frame-pipelined launches (two pictures of
+    every stream per launch).
     Every picture vs the reference MD5s, no checker bit."""
     import bench
     monkeypatch.setenv("H264MI_CHECK", "1")
     seeds = bench.shard_seeds(0, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
-    phases = bench.gop_phases(8, n, pipe) if staggered else None
+    phases = bench.gop_phases(8, n, pipe, warmup=4) if staggered else None
     run = bench.DeviceRun(_lib.mi(), caps, 4, n - 4, pipe, phases=phases)
     try:
         assert run.P == pipe

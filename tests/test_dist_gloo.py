@@ -93,12 +93,12 @@ def test_bench_dry_run_two_ranks():
     line = json.loads(res[0].strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["steps"] == 3 and line["warmup"] == 1
     assert line["config"]["total_streams"] == 4 and line["config"]["seeds"] == "100..103"
-    # GOP phases 0 and 30 of the 60-picture streams (two steps per launch):
-    # 30 pre-roll launches + 1 warmup step + the 3 timed ones as a pair and a
-    # single, then the aligned P-only leg (2 pre-roll + 1 warmup + a pair)
+    # GOP phases 0 and 30 of the 60-picture streams (three steps per launch):
+    # 30 pre-roll launches + 1 warmup step + the 3 timed ones as one launch,
+    # then the aligned P-only leg (3 pre-roll + 1 warmup step + a triple)
     assert line["dry_run"]["preroll_launches"] == 30 and line["dry_run"]["seeds"] == [100, 101]
-    assert line["dry_run"]["launches"] == 30 + 1 + 2 + 2 + 1 + 1
-    assert line["kernels"]["k_wgpp"]["trace_steps"] == [2, 1]
+    assert line["dry_run"]["launches"] == 30 + 1 + 1 + 3 + 1 + 1
+    assert line["kernels"]["k_wgpp"]["trace_steps"] == [3]
     assert line["value"] > 0 and line["scaling"] == "weak"
     assert line["bitexact_check"]["frames_expected"] == 2 * 2 * 4
     assert line["p_only"]["i_pictures_timed"] == 0

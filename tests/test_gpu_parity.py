@@ -184,7 +184,8 @@ def test_engine_bench_streams_vs_reference(rpw, mc, monkeypatch):
 
 
 @pytest.mark.parametrize("rank,pipe,staggered",
-                         [(r, 2, True) for r in range(8)] + [(0, 1, True), (1, 1, True), (0, 2, False), (1, 2, False)])
+                         [(r, 2, True) for r in range(8)] + [(0, 1, True), (1, 1, True), (0, 2, False), (1, 2, False),
+                                                             (0, 3, True), (1, 3, True), (0, 4, True)])
 def test_configs3_shard_vs_reference(rank, pipe, staggered):
     """configs[3]: 64 streams, 8 per GPU.  Rank r's shard (seeds 100+8r ..
     100+8r+7, bench.shard_seeds) through bench.py's own device-resident path
@@ -192,24 +193,25 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
     k_prep in each launch's tail) and its verification pass.  staggered: GOP
     phases staggered over the streams, each 60-picture stream decoded
     cyclically after an untimed pre-roll -- with pipe 2 (the bench default)
-    two consecutive pictures of every stream per launch, the phases odd so
-    that an IDR is always the second picture of its launch; aligned: decode order from picture 0, every
-    launch two steps (frame-pipelined batches).  Every picture of every
+    two consecutive pictures of every stream per launch (3 and 4 too), the
+    phases such that an IDR is always the last picture of its launch;
+    aligned: decode order from picture 0, every launch P steps
+    (frame-pipelined batches).  Every picture of every
     launch vs the reference MD5s, and after the run every frame slot's last
     picture."""
     import bench
     seeds = bench.shard_seeds(rank, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
-    phases = bench.gop_phases(8, n, pipe) if staggered else None
+    phases = bench.gop_phases(8, n, pipe, warmup=4) if staggered else None
     run = bench.DeviceRun(_lib.mi(), caps, 4, n - 4, pipe, phases=phases)
     try:
         assert run.P == pipe and all(d == 0 for _, d in run.placement())
         if staggered:
             steps = sum(len(x) for x in run.launches[run.n_pre:])
             assert run.n_pre == max(phases) and steps == n
-            # no two-step launch starts with an IDR (odd phases: IDRs are second)
-            assert all(not run.holds_idr(x[:1]) for x in run.launches[run.n_pre:] if len(x) > 1)
+            # an IDR is always the last picture of its launch (the phases)
+            assert all(not run.holds_idr(x[:-1]) for x in run.launches[run.n_pre:])
             timed = run.timed_pictures()
             # stream s's IDR is at step (n - phase) % n: those in the timed window
             want = sum(1 for ph in phases if 4 <= (n - ph) % n)
@@ -225,10 +227,10 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
         run.free()
 
 
-@pytest.mark.parametrize("wh", [(13, 7), (12, 9), (20, 11)])
-def test_engine_pipelined_steps_vs_oracle(wh):
-    """Frame-pipelined launches (two consecutive pictures of each of 3
-    streams per launch, physical slots renamed) on sizes whose chroma rows
+@pytest.mark.parametrize("wh,pipe", [((13, 7), 2), ((12, 9), 2), ((20, 11), 2), ((13, 7), 3), ((20, 11), 4)])
+def test_engine_pipelined_steps_vs_oracle(wh, pipe):
+    """Frame-pipelined launches (two to four consecutive pictures of each of
+    3 streams per launch, physical slots renamed) on sizes whose chroma rows
     and Cb/Cr planes do not end on 128-B lines (odd w*h: a line straddles
     the Cb/Cr boundary), every picture vs the oracle's decode of the stream."""
     import bench
@@ -238,10 +240,10 @@ def test_engine_pipelined_steps_vs_oracle(wh):
     caps = [Capture(s) for s in streams]
     refs = [O.decode(s)[0] for s in streams]
     n = min(c.npics for c in caps)
-    n -= n % 2
-    run = bench.DeviceRun(_lib.mi(), caps, 0, n, 2)
+    n -= n % pipe
+    run = bench.DeviceRun(_lib.mi(), caps, 0, n, pipe)
     try:
-        assert run.P == 2
+        assert run.P == pipe
         for i, launch in enumerate(run.launches):
             run.launch(i)
             run.eng.sync()
