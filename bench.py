@@ -1158,7 +1158,7 @@ def main(argv=None):
                        "i_share_timed": round(n_i_all / max(frames_total, 1), 5),
                        "parallelism": f"streams sharded {S}/GPU over {world} rank(s), no collective; "
                                       f"{P} consecutive picture(s) of each stream per launch"},
-            "roofline": {"kernel": f"k_wgpp (one launch = {P} step(s)" + (", one step when it would hold an IDR" if P > 1 and phases else "") +
+            "roofline": {"kernel": f"k_wgpp (one launch = {P} step(s)" + (", every IDR the last picture of its launch" if P > 1 and phases else "") +
                                    "; k_prep of the next launch runs in its tail)",
                          # what limits the kernel: the MB-row deblocking dependency chain
                          # (DESIGN.md §3), not HBM; `frac` is still quoted against the HBM
