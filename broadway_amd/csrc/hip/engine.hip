@@ -364,9 +364,11 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     // rounds); H264MI_ROW_PRIO=0 turns it off
     static const int row_prio = getenv("H264MI_ROW_PRIO") ? atoi(getenv("H264MI_ROW_PRIO")) : 1;
     a.row_prio_split = row_prio;
-    // study knob: the 2-MC-wave urgency distance (MBs, default 8)
-    static const int mc_urg = getenv("H264MI_MC_URGENCY") ? atoi(getenv("H264MI_MC_URGENCY")) : 8;
-    a.mc_urgency = mc_urg;
+    // the 2-MC-wave urgency distance (MBs; H264MI_MC_URGENCY): 8, and 12 in
+    // launches of three or more steps (profiles/r93_ab_knobs_pipe3.txt: 303.0
+    // vs 303.9 us per step, 4 of 4 rounds)
+    static const int mc_urg = getenv("H264MI_MC_URGENCY") ? atoi(getenv("H264MI_MC_URGENCY")) : 0;
+    a.mc_urgency = mc_urg > 0 ? mc_urg : P > 2 ? 12 : 8;
     a.chk_inject = e->check ? e->check_inject : 0;
 
     a.pics = d_pics;
