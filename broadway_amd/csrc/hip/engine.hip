@@ -376,7 +376,11 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     a.w = e->w; a.h = e->h;
     a.err = e->d_err;
     a.S = S;
-    a.P = P;
+    // study knob (H264MI_STUDY_NODEP=1; output NOT valid): the steps of a
+    // launch wait on nothing -- the overlap an exact finer-grained dependency
+    // could reach at most
+    static const bool nodep = getenv("H264MI_STUDY_NODEP") && atoi(getenv("H264MI_STUDY_NODEP"));
+    a.P = nodep ? 1 : P;
     a.done = e->d_done;
     a.dbrec = e->d_dbrec + hb * mbs * 64;
     a.res = e->d_res + hb * mbs * 384;
