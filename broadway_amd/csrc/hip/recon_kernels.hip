@@ -1873,6 +1873,9 @@ struct DepState {
     uint32_t slot;         // DEP3: their target slots (bit per physical slot, < 32); else step j-1's target slot
     int pic;               // the step j - 1 picture
     int known;             // its leading row workgroups seen done by this wave
+#ifdef STUDY_NEAR
+    int cap;               // study build (output not valid): waits capped at the MB's own row + 3
+#endif
 };
 
 template <bool DEP3>
@@ -1896,6 +1899,9 @@ __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0,
             need = max(need, hit ? (int)row + 2 : 0);
         }
         need = min(need, a.h);
+#ifdef STUDY_NEAR
+        need = min(need, D.cap);
+#endif
         unsigned spins = 0;
         while (need > D.known) {
             const int idx = D.known + lane;
@@ -1919,6 +1925,9 @@ __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0,
             if (((refs >> (q * 8)) & 255) == D.slot) need = max(need, (int)row + 2);
         }
         need = min(need, a.h);
+#ifdef STUDY_NEAR
+        need = min(need, D.cap);
+#endif
         unsigned spins = 0;
         while (need > D.known) {
             const int idx = D.known + lane;
@@ -2060,6 +2069,9 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     const uint32_t *recrow = (const uint32_t *)(a.rec + pd.rec_base + r * a.w);
     DepState D;
     D.n = 0;
+#ifdef STUDY_NEAR
+    D.cap = min(r + 3, a.h);
+#endif
     if (a.P > 1) {
         const int S = a.S, j = p / S;
         if (DEP3) {
