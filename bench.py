@@ -64,6 +64,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MBREC = 96
 MAX_E2E_PROCS = 8          # end-to-end leg: decoder processes (the box allows 16 GPU processes)
+E2E_REPS = 18              # end-to-end leg: passes over each 60-picture stream (>= 3 s at ~360 frames/s per process)
 
 
 def parse_args(argv=None):
@@ -367,7 +368,8 @@ def rgba_leg(torch, L, eng, S, w_mbs, h_mbs, reps=50):
     base = eng.frame_ptr(0, 0)
     stride = eng.frame_ptr(1, 0) - base if S > 1 else 0
     st = torch.cuda.current_stream()
-    launch = lambda: L.h264mi_yuv2rgba_device(base, out.data_ptr(), width, height, S, stride, width * height * 4,
+    launch = lambda: L.h264mi_yuv2rgba_device_pitch(base, out.data_ptr(), width, height, eng.chroma_pitch, S, stride,
+                                                    width * height * 4,
                                               st.cuda_stream)
     for _ in range(5):
         assert launch() == 0
@@ -457,21 +459,27 @@ def e2e_core_plan(local: int, numa, allowed):
     return plan[local], plan
 
 
-def end_to_end(streams, nframes, reps=3, device=0, cpus=None):
+def end_to_end(streams, nframes, reps=E2E_REPS, device=0, cpus=None, max_procs=MAX_E2E_PROCS, release=None):
     """End-to-end decode through the product C-ABI: one
     broadway_amd/lib/h264mi_dec process per stream (at most MAX_E2E_PROCS),
     all in parallel (one host thread each), each decoding its stream `reps`
     times -- host CAVLC parse, H2D of the MB records, k_prep + k_wgpp, D2H of
     every output picture.  Rate = all pictures / the slowest process's decode
     time (HIP start-up of each process excluded; it is paid before its timed
-    loop).  The processes decode on GPU `device` (H264MI_DEVICE) and, given
-    `cpus`, run pinned to those host cores (h264mi_dec -A: the process and
-    every thread it starts)."""
+    loop).  Start gate (h264mi_dec -G): every process reports ready after its
+    warm-up and all are released at once; the rate divides all pictures by
+    the union of the processes' decode windows (CLOCK_MONOTONIC, earliest
+    start to latest end), so start-up skew cannot inflate it.  The processes
+    decode on GPU `device` (H264MI_DEVICE) and, given `cpus`, run pinned to
+    those host cores (h264mi_dec -A: the process and every thread it
+    starts).  `release`, if given, is called once every local process is
+    ready and before they are released (the ranks' barrier: all GPUs' decoder
+    processes start together)."""
     from broadway_amd import _lib
     exe = os.path.join(_lib.LIB_DIR, "h264mi_dec")      # H264MI_LIB_DIR: an A/B build's
     if not os.path.exists(exe):
         return None
-    streams = streams[:MAX_E2E_PROCS]
+    streams = streams[:max_procs]
     # a thread waiting for the GPU sleeps instead of spinning: the host cores
     # are the bound on this path (tools/e2e_env_sweep.sh: 1.89k -> 2.08k fps)
     env = dict(os.environ)
@@ -489,9 +497,21 @@ def end_to_end(streams, nframes, reps=3, device=0, cpus=None):
             pth = os.path.join(td, f"s{i}.h264")
             with open(pth, "wb") as f:
                 f.write(s)
-            procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T"] + pin + [pth], stdout=subprocess.PIPE,
-                                          stderr=subprocess.PIPE, text=True, env=env))
-        secs, pics, parts, cpu_s, sys_s = [], 0, {}, 0.0, 0.0
+            procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T", "-G"] + pin + [pth], stdin=subprocess.PIPE,
+                                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
+        # start gate: wait until every process has warmed up, then release all
+        for pr in procs:
+            line = pr.stdout.readline()
+            if line.strip() != "ready":
+                pr.wait(timeout=60)
+                raise RuntimeError(f"h264mi_dec not ready: {line!r} {pr.stderr.read().strip()[-300:]}")
+        if release is not None:
+            release()
+        for pr in procs:
+            pr.stdin.write("g")
+            pr.stdin.flush()
+        secs, pics, parts, cpu_s, sys_s, starts, ends = [], 0, {}, 0.0, 0.0, [], []
+        threads = {}
         for pr in procs:
             o, e = pr.communicate(timeout=600)
             if pr.returncode != 0:
@@ -504,15 +524,26 @@ def end_to_end(streams, nframes, reps=3, device=0, cpus=None):
                     pics += int(f[1])
                 elif f[0] == "decode_seconds":
                     secs.append(float(f[1]))
+                elif f[0] == "t_start_mono":
+                    starts.append(float(f[1]))
+                elif f[0] == "t_end_mono":
+                    ends.append(float(f[1]))
                 elif f[0].startswith("t_") and len(f) > 1:
                     parts[f[0]] = parts.get(f[0], 0.0) + float(f[1])
                 elif f[0] == "cpu_seconds":
                     cpu_s += float(f[1])
                 elif f[0] == "cpu_sys_seconds":
                     sys_s += float(f[1])
-        t = max(secs)
+                elif f[0] in ("cpu_decode_threads_seconds", "cpu_spec_workers_seconds", "cpu_other_live_threads_seconds"):
+                    threads[f[0]] = threads.get(f[0], 0.0) + float(f[1])
+        # the union of the decode windows: all processes released together
+        t = max(ends) - min(starts) if starts and ends else max(secs)
         res = {"value": round(pics / t, 2), "unit": "frames/s", "host_threads": len(streams),
                "pictures": pics, "seconds": round(t, 6), "device": device,
+               "window": "union of the processes' decode windows after a common start gate",
+               "start_skew_ms": round((max(starts) - min(starts)) * 1e3, 3) if starts else None,
+               "t_start_mono": min(starts) if starts else None, "t_end_mono": max(ends) if ends else None,
+               "longest_single_window_s": round(max(secs), 6),
                "host_cores_assigned": len(cpus) if cpus else None,
                "cpus": format_cpulist(cpus) if cpus else None,
                "sample": f"{len(streams)} x {nframes}-frame 1080p streams x {reps} passes, one h264mi_dec process "
@@ -529,10 +560,24 @@ def end_to_end(streams, nframes, reps=3, device=0, cpus=None):
             res["host_cpu_ms_per_picture"] = round(cpu_s * 1e3 / pics, 3)
             res["host_sys_ms_per_picture"] = round(sys_s * 1e3 / pics, 3)   # of which in the kernel (HIP ioctls, page pinning)
             res["host_cores_busy"] = round(cpu_s / t, 2)
+            if threads:
+                # where the host CPU goes (ms per picture): the calling
+                # (decoding) threads -- parse, submit, waits -- the
+                # speculative-parse workers, the other threads alive in the
+                # process (HIP runtime), and what none of these covers
+                dec = threads.get("cpu_decode_threads_seconds", 0.0)
+                spec = threads.get("cpu_spec_workers_seconds", 0.0)
+                oth = threads.get("cpu_other_live_threads_seconds", 0.0)
+                res["host_cpu_by_thread_ms_per_picture"] = {
+                    "decoding_threads": round(dec * 1e3 / pics, 3),
+                    "spec_parse_workers": round(spec * 1e3 / pics, 3),
+                    "hip_runtime_and_other_threads": round(oth * 1e3 / pics, 3),
+                    "unattributed": round((cpu_s - dec - spec - oth) * 1e3 / pics, 3)}
         # the same streams in ONE process, one thread (H264SwDec instance) per
         # stream, sharing one batched engine (h264mi_set_share, -S)
         paths = [os.path.join(td, f"s{i}.h264") for i in range(len(streams))]
-        o = subprocess.run([exe, "-Onone", f"-r{reps}", "-T", f"-S{len(streams)}"] + pin + paths, capture_output=True,
+        o = subprocess.run([exe, "-Onone", f"-r{max(1, reps // 3)}", "-T", f"-S{len(streams)}"] + pin + paths,
+                           capture_output=True,
                            text=True, timeout=600, env=env)
         if o.returncode == 0:
             d = {}
@@ -552,6 +597,43 @@ def end_to_end(streams, nframes, reps=3, device=0, cpus=None):
         return res
     finally:
         shutil.rmtree(td, ignore_errors=True)
+
+
+def load_ubench():
+    """Lone-wave chain costs from the committed micro-benchmark
+    (tools/ubench/ubench_deblock.hip's JSON line -> profiles/ubench.json), or
+    None."""
+    p = os.path.join(ROOT, "profiles", "ubench.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        return json.load(f)
+
+
+def latency_floor(w_mbs, h_mbs, steps, ub, launch_us):
+    """The row chain's latency floor, beside the HBM
+    roofline: a picture cannot finish before its last row has run W MBs of
+    lone-wave vertical + horizontal passes after H - 1 row-to-row hand-offs,
+    each the patch edge plus one granule hop; a later picture of a
+    frame-pipelined launch trails the earlier one by at least two row lags
+    and one 128-B line of MB columns plus the store-progress lag (8 MBs).
+    The floor is per launch (the S streams' pictures run side by side);
+    `frac` = floor / the measured launch time."""
+    if not ub:
+        return None
+    mb = ub["vh_us"]
+    lag = ub["patch_us"] + min(ub["hop_same_xcd_us"], ub["hop_other_xcd_us"])
+    pic = w_mbs * mb + (h_mbs - 1) * lag
+    trail = 2 * lag + 8 * mb
+    floor = pic + (steps - 1) * trail
+    return {"model": "W x (V+H) + (H-1) x (patch + hop) per picture, + (P-1) x (2 row lags + 8 MB periods) "
+                     "per frame-pipelined launch",
+            "per_mb_vh_us": round(mb, 4), "row_lag_us": round(lag, 4),
+            "picture_floor_us": round(pic, 2), "step_trail_us": round(trail, 2),
+            "launch_floor_us": round(floor, 2), "steps_per_launch": steps,
+            "measured_launch_us": round(launch_us, 2),
+            "frac": round(floor / launch_us, 4) if launch_us else None,
+            "source": ub.get("source", "profiles/ubench.json")}
 
 
 def load_traffic():
@@ -1113,14 +1195,23 @@ def main(argv=None):
         # pinned at N = 1 too: the GPU's NUMA-local cores (tools/e2e_only.py
         # E2E_PIN A/B, profiles/r80_e2e_pin.txt: 4.53-4.68 vs 4.97-5.70 ms of
         # host CPU per picture, and steadier)
-        e2e = end_to_end(streams, nframes, device=local, cpus=my_cpus if my_cpus else None)
+        # one-device rehearsal (BENCH_ONE_DEVICE=1): every rank's processes
+        # share one GPU, which admits 16 GPU processes -- fewer per rank
+        procs = MAX_E2E_PROCS if os.environ.get("BENCH_ONE_DEVICE") != "1" or world == 1 \
+            else max(1, (16 - world) // world)
+        e2e = end_to_end(streams, nframes, device=local, cpus=my_cpus if my_cpus else None, max_procs=procs,
+                         release=dist.barrier if dist else None)
     if dist:
         plans, e2es = [None] * world, [None] * world
         dist.all_gather_object(plans, e2e_plan)
         dist.all_gather_object(e2es, e2e)
         if e2e is not None and all(x is not None for x in e2es):
-            # all ranks decoded at once: every rank's pictures over the slowest rank's time
-            e2e = {"value": round(sum(x["pictures"] for x in e2es) / max(x["seconds"] for x in e2es), 2),
+            # all ranks' processes released together (the barrier in the
+            # start gate): every rank's pictures over the union of all windows
+            # (CLOCK_MONOTONIC is one clock on the host)
+            span = max(x["t_end_mono"] for x in e2es) - min(x["t_start_mono"] for x in e2es)
+            e2e = {"value": round(sum(x["pictures"] for x in e2es) / span, 2),
+                   "seconds": round(span, 6), "window": "union of every rank's decode windows, common start gate",
                    "unit": "frames/s", "n_gpus": world,
                    "host_cores_total": sum(x["host_cores_assigned"] or 0 for x in e2es),
                    "host_cpu_ms_per_picture": round(sum(x.get("host_cpu_ms_per_picture", 0) * x["pictures"] for x in e2es)
@@ -1192,7 +1283,10 @@ def main(argv=None):
                          "launches_p_only": {"n": split["p"][0], "avg_launch_kernel_us": split["p"][1],
                                              "avg_us_per_step": split["p"][2]} if split else None,
                          "aggregate_achieved_GBs": round(frame_read_gbs, 1),
-                         "traffic_source": traffic.get("source") if traffic else None},
+                         "traffic_source": traffic.get("source") if traffic else None,
+                         # the bound this kernel actually has: the row chain's latency
+                         "latency": latency_floor(w, h, P, load_ubench(),
+                                                  (split["p"][1] if split and split["p"][0] else step_us))},
             "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2),
                                    "pictures_per_launch": round(S * a.steps / max(launches_timed, 1), 2),
                                    "steps_per_launch": P,

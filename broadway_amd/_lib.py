@@ -163,6 +163,9 @@ def mi() -> C.CDLL:
     L.h264mi_engine_read_rgba.restype = i32
     L.h264mi_yuv2rgba_device.argtypes = [vp, vp, i32, i32, i32, C.c_size_t, C.c_size_t, vp]
     L.h264mi_yuv2rgba_device.restype = i32
+    if hasattr(L, "h264mi_yuv2rgba_device_pitch"):      # (absent from A/B builds of older trees)
+        L.h264mi_yuv2rgba_device_pitch.argtypes = [vp, vp, i32, i32, i32, i32, C.c_size_t, C.c_size_t, vp]
+        L.h264mi_yuv2rgba_device_pitch.restype = i32
     L.H264SwDecNextPictureRGBA.argtypes = [vp, C.POINTER(H264SwDecPicture), u32, vp]
     L.H264SwDecNextPictureRGBA.restype = i32
     L.h264mi_engine_sync.argtypes = [vp]
@@ -194,6 +197,11 @@ def mi() -> C.CDLL:
     L.h264mi_engine_frame_ptr.restype = vp
     L.h264mi_engine_frame_bytes.argtypes = [vp]
     L.h264mi_engine_frame_bytes.restype = sz
+    if hasattr(L, "h264mi_engine_slot_bytes"):
+        L.h264mi_engine_slot_bytes.argtypes = [vp]
+        L.h264mi_engine_slot_bytes.restype = sz
+        L.h264mi_engine_chroma_pitch.argtypes = [vp]
+        L.h264mi_engine_chroma_pitch.restype = i32
     L.h264mi_capture_stream.argtypes = [vp, sz, i32]
     L.h264mi_capture_stream.restype = vp
     L.h264mi_capture_info.argtypes = [vp] + [C.POINTER(i32)] * 5

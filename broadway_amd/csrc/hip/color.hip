@@ -52,22 +52,23 @@ __device__ __forceinline__ void rgba_group(const uint8_t *Y, const uint8_t *U, c
 
 // grid: (ceil(groups / 128) blocks of 64 threads, npics), groups = the
 // picture's (row pair, 4-column group) pairs in raster order, so no lane
-// idles at row ends; picture k at in + k * in_stride -> out + k * out_stride
+// idles at row ends; picture k at in + k * in_stride -> out + k * out_stride;
+// chroma rows cpitch bytes apart (width / 2 packed, H264MI_CPITCH in a slot)
 __global__ __launch_bounds__(64) void k_yuv2rgba(const uint8_t *__restrict__ in, uint8_t *__restrict__ out, int width,
-                                                 int height, size_t in_stride, size_t out_stride)
+                                                 int height, int cpitch, size_t in_stride, size_t out_stride)
 {
     const int ng = width >> 2;                      // 4-column groups per row
     const int nf = ng * (height >> 1);
     const uint8_t *Y = in + blockIdx.y * in_stride;
     const uint8_t *U = Y + (size_t)width * height;
-    const uint8_t *V = U + (size_t)(width >> 1) * (height >> 1);
+    const uint8_t *V = U + (size_t)cpitch * (height >> 1);
     uint8_t *O = out + blockIdx.y * out_stride;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int f = blockIdx.x * 128 + h * 64 + (int)threadIdx.x;
         if (f < nf) {
             const int y2 = f / ng, g = f - y2 * ng;
-            rgba_group(Y, U, V, O, width, (size_t)(2 * y2) * width + 4 * g, (size_t)y2 * (width >> 1) + 2 * g);
+            rgba_group(Y, U, V, O, width, (size_t)(2 * y2) * width + 4 * g, (size_t)y2 * cpitch + 2 * g);
         }
     }
 }

@@ -75,7 +75,7 @@ __device__ __forceinline__ void cc_plane_fp(const int32_t (*S)[4], int A, int B,
 // dynamic LDS bound of k_conceal (one byte per MB): the CU's 160 KB less
 // the static sums and headroom
 #define CONCEAL_LDS_MAX (159 * 1024)
-__global__ __launch_bounds__(64) void k_conceal(uint8_t *frame, int w, int h, const int *order, int n,
+__global__ __launch_bounds__(64) void k_conceal(uint8_t *frame, int w, int h, int cp, const int *order, int n,
                                                const uint8_t *dec0)
 {
     extern __shared__ uint8_t cc_dec[];
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(64) void k_conceal(uint8_t *frame, int w, int h, co
     const int nmbs = w * h;
     for (int i = lane; i < nmbs; i += 64) cc_dec[i] = dec0[i];
     __syncthreads();
-    const int W = w * 16, H = h * 16, CW = W / 2;
+    const int W = w * 16, H = h * 16, CW = cp;     // chroma row pitch (H264MI_CPITCH)
     uint8_t *const Y = frame;
     uint8_t *const U = frame + (size_t)W * H;
     uint8_t *const V = U + (size_t)CW * (H / 2);

@@ -27,7 +27,9 @@
 struct h264mi_engine {
     int dev;
     int w, h, nmbs, nstreams, nslots;
-    size_t frame_bytes;
+    size_t frame_bytes;           // device slot stride (H264MI_SLOT_BYTES: chroma rows padded to 128 B)
+    size_t pic_bytes;             // packed I420 picture (what leaves the device)
+    int cpitch;                   // chroma row pitch in a slot (H264MI_CPITCH)
     uint8_t *d_frames;
     unsigned long long *d_mbx;    // row mailboxes: 32 granules (256 B) per batch MB
     unsigned epoch;
@@ -78,9 +80,10 @@ struct h264mi_engine {
     int tev_stride, tev_seq;  // record every tev_stride-th launch (h264mi_engine_set_timing_stride)
     uint8_t *d_rgba;          // h264mi_engine_read_rgba staging (w*h*4 B, allocated on first use)
     int steps;                // pictures per stream per launch (h264mi_engine_set_steps)
-    unsigned *d_done;         // per picture row of a launch: epoch tag once the row is final in its slot
+    unsigned long long *d_prog;   // per picture row of a launch, per row wave: {MBs stored, epoch} (frame-pipelined launches)
     int check;                // H264MI_CHECK=1: the dependency-checker kernels (recon_kernels.hip CHK_*)
     int check_inject;         // H264MI_CHECK_INJECT: test hook (ReconArgs::chk_inject)
+    int check_short_cols, check_short_rows;   // H264MI_CHECK_INJECT_REFCOLS / _REFROWS: test hooks
     uint32_t err_bits;        // OR of every picture's device flags since the last h264mi_engine_error_bits
 };
 
@@ -89,9 +92,9 @@ struct h264mi_engine {
 static void free_pic_buffers(h264mi_engine *e)
 {
     (void)hipFree(e->d_mbx); (void)hipFree(e->d_dbrec); (void)hipFree(e->d_res); (void)hipFree(e->d_err);
-    (void)hipFree(e->d_done);
+    (void)hipFree(e->d_prog);
     (void)hipHostFree(e->h_err);
-    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL; e->d_done = NULL;
+    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL; e->d_prog = NULL;
     e->h_err = NULL;
     e->pipe_cap = 0;
 }
@@ -103,13 +106,13 @@ static int alloc_pic_buffers(h264mi_engine *e, int cap)
               hipMalloc(&e->d_dbrec, 2 * mbs * 64) == hipSuccess &&
               hipMalloc(&e->d_res, 2 * mbs * 768) == hipSuccess &&
               hipMalloc(&e->d_err, sizeof(unsigned) * np) == hipSuccess &&
-              hipMalloc(&e->d_done, sizeof(unsigned) * np * e->h) == hipSuccess &&
+              hipMalloc(&e->d_prog, sizeof(unsigned long long) * 2 * np * e->h) == hipSuccess &&
               hipHostMalloc(&e->h_err, sizeof(unsigned) * np, hipHostMallocDefault) == hipSuccess;
     if (!ok) { free_pic_buffers(e); return -1; }
     // cleared granules carry epoch 0, which no launch uses
     (void)hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st);
     (void)hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * np, e->st);
-    (void)hipMemsetAsync(e->d_done, 0, sizeof(unsigned) * np * e->h, e->st);
+    (void)hipMemsetAsync(e->d_prog, 0, sizeof(unsigned long long) * 2 * np * e->h, e->st);
     memset(e->h_err, 0, sizeof(unsigned) * np);
     e->pipe_cap = cap;
     return 0;
@@ -128,7 +131,9 @@ static void engine_config(h264mi_engine *e)
     e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
     e->launch_intra = -1;
     e->check = getenv("H264MI_CHECK") && atoi(getenv("H264MI_CHECK"));
-    e->check_inject = getenv("H264MI_CHECK_INJECT") ? atoi(getenv("H264MI_CHECK_INJECT")) : 0;
+    e->check_inject = h264mi_test_hooks() && getenv("H264MI_CHECK_INJECT") ? atoi(getenv("H264MI_CHECK_INJECT")) : 0;
+    e->check_short_cols = h264mi_test_hooks() && getenv("H264MI_CHECK_INJECT_REFCOLS") ? atoi(getenv("H264MI_CHECK_INJECT_REFCOLS")) : 0;
+    e->check_short_rows = h264mi_test_hooks() && getenv("H264MI_CHECK_INJECT_REFROWS") ? atoi(getenv("H264MI_CHECK_INJECT_REFROWS")) : 0;
     const char *rp = getenv("H264MI_RPW");
     e->rpw_env = rp ? atoi(rp) : 0;
     if (e->rpw_env < 0 || e->rpw_env > 3) e->rpw_env = 0;
@@ -178,9 +183,14 @@ static void engine_config(h264mi_engine *e)
     // k_conceal keeps one decoded flag per MB in dynamic LDS: up to the CU's
     // 160 KB less its static part; larger pictures conceal on the host
     // (engine_conceal_fits -> the backend's conceal_ok)
-    e->conceal_fits = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conceal),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, CONCEAL_LDS_MAX) == hipSuccess &&
-                      (size_t)e->nmbs <= CONCEAL_LDS_MAX;
+    // (one byte per MB; the attribute is raised only for pictures above the
+    // default 64 KB limit (less k_conceal's static sums and headroom), so a
+    // device that refuses it still conceals
+    // the sizes that fit)
+    e->conceal_fits = (size_t)e->nmbs <= 60 * 1024 ||
+                      ((size_t)e->nmbs <= CONCEAL_LDS_MAX &&
+                       hipFuncSetAttribute(reinterpret_cast<const void *>(&k_conceal),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, CONCEAL_LDS_MAX) == hipSuccess);
 }
 
 extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots)
@@ -202,7 +212,9 @@ extern "C" h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs,
     e->w = w_mbs; e->h = h_mbs; e->nmbs = w_mbs * h_mbs;
     e->nstreams = nstreams; e->nslots = nslots;
     e->steps = 1;
-    e->frame_bytes = (size_t)e->nmbs * 384;
+    e->frame_bytes = H264MI_SLOT_BYTES(w_mbs, h_mbs);
+    e->pic_bytes = (size_t)e->nmbs * 384;
+    e->cpitch = H264MI_CPITCH(w_mbs);
     e->coef_cap = (size_t)nstreams * e->nmbs * 8 + 1024;
     e->h_coef_cap = e->coef_cap;
     bool ok = hipMalloc(&e->d_frames, e->frame_bytes * nslots * nstreams) == hipSuccess &&
@@ -339,6 +351,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     memset(&a, 0, sizeof(a));
     a.frames = e->d_frames;
     a.frame_bytes = e->frame_bytes;
+    a.cpitch = e->cpitch;
     a.rec = d_rec;
     a.coef = d_coef;
     a.mbx = e->d_mbx;
@@ -346,7 +359,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     if (++e->epoch >= (1u << 20)) {           // granule tags: epoch in the high dword
         if (h264mi_engine_sync(e)) return -1;
         HIPCHECK(hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st));
-        HIPCHECK(hipMemsetAsync(e->d_done, 0, sizeof(unsigned) * e->pipe_cap * e->h, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_prog, 0, sizeof(unsigned long long) * 2 * e->pipe_cap * e->h, e->st));
         e->epoch = 1;
     }
     a.epoch = e->epoch;
@@ -370,18 +383,24 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     static const int mc_urg = getenv("H264MI_MC_URGENCY") ? atoi(getenv("H264MI_MC_URGENCY")) : 0;
     a.mc_urgency = mc_urg > 0 ? mc_urg : P > 2 ? 12 : 8;
     a.chk_inject = e->check ? e->check_inject : 0;
+    a.chk_short_cols = e->check ? e->check_short_cols : 0;
+    a.chk_short_rows = e->check ? e->check_short_rows : 0;
 
     a.pics = d_pics;
     a.npics = npics;
     a.w = e->w; a.h = e->h;
     a.err = e->d_err;
     a.S = S;
-    // study knob (H264MI_STUDY_NODEP=1; output NOT valid): the steps of a
+    // study build only (-DSTUDY_NODEP; output NOT valid): the steps of a
     // launch wait on nothing -- the overlap an exact finer-grained dependency
-    // could reach at most
-    static const bool nodep = getenv("H264MI_STUDY_NODEP") && atoi(getenv("H264MI_STUDY_NODEP"));
-    a.P = nodep ? 1 : P;
-    a.done = e->d_done;
+    // could reach at most.  A compile-time switch, like
+    // STUDY_NEAR: no environment variable changes what the library computes
+#ifdef STUDY_NODEP
+    a.P = 1;
+#else
+    a.P = P;
+#endif
+    a.prog = e->d_prog;
     a.dbrec = e->d_dbrec + hb * mbs * 64;
     a.res = e->d_res + hb * mbs * 384;
     const int rows = npics * e->h;
@@ -405,13 +424,14 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     }
     const bool rec = e->timing || rec_tev;
     e->last_kernel = "k_wgpp";
-    // three or more steps: the DEP3 instances (single-row, 2 MC waves)
-    const bool dep3 = P > 2;
+    // frame-pipelined launches: the DEP3 instances (single-row, 2 MC waves;
+    // store-progress granules and column-granular waits)
+    const bool dep3 = P > 1;
     const int rpw = dep3 ? 1 : rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
     const int nmc = dep3 ? 2 : launch_nmc(e, rpw, P);
     e->launch_intra = -1;                     // a hint covers one launch
-    const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w) : WgppLds<2, 1>::bytes(e->w))
+    const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w) : WgppLds<2, 1>::bytes(e->w, dep3))
                         : rpw == 3 ? WgppLds<3, 3>::bytes(e->w) : rpw == 2 ? WgppLds<3, 2>::bytes(e->w)
                         : WgppLds<3, 1>::bytes(e->w);
     if (dep3) {
@@ -603,7 +623,8 @@ extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)
 {
     // (frame-pipelined launches name the earlier steps' target slots in a
     // 32-bit mask: recon_kernels.hip dep_wait)
-    if (!e || steps < 1 || steps > H264MI_MAX_STEPS || (steps > 1 && e->nslots > 32)) return -1;
+    // (a later step's producers are found by slot equality, 8-bit slots)
+    if (!e || steps < 1 || steps > H264MI_MAX_STEPS || (steps > 1 && e->nslots > 255)) return -1;
     if (steps == e->steps) return 0;
     if (h264mi_engine_sync(e)) return -1;
     free_pic_buffers(e);
@@ -765,27 +786,51 @@ extern "C" int h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long
     return 0;
 }
 
+// D2H of a slot as packed I420 on `st`, asynchronous: the luma plane and the
+// padded chroma rows (H264MI_CPITCH) as one strided copy of 2 * h * 8 rows
+int engine_copy_out(h264mi_engine *e, int stream, int slot, uint8_t *dst, hipStream_t st)
+{
+    const uint8_t *src = e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot);
+    const size_t ysz = (size_t)e->nmbs * 256, cw = (size_t)e->w * 8;
+    if ((size_t)e->cpitch == cw) {
+        HIPCHECK(hipMemcpyAsync(dst, src, e->pic_bytes, hipMemcpyDeviceToHost, st));
+        return 0;
+    }
+    HIPCHECK(hipMemcpyAsync(dst, src, ysz, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipMemcpy2DAsync(dst + ysz, cw, src + ysz, (size_t)e->cpitch, cw, (size_t)e->h * 16, hipMemcpyDeviceToHost, st));
+    return 0;
+}
+size_t engine_slot_bytes(const h264mi_engine *e) { return e->frame_bytes; }
+
 extern "C" int h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst)
 {
     if (!e || stream < 0 || stream >= e->nstreams || slot < 0 || slot >= e->nslots) return -1;
     if (h264mi_engine_sync(e)) return -1;
-    HIPCHECK(hipMemcpy(dst, e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot), e->frame_bytes,
-                       hipMemcpyDeviceToHost));
+    if (engine_copy_out(e, stream, slot, dst, e->st)) return -1;
+    HIPCHECK(hipStreamSynchronize(e->st));
     return 0;
 }
 
 // I420 -> RGBA (DecoderPost.js `rgb: true`, color.hip) for `npics` pictures
 // of width x height pixels at in + k * in_stride -> out + k * out_stride,
 // device pointers, on `stream` (NULL: the null stream); asynchronous
+extern "C" int h264mi_yuv2rgba_device_pitch(const void *d_i420, void *d_rgba, int width, int height, int cpitch,
+                                            int npics, size_t in_stride, size_t out_stride, void *stream)
+{
+    if (!d_i420 || !d_rgba || width <= 0 || height <= 0 || (width & 15) || (height & 15) || npics < 1 ||
+        cpitch < width / 2)
+        return -1;
+    const int nblk = ((height >> 1) * (width >> 2) + 127) >> 7;
+    hipLaunchKernelGGL(k_yuv2rgba, dim3(nblk, npics), dim3(64), 0, (hipStream_t)stream,
+                       (const uint8_t *)d_i420, (uint8_t *)d_rgba, width, height, cpitch, in_stride, out_stride);
+    HIPCHECK(hipGetLastError());
+    return 0;
+}
+
 extern "C" int h264mi_yuv2rgba_device(const void *d_i420, void *d_rgba, int width, int height, int npics,
                                       size_t in_stride, size_t out_stride, void *stream)
 {
-    if (!d_i420 || !d_rgba || width <= 0 || height <= 0 || (width & 15) || (height & 15) || npics < 1) return -1;
-    const int nblk = ((height >> 1) * (width >> 2) + 127) >> 7;
-    hipLaunchKernelGGL(k_yuv2rgba, dim3(nblk, npics), dim3(64), 0, (hipStream_t)stream,
-                       (const uint8_t *)d_i420, (uint8_t *)d_rgba, width, height, in_stride, out_stride);
-    HIPCHECK(hipGetLastError());
-    return 0;
+    return h264mi_yuv2rgba_device_pitch(d_i420, d_rgba, width, height, width / 2, npics, in_stride, out_stride, stream);
 }
 
 extern "C" int h264mi_engine_read_rgba(h264mi_engine *e, int stream, int slot, uint8_t *dst)
@@ -793,8 +838,8 @@ extern "C" int h264mi_engine_read_rgba(h264mi_engine *e, int stream, int slot, u
     if (!e || stream < 0 || stream >= e->nstreams || slot < 0 || slot >= e->nslots) return -1;
     const size_t bytes = (size_t)e->nmbs * 256 * 4;
     if (!e->d_rgba) HIPCHECK(hipMalloc(&e->d_rgba, bytes));
-    if (h264mi_yuv2rgba_device(e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot), e->d_rgba,
-                               e->w * 16, e->h * 16, 1, 0, 0, e->st))
+    if (h264mi_yuv2rgba_device_pitch(e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot), e->d_rgba,
+                                     e->w * 16, e->h * 16, e->cpitch, 1, 0, 0, e->st))
         return -1;
     HIPCHECK(hipMemcpyAsync(dst, e->d_rgba, bytes, hipMemcpyDeviceToHost, e->st));
     HIPCHECK(hipStreamSynchronize(e->st));
@@ -807,7 +852,9 @@ extern "C" void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot)
     return e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot);
 }
 
-extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? e->frame_bytes : 0; }
+extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? e->pic_bytes : 0; }
+extern "C" size_t h264mi_engine_slot_bytes(h264mi_engine *e) { return e ? e->frame_bytes : 0; }
+extern "C" int h264mi_engine_chroma_pitch(h264mi_engine *e) { return e ? e->cpitch : 0; }
 
 // neighbour-based concealment of a picture's missing MBs on the device
 // (k_conceal, conceal.hip), behind the work already on the engine's stream:
@@ -843,7 +890,7 @@ extern "C" int h264mi_engine_conceal(h264mi_engine *e, int stream, int slot, con
     HIPCHECK(hipMemcpyAsync(e->d_conceal, e->h_conceal, bytes, hipMemcpyHostToDevice, e->st));
     HIPCHECK(hipEventRecord(e->ev_conceal, e->st));
     hipLaunchKernelGGL(k_conceal, dim3(1), dim3(64), (size_t)e->nmbs, e->st, (uint8_t *)h264mi_engine_frame_ptr(e, stream, slot),
-                       e->w, e->h, (const int *)e->d_conceal, n, (const uint8_t *)(e->d_conceal + sizeof(int) * (size_t)e->nmbs));
+                       e->w, e->h, e->cpitch, (const int *)e->d_conceal, n, (const uint8_t *)(e->d_conceal + sizeof(int) * (size_t)e->nmbs));
     HIPCHECK(hipGetLastError());
     g_conceal_launches++;
     return 0;
@@ -920,7 +967,9 @@ int engine_reuse(h264mi_engine *e)
     HIPCHECK(hipSetDevice(e->dev));
     engine_config(e);
     e->prepped_rec = e->prepped_pics = NULL;
+    e->prepped_n = 0;
     e->err_accum = 0;
+    e->err_bits = 0;          // the previous owner's device / checker flags
     e->steps = 1;
     e->last_kernel = NULL;
     // the epoch keeps counting: the mailboxes hold tags of earlier launches only

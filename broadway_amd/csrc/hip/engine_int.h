@@ -24,6 +24,11 @@ int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int
  * was created under H264MI_BLOCKING_SYNC); no flag accounting */
 int engine_wait(h264mi_engine *e);
 hipStream_t engine_stream(h264mi_engine *e);
+/* a slot's device stride (H264MI_SLOT_BYTES) and its D2H as packed I420 on st */
+size_t engine_slot_bytes(const h264mi_engine *e);
+int engine_copy_out(h264mi_engine *e, int stream, int slot, uint8_t *dst, hipStream_t st);
+/* 1 when H264MI_TEST=1: test hooks are honoured (host/capture.c) */
+extern "C" int h264mi_test_hooks(void);
 /* device flag words of the batch's pictures (ReconArgs::err), one per picture */
 unsigned *engine_err_words(h264mi_engine *e);
 /* the engine's shape and whether its waits sleep (H264MI_BLOCKING_SYNC at creation) */

@@ -26,8 +26,9 @@
 #define PROF_MB 8
 
 struct ReconArgs {
-    uint8_t *frames;          // frame pool (I420 per slot)
-    unsigned long long frame_bytes;
+    uint8_t *frames;          // frame pool (I420 per slot, chroma rows cpitch apart: H264MI_CPITCH)
+    unsigned long long frame_bytes;     // slot stride (H264MI_SLOT_BYTES)
+    int cpitch;               // chroma row pitch (bytes)
     const MbRec *rec;         // batch records (pictures back to back)
     const int16_t *coef;      // batch coefficient blocks
     const PicDesc *pics;
@@ -55,10 +56,12 @@ struct ReconArgs {
     // frame-pipelined launches (P > 1): the launch holds P consecutive
     // pictures of each of the S streams, step-major (picture p = j * S + s);
     // step j's MC reads of a slot written by step j - k of the same launch
-    // wait for that picture's rows (done[(p - k * S) * h + r] == epoch, set
-    // by row r's workgroup after its frame stores and an agent release)
+    // wait for that picture's store progress: prog[((p - k * S) * h + r) * 2
+    // + w] = {MBs of row wave w's parity below this are stored, epoch}, an
+    // 8-B granule the row wave publishes behind its write-through frame
+    // stores (row_pp, dep_wait)
     int P;
-    unsigned int *done;
+    unsigned long long *prog;
     // profiling build only: 1 = the row waves only drain the MC ring (no
     // deblocking, no stores) -- SQ counters of such a launch minus those of
     // a normal one split the instruction counts by wave role (tools/sq_roles.py)
@@ -76,6 +79,9 @@ struct ReconArgs {
     // deliberately breaks one hand-off so the tests can see the checker fire
     // (0: none; 1: MB 5 of every row hands the row waves a wrong ring tag)
     int chk_inject;
+    // (frame-pipelined CHK launches) test hooks: dep_wait waits for this many
+    // MB columns / rows less than the loads need, which CHK_REFROW must catch
+    int chk_short_cols, chk_short_rows;
 };
 
 // Dependency checker (the reference's compile-time
@@ -88,8 +94,9 @@ struct ReconArgs {
 //               whose H pass its hdone announced
 //   CHK_PROG    an intra progress word names another MB than the left one
 //   CHK_REFROW  (frame-pipelined launches) a reference line is read from a
-//               picture of the same launch before every row holding a byte
-//               of it was tagged final -- checks the host's set_ref_rows
+//               picture of the same launch before every (MB row, MB column)
+//               holding a byte of it was published final -- checks the
+//               host's set_ref_rows against the loads' own geometry
 // The checker's MB tags ride in bytes 22..23 of the 64-B deblocking record
 // (class 0's threshold entry {alpha, beta, tc0[3], indexA} leaves them
 // unused): the MC wave writes MB c's index there with the record it puts in
@@ -1289,9 +1296,17 @@ struct __attribute__((aligned(16))) PPLds {
 // UPL / MEL: the row above's mailbox (mbx_up) / this row's (mbx_me) is the
 // workgroup's LDS one (k_wgpp RPW = 2: the upper row of the pair publishes to
 // LDS, the lower one reads from there)
-template <bool PROF, bool UPL, bool MEL, int RK, bool CHK>
+// COLP (frame-pipelined launches): when a later step of the launch reads
+// this picture (pubp), the frame stores are write-through (sc1) and the wave
+// publishes its store progress, a granule {c, epoch} at the top of each MB c
+// behind an s_waitcnt vmcnt(0): every MB of its parity below c is in memory
+// (MI355X_MICROARCH.md, valid forms: sc1 payload, drained, sc1 flag).  A
+// sample of MB row r, column x is final once row r's MBs 0..x+1 and row
+// r+1's MBs 0..x have stored (row r+1 stores row r's rows 12..15 after its
+// top-edge filter; MB x+1 stores MB x's columns 12..15 after its left edge).
+template <bool PROF, bool UPL, bool MEL, int RK, bool CHK, bool COLP = false>
 __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing<RK> *R,
-                       const unsigned long long *mbx_up, unsigned long long *mbx_me)
+                       const unsigned long long *mbx_up, unsigned long long *mbx_me, bool pubp = false)
 {
     const int W = a.w, H = a.h;
     if (PROF && a.prof_mode == 1) {     // role split (see ReconArgs::prof_mode): drain the ring only
@@ -1309,7 +1324,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     const PicDesc *pdp = a.pics + p;
     const int rec_base = __builtin_amdgcn_readfirstlane(pdp->rec_base);
     const int fslot = __builtin_amdgcn_readfirstlane(pdp->frame_base + pdp->cur_slot);
-    const int W16 = W * 16, H16 = H * 16, CW = W16 / 2, CH = H16 / 2;
+    const int W16 = W * 16, H16 = H * 16, CP = a.cpitch, CH = H16 / 2;
     uint8_t *cur = a.frames + (unsigned long long)fslot * a.frame_bytes;
     uint8_t *curU = cur + (size_t)W16 * H16;
     unsigned *perr = a.err + p;
@@ -1328,9 +1343,9 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;          // chroma dwords (32..63 mirror)
     const int le = li < 24 ? li : li - 8;                                        // mailbox entry dword
     uint8_t *const ybase = cur + (size_t)r * 16 * W16;
-    uint8_t *const cbase = curU + (size_t)r * 8 * CW;
+    uint8_t *const cbase = curU + (size_t)r * 8 * CP;
     const uint32_t yoff = (uint32_t)(orow * W16 + oq * 4);
-    const uint32_t coff = (uint32_t)(ccomp * CW * CH + crow * CW + cq * 4);
+    const uint32_t coff = (uint32_t)(ccomp * CP * CH + crow * CP + cq * 4);
     // common-case frame store maps (as row_unit): offsets in the region /
     // relative to (row r*16-4 | r*8-2, col -4) of MB c
     uint32_t sa_lds, sa_glb, sb_lds, sb_glb;
@@ -1351,7 +1366,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         else if (k < 24) { comp = (k - 12) / 6; row = (k - 12) % 6; col = -4; }
         else { comp = (k - 24) >> 2; row = -2 + (((k - 24) >> 1) & 1); col = ((k - 24) & 1) * 4; }
         sb_lds = (uint32_t)((comp ? Lrv : Lru) + (row + 2) * RC_S + 4 + col);
-        sb_glb = (uint32_t)(comp * CW * CH + (row + 2) * CW + col + 4);
+        sb_glb = (uint32_t)(comp * CP * CH + (row + 2) * CP + col + 4);
         sb_left = k >= 12 && k < 24;
         sb_top = k >= 24;
     }
@@ -1436,6 +1451,17 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                             : (uint32_t)((int)(junk - Lb) + lane * 4);
     }
     unsigned long long *const sink = a.gjunk + ((p * H + r) & 127) * 64 + lane;
+    const bool wt = COLP && pubp;       // write-through frame stores + progress granules
+#ifdef STUDY_COLP_PLAIN
+    const bool wst = false;             // study build (output not valid): plain frame stores
+#else
+    const bool wst = wt;
+#endif
+    unsigned long long *const prog_me = a.prog + ((size_t)p * H + r) * 2 + w;
+    auto fst = [&](void *ptr, uint32_t v) {
+        if (wst) st32<true>(ptr, v);
+        else st32<false>(ptr, v);
+    };
 
     unsigned long long pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const bool prof = PROF && a.prof != nullptr;
@@ -1450,6 +1476,14 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 
     for (int c = w; c < W; c += 2) {
         if (a.row_prio_split) __builtin_amdgcn_s_setprio(1);
+        if (wt && c >= 2) {
+            // MB c - 2's write-through stores (issued one MB of the partner
+            // earlier) drained: publish this wave's progress, off the chain
+#ifndef STUDY_COLP_NOWAIT
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+            if (lane == 0) st_gran(prog_me, (uint32_t)c, tag);
+        }
         if (prof) tc0 = clock64();
         // per-MB stamps (100 MHz wall clock): [0] row-above entry c in hand (H(c)
         // may start); [1] V(c) start (after the hdone wait and halo copy) in
@@ -1624,41 +1658,46 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             const uint32_t va = *(const uint32_t *)(Lb + sa_lds);
             const uint32_t vb = *(const uint32_t *)(Lb + sb_lds);
             uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
-            uint8_t *const cb = cbase + c * 8 - 2 * CW - 4;
+            uint8_t *const cb = cbase + c * 8 - 2 * CP - 4;
             const bool oka = (!sa_left || c > 0) && (!sa_top || has_up);
             const bool okb = (!sb_left || c > 0) && (!sb_top || has_up);
-            st32<false>(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
-            st32<false>(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
+            fst(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
+            fst(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
         } else {
             const int yrows = last_row ? 16 : 12;
             const int crows = last_row ? 8 : 6;
             const bool last_col = c == W - 1;
             if (orow < yrows && (oq < 3 || last_col))
-                st32<false>(ybase + c * 16 + yoff, *(const uint32_t *)&G.ry[(orow + 4) * RY_S + 4 + oq * 4]);
+                fst(ybase + c * 16 + yoff, *(const uint32_t *)&G.ry[(orow + 4) * RY_S + 4 + oq * 4]);
             if (lane < 32 && crow < crows && (cq == 0 || last_col))
-                st32<false>(cbase + c * 8 + coff, *(const uint32_t *)&(ccomp ? G.rv : G.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
+                fst(cbase + c * 8 + coff, *(const uint32_t *)&(ccomp ? G.rv : G.ru)[(crow + 2) * RC_S + 4 + cq * 4]);
             if (c > 0) {
                 if (lane < 16) {
                     if (lane < yrows)
-                        st32<false>(ybase + c * 16 - 4 + lane * W16, *(const uint32_t *)&G.ry[(lane + 4) * RY_S]);
+                        fst(ybase + c * 16 - 4 + lane * W16, *(const uint32_t *)&G.ry[(lane + 4) * RY_S]);
                 } else if (lane < 32) {
                     const int k = lane - 16, comp = k >> 3, row = k & 7;
                     if (row < crows)
-                        st32<false>(cbase + c * 8 - 4 + comp * CW * CH + row * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[(row + 2) * RC_S]);
+                        fst(cbase + c * 8 - 4 + comp * CP * CH + row * CP, *(const uint32_t *)&(comp ? G.rv : G.ru)[(row + 2) * RC_S]);
                 }
             }
             if (has_up) {
                 if (lane >= 32 && lane < 48) {
                     const int k = lane - 32;
-                    st32<false>(ybase + c * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&G.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
+                    fst(ybase + c * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&G.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
                 } else if (lane >= 48 && lane < 56) {
                     const int k = lane - 48, comp = k >> 2, row = (k >> 1) & 1, qq = k & 1;
-                    st32<false>(cbase + c * 8 + qq * 4 + comp * CW * CH + (row - 2) * CW, *(const uint32_t *)&(comp ? G.rv : G.ru)[row * RC_S + 4 + qq * 4]);
+                    fst(cbase + c * 8 + qq * 4 + comp * CP * CH + (row - 2) * CP, *(const uint32_t *)&(comp ? G.rv : G.ru)[row * RC_S + 4 + qq * 4]);
                 }
             }
         }
         wave_sync();
         PPT(4);
+    }
+    if (wt) {
+        // the row's last MBs of this parity: every MB of the wave stored
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) st_gran(prog_me, (uint32_t)W, tag);
     }
     if (prof) {
         unsigned long long *o = a.prof + ((size_t)r * a.npics + p) * 16;
@@ -1736,11 +1775,11 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
         L.c_ax = clip3(0, CW - 8, L.c_x0 & ~3);
         {
             const uint8_t *ref = a.frames + (unsigned long long)(pd.frame_base + ((refs >> ((cb >> 2) * 8)) & 255)) * a.frame_bytes +
-                                 (unsigned long long)W16 * H16 + (unsigned long long)ccomp * CW * CH;
+                                 (unsigned long long)W16 * H16 + (unsigned long long)ccomp * a.cpitch * CH;
 #pragma unroll
             for (int wy = 0; wy < 3; wy++) {
                 const int y = clip3(0, CH - 1, c_y0 + wy);
-                const uint32_t *src = (const uint32_t *)(ref + (size_t)y * CW + L.c_ax);
+                const uint32_t *src = (const uint32_t *)(ref + (size_t)y * a.cpitch + L.c_ax);
                 uint2 t;
                 __builtin_memcpy(&t, src, 8);                 // one dwordx2 load (4-byte aligned)
                 L.cw[wy][0] = t.x; L.cw[wy][1] = t.y;
@@ -1854,93 +1893,118 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
 
 // Frame-pipelined launches (a.P > 1): before MB mb's reference loads are
 // issued, wait until every 128-B line they touch is final in the slots that
-// earlier steps of this launch reconstruct.  Row r of a picture is final in
-// memory once row workgroups 0..r+1 are done (row r+1 stores row r's rows
-// 12..15 after its top-edge filter; the last row stores its own).  A line
-// is only read once all of its bytes are final, so no CU's L1 and no XCD's
-// L2 ever holds a stale copy of it (the producer's release writes its L2
-// back; lines from earlier launches were dropped at kernel start), and the
-// loads themselves stay plain.
+// earlier steps of this launch reconstruct.  Each lane takes the windows it
+// loads itself (mc_issue's geometry: luma block lane >> 2, window rows
+// lane & 3 .. 8; chroma block (lane & 31) >> 1, component lane & 1): the MB
+// rows R_lo..R_hi their lines hold and the last MB column X of those lines.
+// They need rows R_lo..R_hi final through column X -- those row workgroups'
+// stores through MB X + 1 -- and row R_hi + 1's through MB X (row_pp).  A
+// line is only read once all of its bytes are final, so no CU's L1 and no
+// XCD's L2 ever holds a stale copy of it (the frame stores are write-through;
+// lines from earlier launches were dropped at kernel start), and the loads
+// themselves stay plain.  Luma rows whose 128-B lines also hold the end of
+// the row above (w % 8 != 0) need that row to its last column.
 //
-// Three or more steps: the done tags are chained -- row r of step j >= 1 tags
-// itself done only once row r of step j - 1 is (k_wgpp), so the step j - 1
-// picture's leading rows seen done imply the same rows of every earlier step
-// done, and one counter covers every in-launch producer: a partition whose
-// reference slot is any earlier step's target (DepState.slot as a mask) waits on step j - 1's
-// tags.  (Per-producer counters would spill the MC waves' 128 VGPRs.)
+// The producer of a block's reference is the earlier step whose picture of
+// this stream writes that slot (at most one: no picture of a launch writes a
+// slot an earlier one reads or writes).  Its store progress is read from its
+// granules (one per row wave, 8 B: {MBs stored, epoch}); what the row's MC
+// waves have seen is kept in the workgroup's LDS (values only grow, so any
+// value a wave stores is a valid lower bound), so most MBs need no load.
+#define PC_ROWS 136         // MB rows of a producer the LDS progress cache holds (2160p: 135)
 struct DepState {
-    int n;                 // 1: the picture has in-launch producers
-    uint32_t slot;         // DEP3: their target slots (bit per physical slot, < 32); else step j-1's target slot
-    int pic;               // the step j - 1 picture
-    int known;             // its leading row workgroups seen done by this wave
-#ifdef STUDY_NEAR
-    int cap;               // study build (output not valid): waits capped at the MB's own row + 3
-#endif
+    int n;                 // in-launch producers: steps j - 1 .. j - n (0: none)
+    uint32_t slots;        // their target slots, 8 bits each (step j - 1 - k at bits 8k)
 };
+typedef __attribute__((address_space(3))) unsigned long long lds_u2;   // {wave 0, wave 1} progress
 
-template <bool DEP3>
-__device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, uint32_t v0, int lane, DepState &D)
+// rows R_lo..R_hi of producer k final through MB column X (and R_hi + 1
+// through X - 1); load: poll the granules the LDS cache cannot vouch for
+__device__ __forceinline__ bool dep_rows_ok(const ReconArgs &a, int p, int k, int rlo, int rhi, int X, bool load,
+                                            lds_u2 *pc)
 {
-    // the record's dwords 4..6 (wave-uniform): per 8x8 partition the last MB
-    // row of its reference slot that its MC lines touch (MbRec.i4 of an
-    // inter MB, filled by the host) and the slot
-    const uint32_t d0 = rec_dw(v0, 0);
+    const int pk = p - (k + 1) * a.S;
+    bool ok = true;
+    for (int R = rlo; R <= rhi + 1 && R < a.h; R++) {
+        const uint32_t need = (uint32_t)min(R <= rhi ? X + 2 : X + 1, a.w);
+        const unsigned long long c = R < PC_ROWS ? pc[k * PC_ROWS + R] : 0ull;
+        uint32_t vx = (uint32_t)c, vy = (uint32_t)(c >> 32);
+        if (min(vx, vy) < need && load) {
+            const unsigned long long *g = a.prog + ((size_t)pk * a.h + R) * 2;
+            const unsigned long long g0 = ld_gran(g), g1 = ld_gran(g + 1);
+            if ((uint32_t)(g0 >> 32) == a.epoch) vx = max(vx, (uint32_t)g0);
+            if ((uint32_t)(g1 >> 32) == a.epoch) vy = max(vy, (uint32_t)g1);
+            if (R < PC_ROWS) pc[k * PC_ROWS + R] = (unsigned long long)vx | ((unsigned long long)vy << 32);
+        }
+        ok &= min(vx, vy) >= need;
+    }
+    return ok;
+}
+
+template <bool CHK>
+__device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, int mb, uint32_t v0, int lane, const DepState &D,
+                                         lds_u2 *pc)
+{
+    const uint32_t d0 = rec_dw(v0, 0), refs = rec_dw(v0, 6);
     if ((d0 & 255) >= MBT_I4x4) return;
-    const uint32_t rw01 = rec_dw(v0, 4), rw23 = rec_dw(v0, 5), refs = rec_dw(v0, 6);
-    // leading row workgroups of the producers this MB needs done, then the
-    // poll of step j - 1's tags
-    if (DEP3) {
-        int need = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t row = ((q < 2 ? rw01 : rw23) >> ((q & 1) * 16)) & 0xFFFF;
-            const uint32_t rs = (refs >> (q * 8)) & 255;
-            const uint32_t hit = rs < 32 ? (D.slot >> rs) & 1 : 0;
-            need = max(need, hit ? (int)row + 2 : 0);
-        }
-        need = min(need, a.h);
-#ifdef STUDY_NEAR
-        need = min(need, D.cap);
+#ifdef STUDY_DEP_NOPOLL
+    return;                             // study build (output not valid): no in-launch wait
 #endif
-        unsigned spins = 0;
-        while (need > D.known) {
-            const int idx = D.known + lane;
-            const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic * a.h + idx) == a.epoch;
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
-            const int adv = __builtin_amdgcn_readfirstlane(~m ? __builtin_ctzll(~m) : 64);
-            D.known = min(D.known + adv, a.h);
-            if (adv == 0) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known = a.h; }
-            }
+    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
+    const int mbx = mb % a.w, mby = mb / a.w;
+    auto producer = [&](uint32_t rs) -> int {
+        int k = -1;
+        for (int i = 0; i < D.n; i++)
+            if (((D.slots >> (i * 8)) & 255) == rs) k = i;
+        return k;
+    };
+    // luma: block lb, window rows lsub .. 8 (mc_issue)
+    int kl, lrlo, lrhi, lx;
+    {
+        const int lb = lane >> 2, lsub = lane & 3;
+        const uint32_t mvl = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + lb) << 2, (int)v0);
+        kl = producer((refs >> ((lb >> 2) * 8)) & 255);
+        const int mvx = (int)(int16_t)(mvl & 0xFFFF), mvy = (int)(int16_t)(mvl >> 16);
+        const int x0 = clip3(0, W16 - 12, (mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2) & ~3);
+        const int y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
+        const int ya = clip3(0, H16 - 1, y0 + lsub), yb = clip3(0, H16 - 1, y0 + 8);
+        if ((W16 & 127) == 0) {             // rows end on lines: a line holds one row's bytes
+            lrlo = ya >> 4; lrhi = yb >> 4;
+            lx = min((x0 + 11) | 127, W16 - 1) >> 4;
+        } else {                            // a line can hold the end of earlier rows: to their last column
+            const uint32_t ls = ((uint32_t)ya * W16 + x0) & ~127u, le = ((uint32_t)yb * W16 + x0 + 11) | 127u;
+            lrlo = (int)(ls / (uint32_t)W16) >> 4;
+            lrhi = min((int)(le / (uint32_t)W16), H16 - 1) >> 4;
+            lx = a.w - 1;
         }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 1; k++) {
-        if (k >= D.n) break;
-        int need = 0;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t row = ((q < 2 ? rw01 : rw23) >> ((q & 1) * 16)) & 0xFFFF;
-            if (((refs >> (q * 8)) & 255) == D.slot) need = max(need, (int)row + 2);
+    }
+    // chroma: block cb, component lane & 1, rows 0..2 (chroma rows padded to 128 B)
+    int kc, crlo, crhi, cx;
+    {
+        const int cb = (lane & 31) >> 1;
+        const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
+        kc = producer((refs >> ((cb >> 2) * 8)) & 255);
+        const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
+        const int x0 = clip3(0, CW - 8, (mbx * 8 + blk_x(cb) * 2 + (cmx >> 3)) & ~3);
+        const int y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3);
+        crlo = clip3(0, CH - 1, y0) >> 3; crhi = clip3(0, CH - 1, y0 + 2) >> 3;
+        cx = min((x0 + 7) | 127, CW - 1) >> 3;
+    }
+    if (CHK && a.chk_short_cols) { lx = max(lx - a.chk_short_cols, 0); cx = max(cx - a.chk_short_cols, 0); }
+    if (CHK && a.chk_short_rows) {
+        lrhi = max(lrhi - a.chk_short_rows, 0); crhi = max(crhi - a.chk_short_rows, 0);
+        lrlo = min(lrlo, lrhi); crlo = min(crlo, crhi);
+    }
+    bool okl = kl < 0, okc = kc < 0;
+    unsigned spins = 0;
+    for (int pass = 0;; pass++) {
+        if (!okl) okl = dep_rows_ok(a, p, kl, lrlo, lrhi, lx, pass > 0, pc);
+        if (!okc) okc = dep_rows_ok(a, p, kc, crlo, crhi, cx, pass > 0, pc);
+        if (__builtin_amdgcn_ballot_w64(!(okl && okc)) == 0) break;
+        if (pass > 0) {
+            __builtin_amdgcn_s_sleep(4);
+            if (++spins > (1u << 21)) { if (lane == 0) atomicOr(a.err + p, 32u); break; }
         }
-        need = min(need, a.h);
-#ifdef STUDY_NEAR
-        need = min(need, D.cap);
-#endif
-        unsigned spins = 0;
-        while (need > D.known) {
-            const int idx = D.known + lane;
-            const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic * a.h + idx) == a.epoch;
-            const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
-            const int adv = __builtin_amdgcn_readfirstlane(~m ? __builtin_ctzll(~m) : 64);
-            D.known = min(D.known + adv, a.h);
-            if (adv == 0) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known = a.h; }
-            }
-        }
-      }
     }
     // order the reference loads after the polls (compiler: the polls are
     // relaxed atomics; hardware: the wave issues in order)
@@ -1981,68 +2045,84 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
         prep_mb(pa, g, lane, wid < NM ? M[wid] : Mx[wid - NM], R.db[wid], T);
 }
 
-// Dependency checker, frame-pipelined launches: the rows of the in-launch
-// producer picture that MB mb's reference loads need final, from the loads'
-// own geometry (mc_issue's windows, at 128-B line granularity, each line's
-// first and last byte and the last byte before a plane boundary it crosses),
-// must all be among the leading rows dep_wait saw done (D.known) -- i.e. the
-// host's set_ref_rows (capture.c) covered every line the kernel reads.  Rows
-// 0..R+1 done make MB row R's bytes final (row R+1 stores R's rows 12..15).
-__device__ __forceinline__ int chk_need_of(uint32_t o, uint32_t ysz, uint32_t csz, int W16, int CW, int h)
+// Dependency checker, frame-pipelined launches: every 128-B line MB mb's
+// reference loads touch (mc_issue's windows, recomputed from the loads' own
+// geometry) must already be final in its in-launch producer picture --
+// (MB row, MB column) by (MB row, MB column) of the bytes it holds, read from
+// the producers' progress granules just before the loads are issued (values
+// only grow: what is final then is final when the loads run).  This checks
+// the host's set_ref_rows encoding and dep_wait together.
+__device__ __forceinline__ bool chk_row_final(const ReconArgs &a, int pk, int R, uint32_t need)
 {
-    // MB rows whose workgroups must be done for byte o of a slot to be final
-    const int R = o < ysz ? (int)(o / (uint32_t)W16) >> 4
-                          : (int)(((o < ysz + csz ? o - ysz : o - ysz - csz)) / (uint32_t)CW) >> 3;
-    return min(R + 2, h);
+    if (R >= a.h || need == 0) return true;
+    const unsigned long long *g = a.prog + ((size_t)pk * a.h + R) * 2;
+    const unsigned long long g0 = ld_gran(g), g1 = ld_gran(g + 1);
+    const uint32_t v0 = (uint32_t)(g0 >> 32) == a.epoch ? (uint32_t)g0 : 0u;
+    const uint32_t v1 = (uint32_t)(g1 >> 32) == a.epoch ? (uint32_t)g1 : 0u;
+    return min(v0, v1) >= need;
 }
-__device__ __forceinline__ int chk_line_need(uint32_t off, uint32_t len, uint32_t ysz, uint32_t csz, int W16, int CW, int h)
+// the bytes [o, o + len) of a plane at pbase (pitch, rows, width bytes; MB
+// mbh rows x mbw bytes): every line they touch final in producer pk
+__device__ __forceinline__ bool chk_access(const ReconArgs &a, int pk, uint32_t o, int len, uint32_t pbase, int pitch,
+                                           int rows, int width, int mbh, int mbw)
 {
-    const uint32_t l0 = off & ~127u, l1 = min(((off + len - 1) | 127u), ysz + 2 * csz - 1);
-    int n = max(chk_need_of(l0, ysz, csz, W16, CW, h), chk_need_of(l1, ysz, csz, W16, CW, h));
-    if (l0 < ysz && l1 >= ysz) n = max(n, chk_need_of(ysz - 1, ysz, csz, W16, CW, h));
-    if (l0 < ysz + csz && l1 >= ysz + csz) n = max(n, chk_need_of(ysz + csz - 1, ysz, csz, W16, CW, h));
-    return n;
+    bool ok = true;
+    for (uint32_t l = o >> 7; l <= (o + len - 1) >> 7; l++) {
+        const uint32_t s0 = (l << 7) - pbase, e = (l << 7) + 127 - pbase;
+        const int ya = (int)(s0 / (uint32_t)pitch);
+        const int yb = min((int)(e / (uint32_t)pitch), rows - 1);
+        const int xe = ya == yb ? min((int)(e % (uint32_t)pitch), width - 1) / mbw : (width - 1) / mbw;
+        for (int R = ya / mbh; R <= yb / mbh; R++)
+            ok &= chk_row_final(a, pk, R, (uint32_t)min(xe + 2, a.w)) && chk_row_final(a, pk, R + 1, (uint32_t)min(xe + 1, a.w));
+    }
+    return ok;
 }
-// (out of line, plain-value arguments: see mc_intra)
-__device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *perr, int mb, uint32_t v0, int lane, uint32_t smask,
-                                                       int known)
+// (inline: an out-of-line call with the kernel arguments by reference
+// fails instruction selection -- a divergent copy into SGPRs)
+__device__ __forceinline__ void chk_ref_rows(const ReconArgs &a, int p, int mb, uint32_t v0, int lane, const DepState &D)
 {
     const uint32_t d0 = rec_dw(v0, 0), refs = rec_dw(v0, 6);
     if ((d0 & 255) >= MBT_I4x4) return;
-    struct { int w, h; } a = {aw, ah};
-    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
-    const uint32_t ysz = (uint32_t)W16 * H16, csz = (uint32_t)CW * CH;
+    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2, CP = a.cpitch;
+    const uint32_t ysz = (uint32_t)W16 * H16, csz = (uint32_t)CP * CH;
     const int mbx = mb % a.w, mby = mb / a.w;
-    int need = 0;
+    // the in-launch producer of slot rs (or -1)
+    auto producer = [&](uint32_t rs) -> int {
+        for (int k = 0; k < D.n; k++)
+            if (((D.slots >> (k * 8)) & 255) == rs) return p - (k + 1) * a.S;
+        return -1;
+    };
+    bool ok = true;
     {   // luma: lane -> block lb, window rows lsub + 4k (mc_issue)
         const int lb = lane >> 2, lsub = lane & 3;
         const uint32_t mvl = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + lb) << 2, (int)v0);
-        if (const uint32_t rs = (refs >> ((lb >> 2) * 8)) & 255; rs < 32 && ((smask >> rs) & 1)) {
+        const int pk = producer((refs >> ((lb >> 2) * 8)) & 255);
+        if (pk >= 0) {
             const int mvx = (int)(int16_t)(mvl & 0xFFFF), mvy = (int)(int16_t)(mvl >> 16);
             const int x0 = clip3(0, W16 - 12, (mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2) & ~3);
             const int y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
-#pragma unroll
             for (int k = 0; k < 3; k++) {
                 const int y = clip3(0, H16 - 1, y0 + min(lsub + 4 * k, 8));
-                need = max(need, chk_line_need((uint32_t)(y * W16 + x0), 12, ysz, csz, W16, CW, a.h));
+                ok &= chk_access(a, pk, (uint32_t)(y * W16 + x0), 12, 0, W16, H16, W16, 16, 16);
             }
         }
     }
     {   // chroma: lane -> block cb, component
         const int cb = (lane & 31) >> 1, ccomp = lane & 1;
         const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
-        if (const uint32_t rs = (refs >> ((cb >> 2) * 8)) & 255; rs < 32 && ((smask >> rs) & 1)) {
+        const int pk = producer((refs >> ((cb >> 2) * 8)) & 255);
+        if (pk >= 0) {
             const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
             const int x0 = clip3(0, CW - 8, (mbx * 8 + blk_x(cb) * 2 + (cmx >> 3)) & ~3);
             const int y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3);
-#pragma unroll
+            const uint32_t pb = ysz + (uint32_t)ccomp * csz;
             for (int wy = 0; wy < 3; wy++) {
                 const int y = clip3(0, CH - 1, y0 + wy);
-                need = max(need, chk_line_need(ysz + (uint32_t)ccomp * csz + (uint32_t)(y * CW + x0), 8, ysz, csz, W16, CW, a.h));
+                ok &= chk_access(a, pk, pb + (uint32_t)(y * CP + x0), 8, pb, CP, CH, CW, 8, 8);
             }
         }
     }
-    if (__builtin_amdgcn_ballot_w64(need > known) != 0 && lane == 0) atomicOr((unsigned *)perr, CHK_REFROW);
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0 && lane == 0) atomicOr(a.err + p, CHK_REFROW);
 }
 
 // MC waves of one row (picture p, MB row r): MB c0 first (c0 = the wave's
@@ -2063,37 +2143,27 @@ __device__ __attribute__((noinline)) void chk_ref_rows(int aw, int ah, g_u32 *pe
 #endif
 template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK, bool DEP3>
 __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing<RK> &R,
-                                       const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me)
+                                       const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me,
+                                       lds_u2 *pc)
 {
     const PicDesc pd = a.pics[p];
     const uint32_t *recrow = (const uint32_t *)(a.rec + pd.rec_base + r * a.w);
     DepState D;
-    D.n = 0;
-#ifdef STUDY_NEAR
-    D.cap = min(r + 3, a.h);
-#endif
-    if (a.P > 1) {
-        const int S = a.S, j = p / S;
-        if (DEP3) {
-            D.slot = 0; D.pic = 0; D.known = 0;
-            if (j > 0) {
-                D.n = 1;
-                D.pic = p - S;
-                uint32_t m = 0;
+    D.n = 0; D.slots = 0;
+    if (DEP3 && a.P > 1) {
+        // the earlier steps of this stream in the launch (at most
+        // H264MI_MAX_STEPS - 1) and the slots their pictures write
+        const int j = p / a.S;
+        uint32_t m = 0;
 #pragma unroll
-                for (int k = 1; k < 4; k++)      // 4: H264MI_MAX_STEPS
-                    if (k <= j) m |= 1u << (a.pics[p - k * S].cur_slot & 31);
-                D.slot = __builtin_amdgcn_readfirstlane(m);
-            }
-        } else if (j >= 1) {
-            D.pic = p - S;
-            D.slot = __builtin_amdgcn_readfirstlane(a.pics[p - S].cur_slot);
-            D.known = 0;
-            D.n = 1;
-        }
+        for (int k = 1; k < 4; k++)
+            if (k <= j) m |= (a.pics[p - k * a.S].cur_slot & 255) << ((k - 1) * 8);
+        D.n = __builtin_amdgcn_readfirstlane(min(j, 3));
+        D.slots = __builtin_amdgcn_readfirstlane(m);
     }
     // the next MB of this wave: the row counter's (dynamic) or c + NMC.  The
-    // claim is one lane's LDS atomic, exec = lane 0 inside the asm (no
+    // claim is one lane's LDS atomic, exec = lane 0 inside the asm, its
+    // result read from lane 0 by v_readlane whatever the caller's exec (no
     // divergent branch in the IR feeding the index; an atomic from all 64
     // lanes on one address serialises: +35 % per launch).  The static walk
     // runs the same block with a zero increment: its wait and compiler
@@ -2110,7 +2180,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
                      "ds_add_rtn_u32 %2, %3, %4\n\t"
                      "s_waitcnt lgkmcnt(0)\n\t"
                      "s_mov_b64 exec, %1\n\t"
-                     "v_readfirstlane_b32 %0, %2"
+                     "v_readlane_b32 %0, %2, 0"
                      : "=s"(u), "=&s"(saved), "=&v"(tmp) : "v"(addr), "v"(inc) : "memory");
         return dyn ? u : c + NMC;
     };
@@ -2118,8 +2188,8 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     int c = c0;
     uint32_t v0 = c < a.w ? recrow[(size_t)c * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
-    if (c < a.w && D.n) dep_wait<DEP3>(a, p, v0, lane, D);
-    if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, DEP3 ? D.slot : 1u << (D.slot & 31), D.known);
+    if (DEP3 && c < a.w && D.n) dep_wait<CHK>(a, p, r * a.w + c, v0, lane, D, pc);
+    if (DEP3 && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
     if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
 
     const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
@@ -2194,8 +2264,8 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         }
         c = cn;
         v0 = nv0;
-        if (c < a.w && D.n) dep_wait<DEP3>(a, p, v0, lane, D);
-        if (CHK && c < a.w && D.n) chk_ref_rows(a.w, a.h, (g_u32 *)(a.err + p), r * a.w + c, v0, lane, DEP3 ? D.slot : 1u << (D.slot & 31), D.known);
+        if (DEP3 && c < a.w && D.n) dep_wait<CHK>(a, p, r * a.w + c, v0, lane, D, pc);
+        if (DEP3 && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
         if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
     }
 }
@@ -2223,7 +2293,10 @@ struct WgppLds {
     static constexpr size_t offM = a16(sizeof(PPLds) * RPW);
     static constexpr size_t offR = offM + a16(sizeof(McScratch) * RPW * NMC);
     static constexpr size_t offX = offR + a16(sizeof(MbRing<RK>) * RPW);
-    static size_t bytes(int w) { return offX + (size_t)(RPW - 1) * w * 256; }
+    static size_t bytes(int w, bool dep3 = false)
+    {
+        return offX + (size_t)(RPW - 1) * w * 256 + (dep3 ? 3 * PC_ROWS * 8 : 0);
+    }
 };
 #ifndef WGPP_WAVES_PER_EU
 #define WGPP_WAVES_PER_EU 4
@@ -2238,9 +2311,9 @@ struct WgppLds {
 #define WGPP2_WAVES_PER_EU 4
 #endif
 
-// DEP3: launches of three or more steps (dep_wait's slot mask and the
-// chained row tags); a separate instance, so that the code of launches of
-// one or two steps stays as it was measured
+// DEP3: frame-pipelined launches (two or more steps per stream): the row
+// waves publish store progress and the MC waves wait on it (dep_wait); a
+// separate instance, so that single-step launches carry none of it
 template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false, bool DEP3 = false>
 __global__ __launch_bounds__(64 * (NMC + 2) * RPW)
 __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : WGPP2_WAVES_PER_EU))) void k_wgpp(ReconArgs a)
@@ -2271,6 +2344,10 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     }
     for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
         L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
+    // frame-pipelined launches: the producers' progress cache (dep_wait)
+    lds_u2 *const pc = (lds_u2 *)(__attribute__((address_space(3))) unsigned char *)(wg_lds + Lay::offX);
+    if (DEP3)
+        for (int e = threadIdx.x; e < 3 * PC_ROWS; e += 64 * (NMC + 2) * RPW) pc[e] = 0ull;
     if (RPW > 1)        // granule tags from an earlier workgroup on this CU must not match
         for (int e = threadIdx.x; e < (RPW - 1) * a.w * 32; e += 64 * (NMC + 2) * RPW) lmbx[e] = 0;
     __syncthreads();
@@ -2288,46 +2365,22 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     unsigned long long *const me = mel ? lmbx + q * W32 : a.mbx + ((size_t)p * a.h + r) * W32;
     if (wid < 2) {
         __builtin_amdgcn_s_setprio(3);
-        if (!upl && !mel) row_pp<PROF, false, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
+        if (DEP3) row_pp<PROF, false, false, RK, CHK, true>(a, p, r, L[q], wid, lane, &R[q], up, me, j + 1 < a.P);
+        else if (!upl && !mel) row_pp<PROF, false, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else if (!upl) row_pp<PROF, false, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else if (mel) row_pp<PROF, true, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else row_pp<PROF, true, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         // row finished: progress for the tail workgroups' start
         if (wid == 0 && lane == 0 && a.rows_done)
             __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (j + 1 < a.P) {
-            // a later step of this launch may read this picture: once both
-            // row waves' frame stores have completed, the second wave writes
-            // the XCD's L2 back and tags the row done
-            if (DEP3 && j > 0) {
-                // chained tags (dep_wait): with three or more steps, row r of
-                // step j - 1 first -- normally long done, this picture's rows
-                // having waited on it
-                const uint32_t *pd = a.done + (size_t)(p - S) * a.h + r;
-                unsigned spins = 0;
-                while (__builtin_amdgcn_readfirstlane(ld_sc1_u32(pd)) != a.epoch) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); break; }
-                }
-            }
-            drain_vm();
-            int last = 0;
-            if (lane == 0) last = __hip_atomic_fetch_add(&L[q].fin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            last = __builtin_amdgcn_readfirstlane(last);
-            if (last == 1 && lane == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_sc1_u32(a.done + (size_t)p * a.h + r, a.epoch);
-            }
-        }
         return;
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
     McScratch &Mw = M[q * NMC + wid - 2];
-    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
-    else mc_row<NMC, PROF, true, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me);
+    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    else mc_row<NMC, PROF, true, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
 }
 template __global__ void k_wgpp<3, false, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 1>(ReconArgs);

@@ -42,65 +42,20 @@ static int cap_configure(void *vctx, int w_mbs, int h_mbs, int nslots)
     return 0;
 }
 
-/* Last MB row of a w x h-MB I420 slot that the 128-B lines holding bytes
- * [first, last] of the slot touch.  Lines run in address order, so that is
- * the row at the end of the last byte's line -- except for a line that
- * crosses the Cb/Cr boundary (w * h odd), which holds Cb's last row even
- * where the bytes read are Cr's top row.  The kernel's frame-pipelined
- * dependency wait relies on it (a line is read only once all its rows are
- * final). */
-static int line_rows(long long first, long long last, int W16, int H16, int h)
+/* Test hooks (H264MI_CHECK_INJECT*, H264MI_DEBUG_FLAG_PICTURE) break a hand-off
+ * or force a device flag on purpose; the library honours them only when
+ * H264MI_TEST=1 is set as well, so that a shipped decoder never produces wrong
+ * pictures because of one stray environment variable (tests/test_knobs.py). */
+int h264mi_test_hooks(void)
 {
-    const long long ysz = (long long)W16 * H16, csz = ysz >> 2, bnd = ysz + csz;
-    const long long le = last | 127;
-    int r;
-    if ((bnd & 127) && (first & ~127ll) <= (bnd & ~127ll) && le >= bnd) return h - 1;
-    if (le < ysz) return (int)(le / W16) >> 4;
-    r = (int)((le < bnd ? le - ysz : le - bnd) / (W16 / 2)) >> 3;
-    return r < h - 1 ? r : h - 1;
-}
-
-static int clampi(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
-
-/* per inter MB and 8x8 partition: the last reference-slot MB row its MC
- * reads (luma 9 rows x 12 bytes per 4x4 block, chroma 3 rows x 8 bytes per
- * 2x2 block and plane, windows clamped as in the kernel's mc_issue) */
-static void set_ref_rows(MbRec *recs, int w, int h)
-{
-    /* test hook of the dependency checker (tests/test_depcheck.py): record
-     * this many rows fewer than the loads need, which the CHK kernels must
-     * report (CHK_REFROW) */
-    const char *inj = getenv("H264MI_CHECK_INJECT_REFROWS");
-    const int short_by = inj ? atoi(inj) : 0;
-    static const int bx[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
-    static const int by[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
-    const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2;
-    for (int mb = 0; mb < w * h; mb++) {
-        MbRec *r = &recs[mb];
-        if (r->type != MBT_INTER && r->type != MBT_SKIP) continue;
-        const int mbx = mb % w, mby = mb / w;
-        uint16_t rows[4] = {0, 0, 0, 0};
-        for (int b = 0; b < 16; b++) {
-            const int mvx = r->mv[b][0], mvy = r->mv[b][1];
-            const int lx0 = mbx * 16 + bx[b] * 4 + (mvx >> 2) - 2;
-            const int lax = clampi(0, W16 - 12, lx0 & ~3);
-            const int ly = clampi(0, H16 - 1, mby * 16 + by[b] * 4 + (mvy >> 2) - 2 + 8);
-            int n = line_rows((long long)ly * W16 + lax, (long long)ly * W16 + lax + 11, W16, H16, h);
-            const int cx0 = mbx * 8 + bx[b] * 2 + (mvx >> 3);
-            const int cax = clampi(0, CW - 8, cx0 & ~3);
-            const int cy0 = mby * 8 + by[b] * 2 + (mvy >> 3);
-            for (int comp = 0; comp < 2; comp++)
-                for (int wy = 0; wy < 3; wy++) {
-                    const long long o = (long long)W16 * H16 + (long long)comp * CW * CH +
-                                        (long long)clampi(0, CH - 1, cy0 + wy) * CW + cax;
-                    const int nc = line_rows(o, o + 7, W16, H16, h);
-                    if (nc > n) n = nc;
-                }
-            if (n > rows[b >> 2]) rows[b >> 2] = (uint16_t)n;
-        }
-        for (int q = 0; q < 4 && short_by > 0; q++) rows[q] = (uint16_t)(rows[q] > short_by ? rows[q] - short_by : 0);
-        memcpy(r->i4, rows, 8);
+    static int cached = -1;
+    int v = __atomic_load_n(&cached, __ATOMIC_RELAXED);
+    if (v < 0) {
+        const char *t = getenv("H264MI_TEST");
+        v = t && atoi(t) == 1;
+        __atomic_store_n(&cached, v, __ATOMIC_RELAXED);
     }
+    return v;
 }
 
 static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
@@ -139,7 +94,6 @@ static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
     p->n_intra = pb->n_intra;
     p->n_coded = pb->n_coded_blocks;
     memcpy(c->recs + c->nrec, pb->rec, sizeof(MbRec) * nmbs);
-    set_ref_rows(c->recs + c->nrec, c->w, c->h);
     p->ref_line_bytes = ref_line_bytes(c->recs + c->nrec, c->w, c->h);
     if (pb->ncoef) memcpy(c->coefs + c->ncoef * 16, pb->coef, (size_t)pb->ncoef * 32);
     c->nrec += nmbs;
@@ -153,12 +107,13 @@ static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
  * windows are mc_issue's (recon_kernels.hip): per 4x4 luma block 9 rows of
  * 12 bytes from (x0 & ~3) clamped to [0, W16 - 12], per 2x2 chroma block and
  * component 3 rows of 8 bytes from (x0 & ~3) clamped to [0, CW - 8], rows
- * clamped to the plane.  Slots are frame_bytes = 384 B per MB apart, a
- * multiple of 128, so line ids never straddle slots. */
+ * clamped to the plane, chroma rows CP = H264MI_CPITCH apart.  Slots are
+ * H264MI_SLOT_BYTES apart, a multiple of 128, so line ids never straddle
+ * slots. */
 static uint64_t ref_line_bytes(const MbRec *rec, int w, int h)
 {
-    const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2;
-    const size_t lines = (size_t)w * h * 3;             /* 384 B per MB / 128 */
+    const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2, CP = H264MI_CPITCH(w);
+    const size_t lines = H264MI_SLOT_BYTES(w, h) / 128;
     int maxslot = -1;
     for (int i = 0; i < w * h; i++)
         if (rec[i].type == MBT_INTER || rec[i].type == MBT_SKIP)
@@ -197,7 +152,7 @@ static uint64_t ref_line_bytes(const MbRec *rec, int w, int h)
                 for (int k = 0; k < 3; k++) {
                     int y = cy0 + k;
                     y = y < 0 ? 0 : y > CH - 1 ? CH - 1 : y;
-                    MARK(slot, (size_t)W16 * H16 + (size_t)comp * CW * CH + (size_t)y * CW + cax, 8);
+                    MARK(slot, (size_t)W16 * H16 + (size_t)comp * CP * CH + (size_t)y * CP + cax, 8);
                 }
         }
     }

@@ -18,6 +18,9 @@
 extern "C" {
 #endif
 
+/* 1 when H264MI_TEST=1: the test hooks are honoured (capture.c) */
+int h264mi_test_hooks(void);
+
 /* Reconstruction backend interface (the device boundary). */
 typedef struct H264Backend {
     void *ctx;

@@ -397,8 +397,7 @@ static int hb_prefetch(void *vctx, int slot, uint8_t *dst)
     HIPCHECK(hipSetDevice(h264mi_engine_device(e)));
     std::unique_lock<std::mutex> l;
     if (c->sh) l = std::unique_lock<std::mutex>(c->sh->mu);
-    HIPCHECK(hipMemcpyAsync(dst, h264mi_engine_frame_ptr(e, c->lane, slot), h264mi_engine_frame_bytes(e), hipMemcpyDeviceToHost,
-                            engine_stream(e)));
+    if (engine_copy_out(e, c->lane, slot, dst, engine_stream(e))) return -1;
     if (c->sh) HIPCHECK(hipEventRecord(c->ev_last, engine_stream(e)));
     c->pref[slot] = dst;
     c->enq++;
@@ -440,8 +439,7 @@ static int hb_read(void *vctx, int slot, uint8_t *dst)
         if (slot < 0 || slot >= c->nslots) return -1;
         if (c->pref[slot] != dst) {
             std::lock_guard<std::mutex> l(c->sh->mu);
-            HIPCHECK(hipMemcpyAsync(dst, h264mi_engine_frame_ptr(c->e, c->lane, slot), h264mi_engine_frame_bytes(c->e),
-                                    hipMemcpyDeviceToHost, engine_stream(c->e)));
+            if (engine_copy_out(c->e, c->lane, slot, dst, engine_stream(c->e))) return -1;
             HIPCHECK(hipEventRecord(c->ev_last, engine_stream(c->e)));
         }
         return slot_flagged(c, slot);
@@ -464,8 +462,8 @@ static int hb_read_rgba(void *vctx, int slot, uint8_t *dst)
         if (!c->d_rgba) HIPCHECK(hipMalloc(&c->d_rgba, bytes));
         {
             std::lock_guard<std::mutex> l(c->sh->mu);
-            if (h264mi_yuv2rgba_device(h264mi_engine_frame_ptr(e, c->lane, slot), c->d_rgba, w * 16, h * 16, 1, 0,
-                                       0, engine_stream(e)))
+            if (h264mi_yuv2rgba_device_pitch(h264mi_engine_frame_ptr(e, c->lane, slot), c->d_rgba, w * 16, h * 16,
+                                             h264mi_engine_chroma_pitch(e), 1, 0, 0, engine_stream(e)))
                 return -1;
             HIPCHECK(hipMemcpyAsync(dst, c->d_rgba, bytes, hipMemcpyDeviceToHost, engine_stream(e)));
             HIPCHECK(hipEventRecord(c->ev_last, engine_stream(e)));
@@ -549,13 +547,13 @@ static int hb_copy(void *vctx, int dst, int src)
     if (c->sh) {
         std::lock_guard<std::mutex> l(c->sh->mu);
         HIPCHECK(hipMemcpyAsync(h264mi_engine_frame_ptr(c->e, c->lane, dst), h264mi_engine_frame_ptr(c->e, c->lane, src),
-                                h264mi_engine_frame_bytes(c->e), hipMemcpyDeviceToDevice, engine_stream(c->e)));
+                                engine_slot_bytes(c->e), hipMemcpyDeviceToDevice, engine_stream(c->e)));
         HIPCHECK(hipEventRecord(c->ev_last, engine_stream(c->e)));
         return 0;
     }
     if (h264mi_engine_sync(c->e)) return -1;
     HIPCHECK(hipMemcpy(h264mi_engine_frame_ptr(c->e, 0, dst), h264mi_engine_frame_ptr(c->e, 0, src),
-                       h264mi_engine_frame_bytes(c->e), hipMemcpyDeviceToDevice));
+                       engine_slot_bytes(c->e), hipMemcpyDeviceToDevice));
     return 0;
 }
 
@@ -598,7 +596,7 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     }
     HipBackendCtx *c = (HipBackendCtx *)calloc(1, sizeof(HipBackendCtx));
     c->device = device;
-    const char *ff = getenv("H264MI_DEBUG_FLAG_PICTURE");
+    const char *ff = h264mi_test_hooks() ? getenv("H264MI_DEBUG_FLAG_PICTURE") : NULL;
     c->force_flag_at = ff && atoi(ff) > 0 ? (unsigned)atoi(ff) : 0;
     be.ctx = c;
     be.configure = hb_configure;

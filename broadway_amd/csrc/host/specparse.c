@@ -1,3 +1,4 @@
+#define _GNU_SOURCE
 /* Speculative parallel slice-data parsing (host throughput of the end-to-end
  * path; no reference counterpart -- the reference parses one NAL per call).
  *
@@ -118,9 +119,22 @@ static void run_job(SpecPool *sp, SpecJob *j)
     j->ok = 1;
 }
 
+/* host CPU attribution (h264mi_host_thread_stats): the speculative-parse
+ * workers' whole-thread CPU, added when each worker exits */
+static unsigned long long g_worker_cpu_ns, g_workers_started;
+
+int h264mi_host_thread_stats(double *spec_worker_cpu_s, unsigned long long *workers_started)
+{
+    if (spec_worker_cpu_s) *spec_worker_cpu_s = 1e-9 * (double)__atomic_load_n(&g_worker_cpu_ns, __ATOMIC_RELAXED);
+    if (workers_started) *workers_started = __atomic_load_n(&g_workers_started, __ATOMIC_RELAXED);
+    return 0;
+}
+
 static void *worker(void *arg)
 {
     SpecPool *sp = (SpecPool *)arg;
+    pthread_setname_np(pthread_self(), "h264mi-spec");
+    __atomic_add_fetch(&g_workers_started, 1, __ATOMIC_RELAXED);
     pthread_mutex_lock(&sp->mu);
     for (;;) {
         while (!sp->stop && sp->next < sp->njobs && sp->jobs[sp->order[sp->next]].started) sp->next++;
@@ -142,6 +156,7 @@ static void *worker(void *arg)
         pthread_cond_broadcast(&sp->cv_done);
     }
     pthread_mutex_unlock(&sp->mu);
+    __atomic_add_fetch(&g_worker_cpu_ns, (unsigned long long)(thread_cpu() * 1e9), __ATOMIC_RELAXED);
     return NULL;
 }
 

@@ -13,7 +13,14 @@
  * first input.  -Acpus (a cpulist: "0-7,16,18") pins the process and every
  * thread it starts (parse workers included) to those host cores before
  * anything else runs -- one GPU's decoder processes on cores of that GPU's
- * NUMA node (bench.py end_to_end); the GPU is H264MI_DEVICE (default 0). */
+ * NUMA node (bench.py end_to_end); the GPU is H264MI_DEVICE (default 0).
+ * -G (start gate): after its HIP warm-up the process prints "ready" and
+ * waits for one byte on stdin before its timed loop, so that a driver can
+ * start several processes' loops together; -T then also prints the loop's
+ * CLOCK_MONOTONIC start / end (comparable across the host's processes) and
+ * the host CPU of the loop by thread: the decoding threads, the
+ * speculative-parse workers, and every other thread of the process (HIP
+ * runtime threads) from /proc/self/task. */
 #define _GNU_SOURCE
 #include "../../../include/h264mi.h"
 
@@ -23,6 +30,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <dirent.h>
+#include <unistd.h>
 #include <sys/resource.h>
 
 static double now_s(void)
@@ -52,6 +61,42 @@ static int parse_cpulist(const char *s, cpu_set_t *set)
         s = e;
     }
     return n ? 0 : -1;
+}
+
+/* CPU seconds (user + system) of every live thread of this process but
+ * `skip` (whose CPU is counted elsewhere), from /proc/self/task/<tid>/stat;
+ * *n: how many */
+static double other_threads_cpu(pid_t skip, int *n)
+{
+    DIR *d = opendir("/proc/self/task");
+    if (!d) return -1.0;
+    const double tick = 1.0 / (double)sysconf(_SC_CLK_TCK);
+    double sum = 0.0;
+    int k = 0;
+    struct dirent *de;
+    while ((de = readdir(d)) != NULL) {
+        if (de->d_name[0] < '0' || de->d_name[0] > '9') continue;
+        const pid_t tid = (pid_t)atoi(de->d_name);
+        if (tid == skip) continue;
+        char path[64], buf[1024];
+        snprintf(path, sizeof(path), "/proc/self/task/%d/stat", (int)tid);
+        FILE *f = fopen(path, "r");
+        if (!f) continue;
+        const size_t m = fread(buf, 1, sizeof(buf) - 1, f);
+        fclose(f);
+        buf[m] = 0;
+        const char *p = strrchr(buf, ')');      /* comm may hold spaces */
+        if (!p) continue;
+        unsigned long ut = 0, st = 0;
+        /* fields after comm: state(3) ... utime(14) stime(15) */
+        if (sscanf(p + 2, "%*c %*d %*d %*d %*d %*d %*u %*u %*u %*u %*u %lu %lu", &ut, &st) == 2) {
+            sum += (double)(ut + st) * tick;
+            k++;
+        }
+    }
+    closedir(d);
+    if (n) *n = k;
+    return sum;
 }
 
 static double g_t[4];   /* parse, submit, wait, copy (H264SwDecGetTiming), summed over instances */
@@ -153,7 +198,7 @@ int main(int argc, char **argv)
 {
     const char *out = NULL;
     const char *ins[256];
-    int nin = 0, no_reorder = 0, timing = 0, reps = 1, share = 0;
+    int nin = 0, no_reorder = 0, timing = 0, reps = 1, share = 0, gate = 0;
     const char *cpus = NULL;
     for (int i = 1; i < argc; i++) {
         if (!strncmp(argv[i], "-O", 2)) out = argv[i] + 2;
@@ -162,10 +207,11 @@ int main(int argc, char **argv)
         else if (!strncmp(argv[i], "-r", 2)) reps = atoi(argv[i] + 2);
         else if (!strncmp(argv[i], "-S", 2)) share = atoi(argv[i] + 2);
         else if (!strncmp(argv[i], "-A", 2)) cpus = argv[i] + 2;
+        else if (!strcmp(argv[i], "-G")) gate = 1;
         else if (nin < 256) ins[nin++] = argv[i];
     }
     if (!nin || reps < 1) {
-        fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] [-SN] [-Acpus] in.h264 [in2.h264 ...]\n");
+        fprintf(stderr, "usage: h264mi_dec [-R] [-Oout] [-rN] [-T] [-SN] [-Acpus] [-G] in.h264 [in2.h264 ...]\n");
         return 2;
     }
     if (cpus) {
@@ -191,8 +237,21 @@ int main(int argc, char **argv)
         if (H264SwDecInit(&warm, 0) != H264SWDEC_OK) { fprintf(stderr, "DECODER INITIALIZATION FAILED\n"); return 1; }
         H264SwDecRelease(warm);
     }
+    if (gate) {
+        /* start gate: every process of the run warmed up, released together */
+        printf("ready\n");
+        fflush(stdout);
+        if (getchar() == EOF) { fprintf(stderr, "start gate closed\n"); return 2; }
+    }
     int pics = 0, errs = 0;
     struct rusage ru0, ru1;
+    double w0 = 0.0, w1 = 0.0;
+    h264mi_host_thread_stats(&w0, NULL);
+    const pid_t main_tid = (pid_t)getpid();
+    int nother0 = 0, nother1 = 0;
+    const double oth0 = other_threads_cpu(main_tid, &nother0);
+    struct timespec mc0, mc1;
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &mc0);
     getrusage(RUSAGE_SELF, &ru0);
     const double t0 = now_s();
     if (nin == 1) {
@@ -205,6 +264,9 @@ int main(int argc, char **argv)
     }
     const double t1 = now_s();
     getrusage(RUSAGE_SELF, &ru1);
+    clock_gettime(CLOCK_THREAD_CPUTIME_ID, &mc1);
+    const double oth1 = other_threads_cpu(main_tid, &nother1);
+    h264mi_host_thread_stats(&w1, NULL);
     if (fo) fclose(fo);
     for (int i = 0; i < nin; i++) {
         if (jobs[i].fail) { fprintf(stderr, "DECODER INITIALIZATION FAILED\n"); return 1; }
@@ -220,6 +282,16 @@ int main(int argc, char **argv)
                            (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec);
         printf("cpu_seconds %.6f\n", cpu);
         printf("cpu_decode_threads_seconds %.6f\n", g_job_cpu);
+        /* by thread: the spec workers (exited ones, library counter), the
+         * main thread when it is not a decoding thread, the threads alive
+         * at the end of the loop other than main (HIP runtime threads, live
+         * spec workers of shared instances) -- their CPU over the loop */
+        const double main_cpu = (double)(mc1.tv_sec - mc0.tv_sec) + 1e-9 * (double)(mc1.tv_nsec - mc0.tv_nsec);
+        printf("cpu_spec_workers_seconds %.6f\n", w1 - w0);
+        printf("cpu_main_thread_seconds %.6f\n", main_cpu);
+        if (oth0 >= 0 && oth1 >= 0)
+            printf("cpu_other_live_threads_seconds %.6f\nother_live_threads %d\n", oth1 - oth0, nother1);
+        printf("t_start_mono %.6f\nt_end_mono %.6f\n", t0, t1);
         printf("cpu_sys_seconds %.6f\n", (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec));
         unsigned long long nb = 0, np = 0;
         h264mi_share_stats(0, &nb, &np);

@@ -86,7 +86,12 @@ class Engine:
         self._h = self._L.h264mi_engine_create(device, w_mbs, h_mbs, nstreams, nslots)
         if not self._h:
             raise RuntimeError("h264mi_engine_create failed (no HIP device?)")
-        self.frame_bytes = self._L.h264mi_engine_frame_bytes(self._h)
+        self.frame_bytes = self._L.h264mi_engine_frame_bytes(self._h)       # packed I420 (read's output)
+        if hasattr(self._L, "h264mi_engine_slot_bytes"):
+            self.slot_bytes = self._L.h264mi_engine_slot_bytes(self._h)     # device slot stride
+            self.chroma_pitch = self._L.h264mi_engine_chroma_pitch(self._h) # H264MI_CPITCH
+        else:                                                               # an older tree's A/B build: packed slots
+            self.slot_bytes, self.chroma_pitch = self.frame_bytes, w_mbs * 8
 
     def decode(self, streams: Sequence[int], pics: Sequence[CapturedPicture]) -> None:
         n = len(pics)
@@ -179,7 +184,8 @@ class Engine:
         return int(self._L.h264mi_pointer_device(p))
 
     def frame_ptr(self, stream: int, slot: int) -> int:
-        """Device address of a frame slot (I420, frame_bytes)."""
+        """Device address of a frame slot (I420, chroma rows chroma_pitch
+        bytes apart; slots slot_bytes apart)."""
         return int(self._L.h264mi_engine_frame_ptr(self._h, stream, slot))
 
     def sync(self) -> None:

@@ -140,6 +140,10 @@ int h264mi_set_share(int lanes);
 /* batches / pictures launched by device's shared engine; returns the
  * instances attached (0: none) */
 int h264mi_share_stats(int device, unsigned long long *batches, unsigned long long *pictures);
+/* diagnostics, host CPU attribution of this process: the CPU seconds of the
+ * speculative-parse worker threads that have exited (threads named
+ * "h264mi-spec"), and how many were started */
+int h264mi_host_thread_stats(double *spec_worker_cpu_s, unsigned long long *workers_started);
 
 /* ---------------------------------------------------------------------- */
 /* 2. Broadway glue (reference Decoder/src/Decoder.c:44-185, make.py:39)   */
@@ -244,6 +248,10 @@ int  h264mi_engine_read_rgba(h264mi_engine *e, int stream, int slot, uint8_t *ds
  * d_rgba + k * out_stride; asynchronous on `hip_stream` (NULL: null stream) */
 int  h264mi_yuv2rgba_device(const void *d_i420, void *d_rgba, int width, int height, int npics,
                             size_t in_stride, size_t out_stride, void *hip_stream);
+/* the same with the chroma rows cpitch bytes apart (an engine slot:
+ * h264mi_engine_chroma_pitch; the packed form above is cpitch = width / 2) */
+int  h264mi_yuv2rgba_device_pitch(const void *d_i420, void *d_rgba, int width, int height, int cpitch, int npics,
+                                  size_t in_stride, size_t out_stride, void *hip_stream);
 int  h264mi_engine_sync(h264mi_engine *e);
 /* number of (launch, picture) slots flagged since the last call: residual
  * range errors (reference transform.c:181) or a bounded wait that expired;
@@ -277,11 +285,17 @@ int  h264mi_engine_timing_list(h264mi_engine *e, double *us, int cap);
  * of its phases, then 4 u64 per MB (chain stamps); enable != 0 allocates and
  * switches to the profiling kernel, out != NULL copies the last launch */
 int  h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long long *out, size_t n);
-void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);          /* device pointer */
+/* device pointer of a frame slot: I420 with the chroma rows padded to
+ * h264mi_engine_chroma_pitch bytes (H264MI_CPITCH, include/h264mi_records.h),
+ * slots h264mi_engine_slot_bytes apart */
+void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot);
 /* diagnostics: name of the last batch's reconstruction kernel ("k_wgpp";
  * "" before the first batch) */
 const char *h264mi_engine_kernel(h264mi_engine *e);
+/* packed I420 bytes of one picture (h264mi_engine_read's output) */
 size_t h264mi_engine_frame_bytes(h264mi_engine *e);
+size_t h264mi_engine_slot_bytes(h264mi_engine *e);
+int    h264mi_engine_chroma_pitch(h264mi_engine *e);
 
 /* MB-record capture: run the host parser over a whole Annex-B stream and keep
  * every picture's record batch (the §8d "pre-parsed MB-record batches"). */

@@ -70,11 +70,8 @@ typedef struct MbRec {
     int8_t   offB;      /* FilterOffsetB */
     uint32_t cbits;     /* coded-block mask, see above */
     uint32_t coef;      /* first coefficient block index */
-    uint8_t  i4[8];     /* I_4x4: Intra4x4PredMode, 4 bits per block, z-scan.
-                           Inter (MBT_INTER / MBT_SKIP) in frame-pipelined batches: four
-                           uint16 (little endian), per 8x8 partition the last MB row of
-                           its reference slot that a 128-B line read by its motion
-                           compensation touches (h264mi_capture fills it) */
+    uint8_t  i4[8];     /* I_4x4: Intra4x4PredMode, 4 bits per block, z-scan (unused
+                           by inter MBs) */
     uint8_t  ref[4];    /* DPB slot per 8x8 partition (inter only) */
     int16_t  mv[16][2]; /* per 4x4 block, z-scan, quarter-pel (x, y) */
     uint16_t slice;     /* slice id within the picture */
@@ -103,5 +100,18 @@ typedef struct PicDesc {
 } PicDesc;
 
 enum { PD_INTRA_HEAVY = 4 };
+
+/* Device frame-slot layout (the engine's HBM frame pool): I420, luma rows
+ * w*16 bytes apart, then the Cb and Cr planes with their rows padded to a
+ * multiple of 128 bytes (the L2 line), so that no 128-B line holds bytes of
+ * two chroma rows -- the frame-pipelined launches hand reference samples
+ * from one picture to the next at (MB row, MB column) granularity and read a
+ * line only once every byte of it is final (recon_kernels.hip dep_wait).
+ * 1080p: 1024-byte chroma rows for 960 samples; 720p and 2160p: no padding.
+ * What leaves the device (h264mi_engine_read, the H264SwDec output) is packed
+ * I420, w*16 * h*16 * 3/2 bytes. */
+#define H264MI_CPITCH(w_mbs) ((((w_mbs) * 8) + 127) & ~127)
+#define H264MI_SLOT_BYTES(w_mbs, h_mbs) \
+    ((size_t)(w_mbs) * 16 * (h_mbs) * 16 + 2 * (size_t)H264MI_CPITCH(w_mbs) * (h_mbs) * 8)
 
 #endif

@@ -133,6 +133,16 @@ extern "C" void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot)
     return oracle_ctx_frame(e->lane[stream], slot);
 }
 extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? (size_t)e->w * e->h * 384 : 0; }
+// the null device keeps its slots packed (chroma pitch = w * 8)
+extern "C" int h264mi_engine_chroma_pitch(h264mi_engine *e) { return e ? e->w * 8 : 0; }
+size_t engine_slot_bytes(const h264mi_engine *e) { return (size_t)e->w * e->h * 384; }
+int engine_copy_out(h264mi_engine *e, int stream, int slot, uint8_t *dst, hipStream_t st)
+{
+    void *p = h264mi_engine_frame_ptr(e, stream, slot);
+    if (!p) return -1;
+    memcpy(dst, p, h264mi_engine_frame_bytes(e));
+    return 0;
+}
 extern "C" int h264mi_engine_sync(h264mi_engine *e) { return e ? 0 : -1; }
 extern "C" int h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_t *dst)
 {
@@ -144,6 +154,11 @@ extern "C" int h264mi_engine_read(h264mi_engine *e, int stream, int slot, uint8_
 extern "C" int h264mi_engine_read_rgba(h264mi_engine *e, int stream, int slot, uint8_t *dst) { return -1; }
 extern "C" int h264mi_yuv2rgba_device(const void *d_i420, void *d_rgba, int width, int height, int npics,
                                       size_t in_stride, size_t out_stride, void *stream)
+{
+    return -1;
+}
+extern "C" int h264mi_yuv2rgba_device_pitch(const void *d_i420, void *d_rgba, int width, int height, int cpitch,
+                                            int npics, size_t in_stride, size_t out_stride, void *stream)
 {
     return -1;
 }

@@ -4,8 +4,9 @@ H264MI_CHECK=1 the engine launches the CHK instantiations of k_wgpp, which
 verify every hand-off at its consumer (recon_kernels.hip CHK_*): the MC
 ring's slot tag and release, the partner row wave's region tag, the intra
 progress words' MB index, and in frame-pipelined launches that every
-reference line read from a picture of the same launch lies in rows already
-tagged final (the host's set_ref_rows).  Each violation sets its own bit of
+reference line read from a picture of the same launch lies in (MB row, MB
+column) cells already published final (the host's set_ref_rows encoding and
+the kernel's dep_wait together).  Each violation sets its own bit of
 the picture's error word.  Green = no bit, frames still the reference's; and
 the deliberately broken hand-offs (test hooks) are caught."""
 import pytest
@@ -81,6 +82,29 @@ def test_checker_catches_a_wrong_ring_tag(monkeypatch):
         ok, checked, _, _ = run.verify(refs)
         assert ok and checked == 8
         assert run.eng.error_bits() & CHK_RING
+    finally:
+        run.free()
+
+
+@pytest.mark.parametrize("pipe", [2, 3])
+def test_checker_catches_short_reference_columns(pipe, monkeypatch):
+    """Test hook H264MI_CHECK_INJECT_REFCOLS: the host records every
+    partition's last reference column 6 MB columns short, so a later picture
+    of a frame-pipelined launch would read reference lines whose columns are
+    not yet stored; the checker must report it (CHK_REFROW) from the loads'
+    own geometry and the producers' progress granules."""
+    import bench
+    monkeypatch.setenv("H264MI_CHECK", "1")
+    monkeypatch.setenv("H264MI_CHECK_INJECT_REFCOLS", "6")
+    streams = [gen.generate(2, 80 + i, nframes=6, w_mbs=22, h_mbs=6, crop_bottom=0, slices=2, gop=6)
+               for i in range(3)]
+    caps = [Capture(s) for s in streams]
+    run = bench.DeviceRun(_lib.mi(), caps, 0, 6, pipe)
+    try:
+        for i in range(len(run.launches)):
+            run.launch(i)
+        run.eng.sync()
+        assert run.eng.error_bits() & CHK_REFROW
     finally:
         run.free()
 

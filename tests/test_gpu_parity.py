@@ -227,12 +227,15 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
         run.free()
 
 
-@pytest.mark.parametrize("wh,pipe", [((13, 7), 2), ((12, 9), 2), ((20, 11), 2), ((13, 7), 3), ((20, 11), 4)])
+@pytest.mark.parametrize("wh,pipe", [((13, 7), 2), ((12, 9), 2), ((20, 11), 2), ((13, 7), 3), ((20, 11), 4),
+                                     ((24, 7), 3), ((8, 9), 2), ((3, 5), 3)])
 def test_engine_pipelined_steps_vs_oracle(wh, pipe):
     """Frame-pipelined launches (two to four consecutive pictures of each of
-    3 streams per launch, physical slots renamed) on sizes whose chroma rows
-    and Cb/Cr planes do not end on 128-B lines (odd w*h: a line straddles
-    the Cb/Cr boundary), every picture vs the oracle's decode of the stream."""
+    3 streams per launch, physical slots renamed) on sizes whose luma rows do
+    not end on 128-B lines (w % 8 != 0: a line holds two rows; w = 3: lines
+    span more MB rows than a window, the whole-picture wait) and whose chroma
+    rows are padded (H264MI_CPITCH), every picture vs the oracle's decode of
+    the stream."""
     import bench
     w, h = wh
     streams = [gen.generate(2, 70 + i, nframes=10, w_mbs=w, h_mbs=h, crop_bottom=0, slices=2, gop=5)

@@ -3,7 +3,7 @@ the distinct 128-B reference lines k_wgpp's MC windows touch, restated here
 from the records with numpy -- mc_issue's window geometry (recon_kernels.hip):
 luma 9 rows x 12 B per 4x4 block from (x0 & ~3) clamped to [0, W16 - 12],
 chroma 3 rows x 8 B per 2x2 block and component from (x0 & ~3) clamped to
-[0, CW - 8], rows clamped to the plane.  Host C only: runs without a GPU."""
+[0, CW - 8], rows clamped to the plane, chroma rows H264MI_CPITCH apart.  Host C only: runs without a GPU."""
 import numpy as np
 import pytest
 
@@ -18,6 +18,7 @@ assert REC.itemsize == engine.MBREC_BYTES
 def lines_numpy(rec, w, h):
     W16, H16 = w * 16, h * 16
     CW, CH = W16 // 2, H16 // 2
+    CP = (CW + 127) & ~127                      # H264MI_CPITCH: chroma rows padded to 128 B
     seen = set()
     b = np.arange(16)
     bx = ((b >> 2) & 1) * 2 + (b & 1)
@@ -40,9 +41,9 @@ def lines_numpy(rec, w, h):
         for comp in range(2):
             for k in range(3):
                 y = np.clip(cy0 + k, 0, CH - 1)
-                base = W16 * H16 + comp * CW * CH
+                base = W16 * H16 + comp * CP * CH
                 for o in (0, 7):
-                    seen.update(zip(slot.tolist(), ((base + y * CW + cax + o) // 128).tolist()))
+                    seen.update(zip(slot.tolist(), ((base + y * CP + cax + o) // 128).tolist()))
     return 128 * len(seen)
 
 

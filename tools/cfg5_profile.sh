@@ -15,5 +15,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_fetch -o bench -- python3 $B4 --no-verify > /dev/null 2> $OUT/pf.err || { tail -20 $OUT/pf.err; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_write -o bench -- python3 $B4 --no-verify > /dev/null 2> $OUT/pw.err || { tail -20 $OUT/pw.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof2 -o bench -- python3 $B2 > /dev/null 2> $OUT/prof2.err || { tail -20 $OUT/prof2.err; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc2_fetch -o bench -- python3 $B2 --no-verify > /dev/null 2> $OUT/pf2.err || { tail -20 $OUT/pf2.err; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc2_write -o bench -- python3 $B2 --no-verify > /dev/null 2> $OUT/pw2.err || { tail -20 $OUT/pw2.err; exit 1; }
+[ "${CFG_TABLE:-1}" = 1 ] || { echo done; exit 0; }
 timeout -k 10 600 python3 tools/config_table.py > $OUT/config_table.json 2> $OUT/config_table.err || { tail -20 $OUT/config_table.err; exit 1; }
 echo done

@@ -163,7 +163,7 @@ def main():
 
         # ours: sequential parse (no slice workers), and its gprof split
         ours = build_ours(tmp, False)
-        env = dict(os.environ, H264MI_PARSE_THREADS="0")
+        env = dict(os.environ, H264MI_PARSE_THREADS="0", H264MI_PARSE_HELP="0")
         wall = cpu = 0.0
         for p in paths:
             w, c = cpu_time([ours, p, "1"], env)
@@ -172,7 +172,7 @@ def main():
               f"{1e3 * cpu / pics:.2f} ms CPU/picture")
         ours_pg = build_ours(tmp, True)
         omap = func_files(ours_pg)
-        rows = gprof_run(ours_pg, paths, [], tmp, {"H264MI_PARSE_THREADS": "0"}, post=["5"])   # 5 passes: samples
+        rows = gprof_run(ours_pg, paths, [], tmp, {"H264MI_PARSE_THREADS": "0", "H264MI_PARSE_HELP": "0"}, post=["5"])   # 5 passes: samples
         report("product host parse, gprof split by file", rows, lambda fn: omap.get(fn, "?"), pics, cpu)
 
 

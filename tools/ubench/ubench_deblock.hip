@@ -37,6 +37,14 @@ __global__ __launch_bounds__(64) void k_ub(unsigned long long *out, int iters, i
         wave_sync();
     }
     unsigned long long t2 = clock64();
+    // the row hand-off patch's arithmetic: one MB-edge step of one line
+    // (row_pp applies it to MB c's rows 12..15 before publishing them)
+    int pv[20];
+    for (int j = 0; j < 20; j++) pv[j] = 100 + ((lane * 5 + j * 11) & 15);
+    const int pbS = bsmode == 2 ? 4 : 2;
+    unsigned long long tp0 = clock64();
+    for (int it = 0; it < iters; it++) filt_line<true>(pv, 0, pbS, 40, 10, 10, 0x03020100u);
+    unsigned long long tp1 = clock64();
     // the filter arithmetic alone: 4 dependent edges on a register line
     int v[20];
     for (int j = 0; j < 20; j++) v[j] = 100 + ((lane * 7 + j * 13) & 15);
@@ -47,10 +55,11 @@ __global__ __launch_bounds__(64) void k_ub(unsigned long long *out, int iters, i
     }
     unsigned long long t3 = clock64();
     int acc = 0;
-    for (int j = 0; j < 20; j++) acc += v[j];
+    for (int j = 0; j < 20; j++) acc += v[j] + pv[j];
     if (lane == 0) {
         out[0] = (t1 - t0) / iters; out[1] = (t2 - t1) / iters; out[2] = (t3 - t2) / iters;
         out[3] = G.ry[100] + acc;
+        out[4] = (tp1 - tp0) / iters;
     }
 }
 
@@ -96,7 +105,8 @@ __global__ __launch_bounds__(64) void k_mc(unsigned long long *out, int iters, c
     const int lane = threadIdx.x;
     ReconArgs a;
     memset(&a, 0, sizeof(a));
-    a.frames = (uint8_t *)frame; a.frame_bytes = 120 * 68 * 384; a.w = 120; a.h = 68;
+    a.frames = (uint8_t *)frame; a.frame_bytes = H264MI_SLOT_BYTES(120, 68); a.cpitch = H264MI_CPITCH(120);
+    a.w = 120; a.h = 68;
     a.dbrec = dbrec; a.res = res; a.err = err;
     PicDesc pd;
     memset(&pd, 0, sizeof(pd));
@@ -129,6 +139,33 @@ __global__ __launch_bounds__(64) void k_mc(unsigned long long *out, int iters, c
     if (lane == 0) { out[0] = acc / iters; out[1] = px[5]; }
 }
 
+// the row-to-row hand-off (row_pp's mailbox granules): two workgroups pass
+// a token back and forth through 8-byte sc1 granules {value, tag}, polled
+// as row_pp polls the row above (sc1 load, s_sleep 1); one-way latency =
+// round trip / 2 on the wall clock.  Blocks 0 and `other` (0 + 8: the same
+// XCD under round-robin placement; 0 + 1: another one)
+__global__ __launch_bounds__(64) void k_hop(unsigned long long *g, unsigned long long *out, int rounds, int other)
+{
+    const int b = blockIdx.x;
+    if (b != 0 && b != other) return;
+    const int lane = threadIdx.x;
+    unsigned long long *mine = g + (b == 0 ? 0 : 16), *theirs = g + (b == 0 ? 16 : 0);
+    const unsigned long long w0 = wall_clock64();
+    unsigned spins = 0;         // bounded: a lost partner ends the loop
+    for (int k = 1; k <= rounds && spins < (1u << 24); k++) {
+        if (b == 0) {
+            if (lane == 0) st_gran(mine, (uint32_t)k, 7u);
+            while (__builtin_amdgcn_readfirstlane((uint32_t)ld_gran(theirs)) != (uint32_t)k && ++spins < (1u << 24))
+                __builtin_amdgcn_s_sleep(1);
+        } else {
+            while (__builtin_amdgcn_readfirstlane((uint32_t)ld_gran(theirs)) != (uint32_t)k && ++spins < (1u << 24))
+                __builtin_amdgcn_s_sleep(1);
+            if (lane == 0) st_gran(mine, (uint32_t)k, 7u);
+        }
+    }
+    if (b == 0 && lane == 0) out[0] = (wall_clock64() - w0);
+}
+
 // wall-clock (100 MHz) against shader clock over the same loop: the clock
 // the passes ran at
 __global__ void k_clk(unsigned long long *out)
@@ -148,11 +185,29 @@ int main()
     (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
     const double mhz = (double)h[1] / (double)h[0] * 100.0;
     printf("shader clock %.0f MHz\n", mhz);
+    double vh_us = 0, patch_us = 0, hop_us[2] = {0, 0};
     for (int mode = 0; mode < 3; mode++) {
+        unsigned long long hh[5];
         hipLaunchKernelGGL(k_ub, dim3(1), dim3(64), 0, 0, d, 2000, mode);
-        (void)hipMemcpy(h, d, 32, hipMemcpyDeviceToHost);
-        printf("bsmode %d: V %llu cycles (%.3f us), H %llu cycles (%.3f us), filt x4 %llu cycles\n", mode,
-               h[0], h[0] / mhz, h[1], h[1] / mhz, h[2]);
+        (void)hipMemcpy(hh, d, 40, hipMemcpyDeviceToHost);
+        printf("bsmode %d: V %llu cycles (%.3f us), H %llu cycles (%.3f us), filt x4 %llu cycles, patch edge %llu cycles\n", mode,
+               hh[0], hh[0] / mhz, hh[1], hh[1] / mhz, hh[2], hh[4]);
+        if (mode == 1) { vh_us = (hh[0] + hh[1]) / mhz; patch_us = hh[4] / mhz; }
+    }
+    {
+        unsigned long long *g;
+        (void)hipMalloc(&g, 256);
+        const int rounds = 2000;
+        for (int k = 0; k < 2; k++) {
+            (void)hipMemset(g, 0, 256);
+            const int other = k == 0 ? 8 : 1;
+            hipLaunchKernelGGL(k_hop, dim3(16), dim3(64), 0, 0, g, d, rounds, other);
+            unsigned long long w = 0;
+            (void)hipMemcpy(&w, d, 8, hipMemcpyDeviceToHost);
+            hop_us[k] = (double)w / 100.0 / (2.0 * rounds);
+            printf("granule hand-off one way (%s XCD): %.3f us\n", k == 0 ? "same" : "other", hop_us[k]);
+        }
+        (void)hipFree(g);
     }
     for (int t = 2; t <= 3; t++) {
         hipLaunchKernelGGL(k_intra, dim3(1), dim3(64), 0, 0, d, 500, t);
@@ -163,8 +218,8 @@ int main()
         uint8_t *frame, *dbrec;
         int16_t *res;
         unsigned *err;
-        (void)hipMalloc(&frame, 120 * 68 * 384);
-        (void)hipMemset(frame, 77, 120 * 68 * 384);
+        (void)hipMalloc(&frame, H264MI_SLOT_BYTES(120, 68));
+        (void)hipMemset(frame, 77, H264MI_SLOT_BYTES(120, 68));
         (void)hipMalloc(&dbrec, 120 * 68 * 64);
         (void)hipMemset(dbrec, 0, 120 * 68 * 64);
         (void)hipMalloc(&res, 120 * 68 * 768);
@@ -177,5 +232,10 @@ int main()
                    h[0], h[0] / mhz);
         }
     }
+    // the inputs of the bench line's latency roofline (bench.py latency_floor,
+    // profiles/ubench.json): lone-wave V + H of a coded P MB (bsmode 1), the
+    // hand-off patch edge, the granule hop (the slower placement)
+    printf("JSON {\"shader_mhz\": %.0f, \"vh_us\": %.4f, \"patch_us\": %.4f, \"hop_same_xcd_us\": %.4f, \"hop_other_xcd_us\": %.4f}\n",
+           mhz, vh_us, patch_us, hop_us[0], hop_us[1]);
     return 0;
 }
