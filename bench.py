@@ -266,6 +266,21 @@ def rename_slots(recs, pics, S, nmbs, nslots, P=2):
     return nphys
 
 
+def far_rows(recs, npics, w, h):
+    """Per picture: the fraction of its MB rows holding an inter MB whose
+    motion reaches far from it -- 2 or more MB rows down or 8 or more MB
+    columns right (a window clamped to the bottom or right picture edge
+    included).  In a frame-pipelined launch such an MB waits for its
+    producer's last rows or a whole row, so (MB row, MB column) waits gain
+    nothing over whole-row waits, which keep the later pictures' rows idle
+    meanwhile (tools/dep_sim.py)."""
+    r = np.frombuffer(recs, dtype=np.uint8).reshape(npics, h * w, MBREC)
+    inter = r[:, :, 0] <= 1
+    mv = r[:, :, 28:92].copy().view("<i2").reshape(npics, h * w, 16, 2)
+    far = inter & (((mv[..., 1] >> 2) >= 32) | ((mv[..., 0] >> 2) >= 128)).any(axis=2)
+    return far.reshape(npics, h, w).any(axis=2).mean(axis=1)
+
+
 def schedule(recs, pics, S, nmbs, warmup, steps, P):
     """Launches as (first step, steps in it).  P > 1 groups steps (Pi ..
     Pi+P-1) when every group meets the engine's frame-pipelined batch
@@ -810,6 +825,12 @@ class DeviceRun:
         self.pics_h, self.recs_h = pics_h, recs_h
         self.slot_of = pics_h[:, 2].reshape(N, S).copy()
         self.is_i = [[c.pictures[k].n_inter == 0 for c in caps] for k in range(N)]
+        # per picture k of stream s: rows with far-reaching motion (far_rows)
+        self.far = far_rows(recs_h, N * S, w, h).reshape(N, S)
+        # frame-pipelined launches' dependency mode: BENCH_DEP_MODE=rows|cols
+        # forces one; by default whole rows when a later picture of the
+        # launch has far-reaching motion in over a quarter of its rows
+        self.dep_force = {"rows": 1, "cols": 2}.get(os.environ.get("BENCH_DEP_MODE", ""), 0)
         self.eng = _DryEngine(device=device) if dry else Engine(w, h, S, nslots, device=device)
         if self.P > 1:
             self.eng.set_steps(self.P)
@@ -887,6 +908,8 @@ class DeviceRun:
         # the launch's shape hint: does it hold an intra-heavy picture
         self.eng.hint_intra(any(2 * self.caps[s].pictures[k].n_intra > self.nmbs
                                 for step in self.launches[i] for s, k in enumerate(step)))
+        if P > 1 and hasattr(self.eng, "hint_deps"):
+            self.eng.hint_deps(self.dep_mode(i))
         if i + 1 < len(self.launches):
             nd, nP = self.d_desc + self.desc_off[i + 1], len(self.launches[i + 1])
             if nP == P:
@@ -896,6 +919,13 @@ class DeviceRun:
                 self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc)
         else:
             self.eng.decode_device_steps(S, P, self.d_recs, self.d_coef, desc)
+
+    def dep_mode(self, i):
+        """Dependency mode of launch i (1 whole rows, 2 (row, column) cells)."""
+        if self.dep_force:
+            return self.dep_force
+        far = max((self.far[k][s] for step in self.launches[i][1:] for s, k in enumerate(step)), default=0.0)
+        return 1 if far > 0.25 else 2
 
     def timed_pictures(self):
         """(stream, picture) of every picture the timed launches decode."""

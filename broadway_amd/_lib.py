@@ -142,6 +142,11 @@ def mi() -> C.CDLL:
     L.h264mi_engine_decode_device.restype = i32
     L.h264mi_engine_hint_intra.argtypes = [vp, i32]
     L.h264mi_engine_hint_intra.restype = i32
+    if hasattr(L, "h264mi_engine_hint_deps"):
+        L.h264mi_engine_hint_deps.argtypes = [vp, i32]
+        L.h264mi_engine_hint_deps.restype = i32
+        L.h264mi_engine_last_deps.argtypes = [vp]
+        L.h264mi_engine_last_deps.restype = i32
     L.h264mi_engine_decode_device_next.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.h264mi_engine_decode_device_next.restype = i32
     L.h264mi_engine_decode_device_steps.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp]

@@ -38,6 +38,7 @@ struct h264mi_engine {
     int pipe_cap;                 // pictures per launch the per-picture buffers hold
     unsigned long long *d_gjunk;  // 64 KiB store sink (ReconArgs::gjunk)
     const char *last_kernel;      // name of the last batch's reconstruction kernel (diagnostics)
+    int last_dep;                 // the last batch's dependency mode (DEP_NONE / DEP_ROWS / DEP_COLS)
     uint8_t *d_dbrec;         // 64 B per batch MB (x2: k_prep double buffer)
     int16_t *d_res;           // 384 x int16 per batch MB (x2)
     // k_prep (deblocking records + residuals) writes buffer half prep_parity;
@@ -56,6 +57,8 @@ struct h264mi_engine {
     int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
     int mc_waves;                      // MC waves per row workgroup: 0 = per launch (below), 2 or 3 forced (H264MI_MC_WAVES)
     int launch_intra;                  // next launch: 1 = has an intra-heavy picture, 0 = none, -1 = unknown
+    int dep_mode;                      // frame-pipelined launches: DEP_ROWS / DEP_COLS (H264MI_DEP_MODE; default rows)
+    int launch_dep;                    // next launch's mode (h264mi_engine_hint_deps), 0 = dep_mode
     int rpw_max;                       // MB rows per k_wgpp workgroup allowed by LDS, 1..3
     int rpw_env;                       // H264MI_RPW: fixed rows per workgroup (0: by batch size)
     int ncu;
@@ -81,6 +84,7 @@ struct h264mi_engine {
     uint8_t *d_rgba;          // h264mi_engine_read_rgba staging (w*h*4 B, allocated on first use)
     int steps;                // pictures per stream per launch (h264mi_engine_set_steps)
     unsigned long long *d_prog;   // per picture row of a launch, per row wave: {MBs stored, epoch} (frame-pipelined launches)
+    unsigned *d_done;             // per picture row of a launch: epoch once the row is stored
     int check;                // H264MI_CHECK=1: the dependency-checker kernels (recon_kernels.hip CHK_*)
     int check_inject;         // H264MI_CHECK_INJECT: test hook (ReconArgs::chk_inject)
     int check_short_cols, check_short_rows;   // H264MI_CHECK_INJECT_REFCOLS / _REFROWS: test hooks
@@ -93,8 +97,9 @@ static void free_pic_buffers(h264mi_engine *e)
 {
     (void)hipFree(e->d_mbx); (void)hipFree(e->d_dbrec); (void)hipFree(e->d_res); (void)hipFree(e->d_err);
     (void)hipFree(e->d_prog);
+    (void)hipFree(e->d_done);
     (void)hipHostFree(e->h_err);
-    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL; e->d_prog = NULL;
+    e->d_mbx = NULL; e->d_dbrec = NULL; e->d_res = NULL; e->d_err = NULL; e->d_prog = NULL; e->d_done = NULL;
     e->h_err = NULL;
     e->pipe_cap = 0;
 }
@@ -106,13 +111,15 @@ static int alloc_pic_buffers(h264mi_engine *e, int cap)
               hipMalloc(&e->d_dbrec, 2 * mbs * 64) == hipSuccess &&
               hipMalloc(&e->d_res, 2 * mbs * 768) == hipSuccess &&
               hipMalloc(&e->d_err, sizeof(unsigned) * np) == hipSuccess &&
-              hipMalloc(&e->d_prog, sizeof(unsigned long long) * 2 * np * e->h) == hipSuccess &&
+              hipMalloc(&e->d_prog, sizeof(unsigned long long) * 2 * PROG_STRIDE * np * e->h) == hipSuccess &&
+              hipMalloc(&e->d_done, sizeof(unsigned) * np * e->h) == hipSuccess &&
               hipHostMalloc(&e->h_err, sizeof(unsigned) * np, hipHostMallocDefault) == hipSuccess;
     if (!ok) { free_pic_buffers(e); return -1; }
     // cleared granules carry epoch 0, which no launch uses
     (void)hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st);
     (void)hipMemsetAsync(e->d_err, 0, sizeof(unsigned) * np, e->st);
-    (void)hipMemsetAsync(e->d_prog, 0, sizeof(unsigned long long) * 2 * np * e->h, e->st);
+    (void)hipMemsetAsync(e->d_prog, 0, sizeof(unsigned long long) * 2 * PROG_STRIDE * np * e->h, e->st);
+    (void)hipMemsetAsync(e->d_done, 0, sizeof(unsigned) * np * e->h, e->st);
     memset(e->h_err, 0, sizeof(unsigned) * np);
     e->pipe_cap = cap;
     return 0;
@@ -130,6 +137,11 @@ static void engine_config(h264mi_engine *e)
     const char *mw = getenv("H264MI_MC_WAVES");
     e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
     e->launch_intra = -1;
+    {
+        const char *dm = getenv("H264MI_DEP_MODE");
+        e->dep_mode = dm && (!strcmp(dm, "cols") || atoi(dm) == DEP_COLS) ? DEP_COLS : DEP_ROWS;
+        e->launch_dep = 0;
+    }
     e->check = getenv("H264MI_CHECK") && atoi(getenv("H264MI_CHECK"));
     e->check_inject = h264mi_test_hooks() && getenv("H264MI_CHECK_INJECT") ? atoi(getenv("H264MI_CHECK_INJECT")) : 0;
     e->check_short_cols = h264mi_test_hooks() && getenv("H264MI_CHECK_INJECT_REFCOLS") ? atoi(getenv("H264MI_CHECK_INJECT_REFCOLS")) : 0;
@@ -169,9 +181,17 @@ static void engine_config(h264mi_engine *e)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<3, false, true, 3, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, false, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, false, DEP_ROWS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, true, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, true, DEP_ROWS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1, false, DEP_ROWS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, false, DEP_COLS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1, true, DEP_COLS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1, false, DEP_COLS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
     e->rpw_max = e->mc_waves == 2 ? 2 : 3;
@@ -359,7 +379,8 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     if (++e->epoch >= (1u << 20)) {           // granule tags: epoch in the high dword
         if (h264mi_engine_sync(e)) return -1;
         HIPCHECK(hipMemsetAsync(e->d_mbx, 0, mbs * 256, e->st));
-        HIPCHECK(hipMemsetAsync(e->d_prog, 0, sizeof(unsigned long long) * 2 * e->pipe_cap * e->h, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_prog, 0, sizeof(unsigned long long) * 2 * PROG_STRIDE * e->pipe_cap * e->h, e->st));
+        HIPCHECK(hipMemsetAsync(e->d_done, 0, sizeof(unsigned) * e->pipe_cap * e->h, e->st));
         e->epoch = 1;
     }
     a.epoch = e->epoch;
@@ -401,6 +422,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     a.P = P;
 #endif
     a.prog = e->d_prog;
+    a.done = e->d_done;
     a.dbrec = e->d_dbrec + hb * mbs * 64;
     a.res = e->d_res + hb * mbs * 384;
     const int rows = npics * e->h;
@@ -424,25 +446,39 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     }
     const bool rec = e->timing || rec_tev;
     e->last_kernel = "k_wgpp";
-    // frame-pipelined launches: the DEP3 instances (single-row, 2 MC waves;
-    // store-progress granules and column-granular waits)
+    // frame-pipelined launches: the DEP_ROWS / DEP_COLS instances (single-row,
+    // 2 MC waves).  The mode is the caller's hint for this launch or the
+    // engine's default; whole rows need every slot below 32 (a bit mask)
     const bool dep3 = P > 1;
+    int dmode = e->launch_dep ? e->launch_dep : e->dep_mode;
+    if (e->nslots > 32) dmode = DEP_COLS;
+    e->launch_dep = 0;                        // a hint covers one launch
+    e->last_dep = dep3 ? dmode : DEP_NONE;
     const int rpw = dep3 ? 1 : rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
     const int nmc = dep3 ? 2 : launch_nmc(e, rpw, P);
     e->launch_intra = -1;                     // a hint covers one launch
-    const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w) : WgppLds<2, 1>::bytes(e->w, dep3))
+    const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w)
+                                                                      : WgppLds<2, 1>::bytes(e->w, dep3 && dmode == DEP_COLS))
                         : rpw == 3 ? WgppLds<3, 3>::bytes(e->w) : rpw == 2 ? WgppLds<3, 2>::bytes(e->w)
                         : WgppLds<3, 1>::bytes(e->w);
     if (dep3) {
-        // (no profiling build: a profiled engine runs them unstamped)
-        e->last_kernel = e->check ? "k_wgpp_check" : "k_wgpp";
-        if (e->check)
-            hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1, true, true>), grid, dim3(256), lmbx, e->st, rec ? t0 : nullptr,
-                                  rec ? t2 : nullptr, 0, a);
-        else
-            hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1, false, true>), grid, dim3(256), lmbx, e->st, rec ? t0 : nullptr,
-                                  rec ? t2 : nullptr, 0, a);
+        e->last_kernel = e->check ? "k_wgpp_check" : a.prof ? "k_wgpp_prof" : "k_wgpp";
+#define DEP_LAUNCH(M)                                                                                          \
+        do {                                                                                                   \
+            if (a.prof && !e->check)                                                                           \
+                hipExtLaunchKernelGGL((k_wgpp<2, true, true, 1, false, M>), grid, dim3(256), lmbx, e->st,      \
+                                      rec ? t0 : nullptr, rec ? t2 : nullptr, 0, a);                          \
+            else if (e->check)                                                                                 \
+                hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1, true, M>), grid, dim3(256), lmbx, e->st,      \
+                                      rec ? t0 : nullptr, rec ? t2 : nullptr, 0, a);                          \
+            else                                                                                               \
+                hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1, false, M>), grid, dim3(256), lmbx, e->st,     \
+                                      rec ? t0 : nullptr, rec ? t2 : nullptr, 0, a);                          \
+        } while (0)
+        if (dmode == DEP_COLS) DEP_LAUNCH(DEP_COLS);
+        else DEP_LAUNCH(DEP_ROWS);
+#undef DEP_LAUNCH
     } else if (a.prof) {
         if (rec) (void)hipEventRecord(t0, e->st);
         if (rpw == 3) hipLaunchKernelGGL((k_wgpp<3, true, true, 3>), grid, dim3(960), lmbx, e->st, a);
@@ -556,6 +592,16 @@ extern "C" int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy)
     return 0;
 }
 
+// the next frame-pipelined launch's dependency mode: 1 whole MB rows, 2 (MB
+// row, MB column) cells, 0 the engine's default (H264MI_DEP_MODE)
+extern "C" int h264mi_engine_hint_deps(h264mi_engine *e, int mode)
+{
+    if (!e || mode < 0 || mode > DEP_COLS) return -1;
+    e->launch_dep = mode;
+    return 0;
+}
+extern "C" int h264mi_engine_last_deps(h264mi_engine *e) { return e ? e->last_dep : -1; }
+
 extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
                                            const void *d_pics)
 {
@@ -623,7 +669,8 @@ extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)
 {
     // (frame-pipelined launches name the earlier steps' target slots in a
     // 32-bit mask: recon_kernels.hip dep_wait)
-    // (a later step's producers are found by slot equality, 8-bit slots)
+    // (a later step's producers: by slot equality, 8-bit slots (DEP_COLS), or
+    // a 32-bit slot mask (DEP_ROWS; engines of more slots run DEP_COLS))
     if (!e || steps < 1 || steps > H264MI_MAX_STEPS || (steps > 1 && e->nslots > 255)) return -1;
     if (steps == e->steps) return 0;
     if (h264mi_engine_sync(e)) return -1;

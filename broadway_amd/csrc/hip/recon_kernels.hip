@@ -56,12 +56,16 @@ struct ReconArgs {
     // frame-pipelined launches (P > 1): the launch holds P consecutive
     // pictures of each of the S streams, step-major (picture p = j * S + s);
     // step j's MC reads of a slot written by step j - k of the same launch
-    // wait for that picture's store progress: prog[((p - k * S) * h + r) * 2
-    // + w] = {MBs of row wave w's parity below this are stored, epoch}, an
-    // 8-B granule the row wave publishes behind its write-through frame
-    // stores (row_pp, dep_wait)
+    // wait until the lines they read are final there: DEP_ROWS by whole MB
+    // rows (done tags), DEP_COLS by (MB row, MB column) through the store
+    // progress granules PROG_AT(prog, p - k * S, h, r, w) = {MBs of row wave
+    // w's parity stored, epoch} (row_pp, dep_wait_cols)
     int P;
     unsigned long long *prog;
+    // DEP_ROWS launches: one u32 per (picture, MB row), epoch once the row is
+    // final in its slot (row workgroup r after its frame stores and an agent
+    // release; chained: step j's row r only after step j - 1's)
+    unsigned int *done;
     // profiling build only: 1 = the row waves only drain the MC ring (no
     // deblocking, no stores) -- SQ counters of such a launch minus those of
     // a normal one split the instruction counts by wave role (tools/sq_roles.py)
@@ -82,6 +86,7 @@ struct ReconArgs {
     // (frame-pipelined CHK launches) test hooks: dep_wait waits for this many
     // MB columns / rows less than the loads need, which CHK_REFROW must catch
     int chk_short_cols, chk_short_rows;
+
 };
 
 // Dependency checker (the reference's compile-time
@@ -103,6 +108,18 @@ struct ReconArgs {
 // the ring slot; the row wave's copy-in carries it into its region.  No LDS
 // layout changes for the normal kernels.
 #define CHK_TAG_OFF 22
+// frame-pipelined launches: store-progress granules, one 128-B line per
+// (picture, MB row, row wave), so that a line is rewritten only by its own
+// wave and polls between two publishes hit the L2 (a line the granules of
+// eight rows shared was rewritten every ~0.3 us: every poll went to memory)
+#ifndef PROG_STRIDE
+#define PROG_STRIDE 16          // u64 per row wave
+#endif
+#define PROG_AT(base, pic, h, r, w) ((base) + (((size_t)(pic) * (h) + (r)) * 2 + (w)) * PROG_STRIDE)
+// a row wave publishes its progress every PROG_EVERY of its MBs
+#ifndef PROG_EVERY
+#define PROG_EVERY 2
+#endif
 #define CHK_RING    64u
 #define CHK_RING_WR 128u
 #define CHK_REGION  256u
@@ -1457,7 +1474,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 #else
     const bool wst = wt;
 #endif
-    unsigned long long *const prog_me = a.prog + ((size_t)p * H + r) * 2 + w;
+    unsigned long long *const prog_me = PROG_AT(a.prog, p, H, r, w);
     auto fst = [&](void *ptr, uint32_t v) {
         if (wst) st32<true>(ptr, v);
         else st32<false>(ptr, v);
@@ -1476,7 +1493,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 
     for (int c = w; c < W; c += 2) {
         if (a.row_prio_split) __builtin_amdgcn_s_setprio(1);
-        if (wt && c >= 2) {
+        if (wt && c >= 2 && ((c >> 1) % PROG_EVERY) == 0) {
             // MB c - 2's write-through stores (issued one MB of the partner
             // earlier) drained: publish this wave's progress, off the chain
 #ifndef STUDY_COLP_NOWAIT
@@ -1912,9 +1929,15 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
 // waves have seen is kept in the workgroup's LDS (values only grow, so any
 // value a wave stores is a valid lower bound), so most MBs need no load.
 #define PC_ROWS 136         // MB rows of a producer the LDS progress cache holds (2160p: 135)
+// k_wgpp's dependency modes (template DEPM): none (one step per launch), whole
+// rows, or (MB row, MB column) cells
+enum { DEP_NONE = 0, DEP_ROWS = 1, DEP_COLS = 2 };
 struct DepState {
     int n;                 // in-launch producers: steps j - 1 .. j - n (0: none)
-    uint32_t slots;        // their target slots, 8 bits each (step j - 1 - k at bits 8k)
+    uint32_t slots;        // DEP_COLS: their target slots, 8 bits each (step j - 1 - k at bits 8k)
+    uint32_t mask;         // DEP_ROWS: their target slots, a bit each (< 32)
+    int pic;               // DEP_ROWS: the step j - 1 picture
+    int known;             // DEP_ROWS: its leading rows seen done by this wave
 };
 typedef __attribute__((address_space(3))) unsigned long long lds_u2;   // {wave 0, wave 1} progress
 
@@ -1930,8 +1953,7 @@ __device__ __forceinline__ bool dep_rows_ok(const ReconArgs &a, int p, int k, in
         const unsigned long long c = R < PC_ROWS ? pc[k * PC_ROWS + R] : 0ull;
         uint32_t vx = (uint32_t)c, vy = (uint32_t)(c >> 32);
         if (min(vx, vy) < need && load) {
-            const unsigned long long *g = a.prog + ((size_t)pk * a.h + R) * 2;
-            const unsigned long long g0 = ld_gran(g), g1 = ld_gran(g + 1);
+            const unsigned long long g0 = ld_gran(PROG_AT(a.prog, pk, a.h, R, 0)), g1 = ld_gran(PROG_AT(a.prog, pk, a.h, R, 1));
             if ((uint32_t)(g0 >> 32) == a.epoch) vx = max(vx, (uint32_t)g0);
             if ((uint32_t)(g1 >> 32) == a.epoch) vy = max(vy, (uint32_t)g1);
             if (R < PC_ROWS) pc[k * PC_ROWS + R] = (unsigned long long)vx | ((unsigned long long)vy << 32);
@@ -1942,8 +1964,8 @@ __device__ __forceinline__ bool dep_rows_ok(const ReconArgs &a, int p, int k, in
 }
 
 template <bool CHK>
-__device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, int mb, uint32_t v0, int lane, const DepState &D,
-                                         lds_u2 *pc)
+__device__ __forceinline__ void dep_wait_cols(const ReconArgs &a, int p, int mb, uint32_t v0, int lane, const DepState &D,
+                                              lds_u2 *pc)
 {
     const uint32_t d0 = rec_dw(v0, 0), refs = rec_dw(v0, 6);
     if ((d0 & 255) >= MBT_I4x4) return;
@@ -2001,14 +2023,122 @@ __device__ __forceinline__ void dep_wait(const ReconArgs &a, int p, int mb, uint
         if (!okl) okl = dep_rows_ok(a, p, kl, lrlo, lrhi, lx, pass > 0, pc);
         if (!okc) okc = dep_rows_ok(a, p, kc, crlo, crhi, cx, pass > 0, pc);
         if (__builtin_amdgcn_ballot_w64(!(okl && okc)) == 0) break;
+#ifdef STUDY_DEP_POLLONCE
+        if (pass > 0) break;                // study build (output not valid): one poll, never wait
+#endif
         if (pass > 0) {
+#ifdef DEP_SLEEP_LONG
+            __builtin_amdgcn_s_sleep(32);       // ~0.85 us: about one MB of the producer's row
+#else
             __builtin_amdgcn_s_sleep(4);
+#endif
             if (++spins > (1u << 21)) { if (lane == 0) atomicOr(a.err + p, 32u); break; }
         }
     }
     // order the reference loads after the polls (compiler: the polls are
     // relaxed atomics; hardware: the wave issues in order)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// DEP_ROWS: the whole-row rule of round 4.  The host records per inter MB
+// and 8x8 partition the last reference MB row its lines touch (MbRec.i4 of
+// an inter MB, capture.c set_ref_rows), and row workgroup r of a picture
+// tags done[p][r] = epoch once its frame stores drained and an agent-scope
+// release wrote its XCD's L2 back.  MB row R of a slot is final once rows
+// 0..R+1 are done (row R+1 stores row R's rows 12..15).  The done tags are
+// chained (row r of step j only after row r of step j - 1), so the step j - 1
+// picture's leading rows seen done imply the same rows of every earlier step:
+// a partition whose reference slot is any earlier step's target (the mask)
+// waits on step j - 1's tags.  For the configs[3] streams, whose windows
+// reach the bottom and right picture edges in most rows (5 % off-picture
+// MVs), this is as early as the data allows (tools/dep_sim.py) and keeps the
+// later pictures' rows idle until then (less contention than DEP_COLS).
+template <bool CHK>
+__device__ __forceinline__ void dep_wait_rows(const ReconArgs &a, int p, uint32_t v0, int lane, DepState &D)
+{
+    const uint32_t d0 = rec_dw(v0, 0);
+    if ((d0 & 255) >= MBT_I4x4) return;
+    const uint32_t rw01 = rec_dw(v0, 4), rw23 = rec_dw(v0, 5), refs = rec_dw(v0, 6);
+    int need = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t row = ((q < 2 ? rw01 : rw23) >> ((q & 1) * 16)) & 0xFFFF;
+        const uint32_t rs = (refs >> (q * 8)) & 255;
+        const uint32_t hit = rs < 32 ? (D.mask >> rs) & 1 : 0;
+        need = max(need, hit ? (int)row + 2 : 0);
+    }
+    if (CHK && a.chk_short_rows) need = max(need - a.chk_short_rows, 0);
+    need = min(need, a.h);
+    unsigned spins = 0;
+    while (need > D.known) {
+        const int idx = D.known + lane;
+        const bool ok = idx >= a.h || ld_sc1_u32(a.done + (size_t)D.pic * a.h + idx) == a.epoch;
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(ok);
+        const int adv = __builtin_amdgcn_readfirstlane(~m ? __builtin_ctzll(~m) : 64);
+        D.known = min(D.known + adv, a.h);
+        if (adv == 0) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); D.known = a.h; }
+        }
+    }
+    // order the reference loads after the polls (compiler: the polls are
+    // relaxed atomics; hardware: the wave issues in order)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// its checker: the rows of the in-launch producer picture that MB mb's
+// reference loads need final, from the loads' own geometry (mc_issue's
+// windows at 128-B line granularity), must all be among the leading rows
+// dep_wait_rows saw done (D.known) -- i.e. set_ref_rows covered every line
+// the kernel reads.  Rows 0..R+1 done make MB row R's bytes final.
+__device__ __forceinline__ int chk_rows_need(uint32_t o, uint32_t ysz, int W16, int CP, int h)
+{
+    // MB rows whose workgroups must be done for byte o of a slot to be final
+    // (chroma rows padded to CP: no line crosses a plane)
+    const uint32_t csz = (uint32_t)CP * (uint32_t)(h * 8);
+    const int R = o < ysz ? (int)(o / (uint32_t)W16) >> 4 : (int)(((o - ysz) % csz) / (uint32_t)CP) >> 3;
+    return min(R + 2, h);
+}
+__device__ __forceinline__ void chk_ref_rows_rows(const ReconArgs &a, int p, int mb, uint32_t v0, int lane, const DepState &D)
+{
+    const uint32_t d0 = rec_dw(v0, 0), refs = rec_dw(v0, 6);
+    if ((d0 & 255) >= MBT_I4x4) return;
+    const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2, CP = a.cpitch;
+    const uint32_t ysz = (uint32_t)W16 * H16, csz = (uint32_t)CP * CH;
+    const int mbx = mb % a.w, mby = mb / a.w;
+    int need = 0;
+    {   // luma: lane -> block lb, window rows lsub + 4k (mc_issue)
+        const int lb = lane >> 2, lsub = lane & 3;
+        const uint32_t mvl = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + lb) << 2, (int)v0);
+        if (const uint32_t rs = (refs >> ((lb >> 2) * 8)) & 255; rs < 32 && ((D.mask >> rs) & 1)) {
+            const int mvx = (int)(int16_t)(mvl & 0xFFFF), mvy = (int)(int16_t)(mvl >> 16);
+            const int x0 = clip3(0, W16 - 12, (mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2) & ~3);
+            const int y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const int y = clip3(0, H16 - 1, y0 + min(lsub + 4 * k, 8));
+                const uint32_t o = (uint32_t)(y * W16 + x0);
+                need = max(need, chk_rows_need(min((o + 11) | 127u, ysz - 1), ysz, W16, CP, a.h));
+            }
+        }
+    }
+    {   // chroma: lane -> block cb, component
+        const int cb = (lane & 31) >> 1, ccomp = lane & 1;
+        const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
+        if (const uint32_t rs = (refs >> ((cb >> 2) * 8)) & 255; rs < 32 && ((D.mask >> rs) & 1)) {
+            const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
+            const int x0 = clip3(0, CW - 8, (mbx * 8 + blk_x(cb) * 2 + (cmx >> 3)) & ~3);
+            const int y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3);
+#pragma unroll
+            for (int wy = 0; wy < 3; wy++) {
+                const int y = clip3(0, CH - 1, y0 + wy);
+                const uint32_t base = ysz + (uint32_t)ccomp * csz;
+                const uint32_t o = base + (uint32_t)(y * CP + x0);
+                need = max(need, chk_rows_need(min((o + 7) | 127u, base + csz - 1), ysz, W16, CP, a.h));
+            }
+        }
+    }
+    if (__builtin_amdgcn_ballot_w64(need > D.known) != 0 && lane == 0) atomicOr(a.err + p, CHK_REFROW);
 }
 
 // k_wgpp tail workgroup: waves 0..NMC-1 run the next batch's k_prep over a
@@ -2055,8 +2185,7 @@ __device__ __forceinline__ void prep_tail(const ReconArgs &a, McScratch *M, MbRi
 __device__ __forceinline__ bool chk_row_final(const ReconArgs &a, int pk, int R, uint32_t need)
 {
     if (R >= a.h || need == 0) return true;
-    const unsigned long long *g = a.prog + ((size_t)pk * a.h + R) * 2;
-    const unsigned long long g0 = ld_gran(g), g1 = ld_gran(g + 1);
+    const unsigned long long g0 = ld_gran(PROG_AT(a.prog, pk, a.h, R, 0)), g1 = ld_gran(PROG_AT(a.prog, pk, a.h, R, 1));
     const uint32_t v0 = (uint32_t)(g0 >> 32) == a.epoch ? (uint32_t)g0 : 0u;
     const uint32_t v1 = (uint32_t)(g1 >> 32) == a.epoch ? (uint32_t)g1 : 0u;
     return min(v0, v1) >= need;
@@ -2141,7 +2270,7 @@ __device__ __forceinline__ void chk_ref_rows(const ReconArgs &a, int p, int mb, 
 #ifndef MC_DYN
 #define MC_DYN 1
 #endif
-template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK, bool DEP3>
+template <int NMC, bool PROF, bool UPL, bool MEL, int RK, bool CHK, int DEPM>
 __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0, int lane, McScratch &Mw, MbRing<RK> &R,
                                        const uint32_t *i4tab, const unsigned long long *mbx_up, unsigned long long *mbx_me,
                                        lds_u2 *pc)
@@ -2149,17 +2278,23 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     const PicDesc pd = a.pics[p];
     const uint32_t *recrow = (const uint32_t *)(a.rec + pd.rec_base + r * a.w);
     DepState D;
-    D.n = 0; D.slots = 0;
-    if (DEP3 && a.P > 1) {
+    D.n = 0; D.slots = 0; D.mask = 0; D.pic = 0; D.known = 0;
+    if (DEPM != DEP_NONE && a.P > 1) {
         // the earlier steps of this stream in the launch (at most
         // H264MI_MAX_STEPS - 1) and the slots their pictures write
         const int j = p / a.S;
-        uint32_t m = 0;
+        uint32_t m = 0, mk = 0;
 #pragma unroll
         for (int k = 1; k < 4; k++)
-            if (k <= j) m |= (a.pics[p - k * a.S].cur_slot & 255) << ((k - 1) * 8);
+            if (k <= j) {
+                const uint32_t cs = a.pics[p - k * a.S].cur_slot;
+                m |= (cs & 255) << ((k - 1) * 8);
+                mk |= 1u << (cs & 31);
+            }
         D.n = __builtin_amdgcn_readfirstlane(min(j, 3));
         D.slots = __builtin_amdgcn_readfirstlane(m);
+        D.mask = __builtin_amdgcn_readfirstlane(mk);
+        D.pic = p - a.S;
     }
     // the next MB of this wave: the row counter's (dynamic) or c + NMC.  The
     // claim is one lane's LDS atomic, exec = lane 0 inside the asm, its
@@ -2188,8 +2323,10 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
     int c = c0;
     uint32_t v0 = c < a.w ? recrow[(size_t)c * 24 + (lane < 24 ? lane : 0)] : 0;
     McLoad ld;
-    if (DEP3 && c < a.w && D.n) dep_wait<CHK>(a, p, r * a.w + c, v0, lane, D, pc);
-    if (DEP3 && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
+    if (DEPM == DEP_COLS && c < a.w && D.n) dep_wait_cols<CHK>(a, p, r * a.w + c, v0, lane, D, pc);
+    if (DEPM == DEP_COLS && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
+    if (DEPM == DEP_ROWS && c < a.w && D.n) dep_wait_rows<CHK>(a, p, v0, lane, D);
+    if (DEPM == DEP_ROWS && CHK && c < a.w && D.n) chk_ref_rows_rows(a, p, r * a.w + c, v0, lane, D);
     if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
 
     const int lead = a.mc_lead > 0 && a.mc_lead < RK ? a.mc_lead : RK;
@@ -2264,8 +2401,14 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         }
         c = cn;
         v0 = nv0;
-        if (DEP3 && c < a.w && D.n) dep_wait<CHK>(a, p, r * a.w + c, v0, lane, D, pc);
-        if (DEP3 && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
+        const unsigned long long tdw = PROF ? wall_clock64() : 0;
+        if (DEPM == DEP_COLS && c < a.w && D.n) dep_wait_cols<CHK>(a, p, r * a.w + c, v0, lane, D, pc);
+        if (DEPM == DEP_ROWS && c < a.w && D.n) dep_wait_rows<CHK>(a, p, v0, lane, D);
+        // PROF stamp [6] of the next MB: its in-launch dependency wait (100 MHz ticks)
+        if (PROF && DEPM != DEP_NONE && c < a.w && lane == 0)
+            a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 6] = wall_clock64() - tdw;
+        if (DEPM == DEP_COLS && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
+        if (DEPM == DEP_ROWS && CHK && c < a.w && D.n) chk_ref_rows_rows(a, p, r * a.w + c, v0, lane, D);
         if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
     }
 }
@@ -2311,10 +2454,10 @@ struct WgppLds {
 #define WGPP2_WAVES_PER_EU 4
 #endif
 
-// DEP3: frame-pipelined launches (two or more steps per stream): the row
-// waves publish store progress and the MC waves wait on it (dep_wait); a
-// separate instance, so that single-step launches carry none of it
-template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false, bool DEP3 = false>
+// DEPM: frame-pipelined launches (two or more steps per stream), DEP_ROWS or
+// DEP_COLS (dep_wait_rows / dep_wait_cols); separate instances, so that
+// single-step launches carry none of it
+template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false, int DEPM = DEP_NONE>
 __global__ __launch_bounds__(64 * (NMC + 2) * RPW)
 __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : WGPP2_WAVES_PER_EU))) void k_wgpp(ReconArgs a)
 {
@@ -2346,7 +2489,7 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
         L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
     // frame-pipelined launches: the producers' progress cache (dep_wait)
     lds_u2 *const pc = (lds_u2 *)(__attribute__((address_space(3))) unsigned char *)(wg_lds + Lay::offX);
-    if (DEP3)
+    if (DEPM == DEP_COLS)
         for (int e = threadIdx.x; e < 3 * PC_ROWS; e += 64 * (NMC + 2) * RPW) pc[e] = 0ull;
     if (RPW > 1)        // granule tags from an earlier workgroup on this CU must not match
         for (int e = threadIdx.x; e < (RPW - 1) * a.w * 32; e += 64 * (NMC + 2) * RPW) lmbx[e] = 0;
@@ -2365,7 +2508,7 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     unsigned long long *const me = mel ? lmbx + q * W32 : a.mbx + ((size_t)p * a.h + r) * W32;
     if (wid < 2) {
         __builtin_amdgcn_s_setprio(3);
-        if (DEP3) row_pp<PROF, false, false, RK, CHK, true>(a, p, r, L[q], wid, lane, &R[q], up, me, j + 1 < a.P);
+        if (DEPM == DEP_COLS) row_pp<PROF, false, false, RK, CHK, true>(a, p, r, L[q], wid, lane, &R[q], up, me, j + 1 < a.P);
         else if (!upl && !mel) row_pp<PROF, false, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else if (!upl) row_pp<PROF, false, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else if (mel) row_pp<PROF, true, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
@@ -2373,14 +2516,38 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
         // row finished: progress for the tail workgroups' start
         if (wid == 0 && lane == 0 && a.rows_done)
             __hip_atomic_fetch_add(a.rows_done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (DEPM == DEP_ROWS && j + 1 < a.P) {
+            // a later step of this launch may read this picture: once both
+            // row waves' frame stores have completed, the second wave writes
+            // the XCD's L2 back and tags the row done -- chained (row r of
+            // step j - 1 first; normally long done, this picture's rows
+            // having waited on it)
+            if (j > 0) {
+                const uint32_t *pd = a.done + (size_t)(p - S) * a.h + r;
+                unsigned spins = 0;
+                while (__builtin_amdgcn_readfirstlane(ld_sc1_u32(pd)) != a.epoch) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > (1u << 22)) { if (lane == 0) atomicOr(a.err + p, 32u); break; }
+                }
+            }
+            drain_vm();
+            int last = 0;
+            if (lane == 0) last = __hip_atomic_fetch_add(&L[q].fin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            last = __builtin_amdgcn_readfirstlane(last);
+            if (last == 1 && lane == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_sc1_u32(a.done + (size_t)p * a.h + r, a.epoch);
+            }
+        }
         return;
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
     McScratch &Mw = M[q * NMC + wid - 2];
-    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
-    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
-    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
-    else mc_row<NMC, PROF, true, false, RK, CHK, DEP3>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    else if (mel) mc_row<NMC, PROF, true, true, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
+    else mc_row<NMC, PROF, true, false, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
 }
 template __global__ void k_wgpp<3, false, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 1>(ReconArgs);
@@ -2396,6 +2563,11 @@ template __global__ void k_wgpp<2, false, true, 1, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 2, true>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 2, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 3, true>(ReconArgs);
-// three or more steps per launch (single-row, 2 MC waves: launch_batch)
-template __global__ void k_wgpp<2, false, true, 1, false, true>(ReconArgs);
-template __global__ void k_wgpp<2, false, true, 1, true, true>(ReconArgs);
+// frame-pipelined launches (single-row, 2 MC waves: launch_batch), by
+// dependency mode; the profiling builds for tools/prof_steps.py
+template __global__ void k_wgpp<2, false, true, 1, false, DEP_ROWS>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 1, true, DEP_ROWS>(ReconArgs);
+template __global__ void k_wgpp<2, true, true, 1, false, DEP_ROWS>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 1, false, DEP_COLS>(ReconArgs);
+template __global__ void k_wgpp<2, false, true, 1, true, DEP_COLS>(ReconArgs);
+template __global__ void k_wgpp<2, true, true, 1, false, DEP_COLS>(ReconArgs);

@@ -58,6 +58,53 @@ int h264mi_test_hooks(void)
     return v;
 }
 
+/* Frame-pipelined launches with whole-row waits (recon_kernels.hip
+ * dep_wait_rows): per inter MB and 8x8 partition, the last MB row of its
+ * reference slot that a 128-B line read by its motion compensation touches,
+ * as four uint16 in MbRec.i4 (luma 9 rows x 12 bytes per 4x4 block, chroma 3
+ * rows x 8 bytes per 2x2 block and plane, windows clamped as in the kernel's
+ * mc_issue).  Slot layout H264MI_SLOT_BYTES: no line crosses a plane
+ * boundary, chroma lines hold one row; a luma line can reach into the next
+ * row (w % 8 != 0), so the row is that of the line's last byte.  The
+ * column-granular mode (dep_wait_cols) takes the geometry in the kernel. */
+static int line_row(long long last, long long pbase, long long pbytes, int pitch, int mbh)
+{
+    long long le = last | 127;
+    if (le > pbase + pbytes - 1) le = pbase + pbytes - 1;
+    return (int)((le - pbase) / pitch) / mbh;
+}
+
+static int clampi(int lo, int hi, int v) { return v < lo ? lo : v > hi ? hi : v; }
+
+static void set_ref_rows(MbRec *recs, int w, int h)
+{
+    static const int bx[16] = {0, 1, 0, 1, 2, 3, 2, 3, 0, 1, 0, 1, 2, 3, 2, 3};
+    static const int by[16] = {0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3};
+    const int W16 = w * 16, H16 = h * 16, CW = W16 / 2, CH = H16 / 2, CP = H264MI_CPITCH(w);
+    const long long ysz = (long long)W16 * H16, csz = (long long)CP * CH;
+    for (int mb = 0; mb < w * h; mb++) {
+        MbRec *r = &recs[mb];
+        if (r->type != MBT_INTER && r->type != MBT_SKIP) continue;
+        const int mbx = mb % w, mby = mb / w;
+        uint16_t rows[4] = {0, 0, 0, 0};
+        for (int b = 0; b < 16; b++) {
+            const int mvx = r->mv[b][0], mvy = r->mv[b][1];
+            const int lax = clampi(0, W16 - 12, (mbx * 16 + bx[b] * 4 + (mvx >> 2) - 2) & ~3);
+            const int ly = clampi(0, H16 - 1, mby * 16 + by[b] * 4 + (mvy >> 2) - 2 + 8);
+            int n = line_row((long long)ly * W16 + lax + 11, 0, ysz, W16, 16);
+            const int cax = clampi(0, CW - 8, (mbx * 8 + bx[b] * 2 + (mvx >> 3)) & ~3);
+            const int cy = clampi(0, CH - 1, mby * 8 + by[b] * 2 + (mvy >> 3) + 2);
+            for (int comp = 0; comp < 2; comp++) {
+                const long long pb = ysz + comp * csz;
+                const int nc = line_row(pb + (long long)cy * CP + cax + 7, pb, csz, CP, 8);
+                if (nc > n) n = nc;
+            }
+            if (n > rows[b >> 2]) rows[b >> 2] = (uint16_t)n;
+        }
+        memcpy(r->i4, rows, 8);
+    }
+}
+
 static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
 {
     struct h264mi_capture *c = (struct h264mi_capture *)vctx;
@@ -94,6 +141,7 @@ static int cap_decode(void *vctx, const PicBuild *pb, int cur_slot)
     p->n_intra = pb->n_intra;
     p->n_coded = pb->n_coded_blocks;
     memcpy(c->recs + c->nrec, pb->rec, sizeof(MbRec) * nmbs);
+    set_ref_rows(c->recs + c->nrec, c->w, c->h);
     p->ref_line_bytes = ref_line_bytes(c->recs + c->nrec, c->w, c->h);
     if (pb->ncoef) memcpy(c->coefs + c->ncoef * 16, pb->coef, (size_t)pb->ncoef * 32);
     c->nrec += nmbs;

@@ -115,6 +115,19 @@ class Engine:
                                                     n_recs, n_coef, n_pics) != 0:
             raise RuntimeError("h264mi_engine_decode_device_next failed")
 
+    def hint_deps(self, mode: int) -> None:
+        """Dependency mode of the next frame-pipelined launch: 1 whole MB
+        rows, 2 (MB row, MB column) cells, 0 the engine's default."""
+        if not hasattr(self._L, "h264mi_engine_hint_deps"):     # an older tree's A/B build
+            return
+        if self._L.h264mi_engine_hint_deps(self._h, int(mode)) != 0:
+            raise RuntimeError("h264mi_engine_hint_deps failed")
+
+    def last_deps(self) -> int:
+        if not hasattr(self._L, "h264mi_engine_last_deps"):
+            return -1
+        return int(self._L.h264mi_engine_last_deps(self._h))
+
     def hint_intra(self, intra_heavy: bool) -> None:
         """Shape hint for the next device-resident launch: does some picture
         have more than half its MBs intra (include/h264mi.h)."""

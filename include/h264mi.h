@@ -182,6 +182,13 @@ int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const i
  * the launch uses 3.  A hint covers one launch.  Returns 0, or -1 on a bad
  * argument. */
 int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy);
+/* the next frame-pipelined launch's dependency mode: 1 whole MB rows of the
+ * earlier steps' pictures (MbRec.i4 rows from h264mi_capture), 2 (MB row, MB
+ * column) cells (geometry in the kernel), 0 the engine's default
+ * (H264MI_DEP_MODE=rows|cols, default rows); last_deps: the mode the last
+ * launch ran (0: one step, no dependency) */
+int h264mi_engine_hint_deps(h264mi_engine *e, int mode);
+int h264mi_engine_last_deps(h264mi_engine *e);
 
 /* Neighbour-based error concealment on the device (ConcealMb's intra branch,
  * h264bsd_conceal.c:337-579, replaces the host pass over a copy of the

@@ -70,8 +70,12 @@ typedef struct MbRec {
     int8_t   offB;      /* FilterOffsetB */
     uint32_t cbits;     /* coded-block mask, see above */
     uint32_t coef;      /* first coefficient block index */
-    uint8_t  i4[8];     /* I_4x4: Intra4x4PredMode, 4 bits per block, z-scan (unused
-                           by inter MBs) */
+    uint8_t  i4[8];     /* I_4x4: Intra4x4PredMode, 4 bits per block, z-scan.
+                           Inter (MBT_INTER / MBT_SKIP) in frame-pipelined batches with
+                           whole-row waits: four uint16 (little endian), per 8x8
+                           partition the last MB row of its reference slot that a 128-B
+                           line read by its motion compensation touches (h264mi_capture
+                           fills it) */
     uint8_t  ref[4];    /* DPB slot per 8x8 partition (inter only) */
     int16_t  mv[16][2]; /* per 4x4 block, z-scan, quarter-pel (x, y) */
     uint16_t slice;     /* slice id within the picture */

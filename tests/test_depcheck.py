@@ -23,8 +23,9 @@ EDGE = sorted(n for n in CASES if n.startswith("edge_"))
 CHK_RING, CHK_RING_WR, CHK_REGION, CHK_PROG, CHK_REFROW = 64, 128, 256, 512, 1024
 
 
-@pytest.mark.parametrize("pipe,staggered", [(1, True), (2, False), (2, True), (3, True)])
-def test_checker_bench_shard_clean(pipe, staggered, monkeypatch):
+@pytest.mark.parametrize("pipe,staggered,mode", [(1, True, ""), (2, False, ""), (2, True, ""), (3, True, ""),
+                                                 (2, False, "cols"), (3, True, "cols")])
+def test_checker_bench_shard_clean(pipe, staggered, mode, monkeypatch):
     """Rank 0's configs[3] shard (8 x 1080p, 60 pictures each) through
     bench.DeviceRun under the checker: the bench's GOP-staggered plan with 1
     to 3 steps per launch (the reference-row checks against every earlier
@@ -33,6 +34,8 @@ def test_checker_bench_shard_clean(pipe, staggered, monkeypatch):
     Every picture vs the reference MD5s, no checker bit."""
     import bench
     monkeypatch.setenv("H264MI_CHECK", "1")
+    if mode:
+        monkeypatch.setenv("BENCH_DEP_MODE", mode)
     seeds = bench.shard_seeds(0, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
@@ -95,6 +98,7 @@ def test_checker_catches_short_reference_columns(pipe, monkeypatch):
     own geometry and the producers' progress granules."""
     import bench
     monkeypatch.setenv("H264MI_CHECK", "1")
+    monkeypatch.setenv("BENCH_DEP_MODE", "cols")
     monkeypatch.setenv("H264MI_CHECK_INJECT_REFCOLS", "6")
     streams = [gen.generate(2, 80 + i, nframes=6, w_mbs=22, h_mbs=6, crop_bottom=0, slices=2, gop=6)
                for i in range(3)]
@@ -110,12 +114,14 @@ def test_checker_catches_short_reference_columns(pipe, monkeypatch):
 
 
 def test_checker_catches_short_reference_rows(monkeypatch):
-    """Test hook H264MI_CHECK_INJECT_REFROWS: the host records every
-    partition's last reference row 64 rows short, so the frame-pipelined
-    launch's later pictures would read their reference before it is final;
-    the checker must report it (CHK_REFROW) from the loads' own geometry."""
+    """Test hook H264MI_CHECK_INJECT_REFROWS: the whole-row waits
+    (dep_wait_rows) wait for 64 rows fewer than the host recorded, so the
+    frame-pipelined launch's later pictures would read their reference
+    before it is final; the checker must report it (CHK_REFROW) from the
+    loads' own geometry."""
     import bench
     monkeypatch.setenv("H264MI_CHECK", "1")
+    monkeypatch.setenv("BENCH_DEP_MODE", "rows")
     monkeypatch.setenv("H264MI_CHECK_INJECT_REFROWS", "64")
     streams = [gen.generate(2, 70 + i, nframes=6, w_mbs=13, h_mbs=7, crop_bottom=0, slices=2, gop=6)
                for i in range(3)]

@@ -183,10 +183,12 @@ def test_engine_bench_streams_vs_reference(rpw, mc, monkeypatch):
     assert eng.errors() == 0
 
 
-@pytest.mark.parametrize("rank,pipe,staggered",
-                         [(r, 2, True) for r in range(8)] + [(0, 1, True), (1, 1, True), (0, 2, False), (1, 2, False),
-                                                             (0, 3, True), (1, 3, True), (0, 4, True)])
-def test_configs3_shard_vs_reference(rank, pipe, staggered):
+@pytest.mark.parametrize("rank,pipe,staggered,mode",
+                         [(r, 2, True, "") for r in range(8)] +
+                         [(0, 1, True, ""), (1, 1, True, ""), (0, 2, False, ""), (1, 2, False, ""),
+                          (0, 3, True, ""), (1, 3, True, ""), (0, 4, True, ""),
+                          (0, 3, True, "cols"), (1, 2, False, "cols"), (2, 4, True, "cols")])
+def test_configs3_shard_vs_reference(rank, pipe, staggered, mode, monkeypatch):
     """configs[3]: 64 streams, 8 per GPU.  Rank r's shard (seeds 100+8r ..
     100+8r+7, bench.shard_seeds) through bench.py's own device-resident path
     (bench.DeviceRun: records in HBM on the rank's engine, the next launch's
@@ -200,6 +202,8 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
     launch vs the reference MD5s, and after the run every frame slot's last
     picture."""
     import bench
+    if mode:
+        monkeypatch.setenv("BENCH_DEP_MODE", mode)
     seeds = bench.shard_seeds(rank, 8)
     n = 60
     _, caps = bench.prepare(3, seeds, n)
@@ -223,13 +227,17 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered):
         assert (ok, checked, missing) == (True, 8 * n, 0)
         assert run.check_resident(refs)[0]
         assert run.eng.errors() == 0
+        if pipe > 1:
+            # configs[3]'s off-picture motion: whole rows by the bench's choice
+            assert run.eng.last_deps() == {"cols": 2}.get(mode, 1)
     finally:
         run.free()
 
 
+@pytest.mark.parametrize("mode", ["rows", "cols"])
 @pytest.mark.parametrize("wh,pipe", [((13, 7), 2), ((12, 9), 2), ((20, 11), 2), ((13, 7), 3), ((20, 11), 4),
                                      ((24, 7), 3), ((8, 9), 2), ((3, 5), 3)])
-def test_engine_pipelined_steps_vs_oracle(wh, pipe):
+def test_engine_pipelined_steps_vs_oracle(wh, pipe, mode, monkeypatch):
     """Frame-pipelined launches (two to four consecutive pictures of each of
     3 streams per launch, physical slots renamed) on sizes whose luma rows do
     not end on 128-B lines (w % 8 != 0: a line holds two rows; w = 3: lines
@@ -237,6 +245,7 @@ def test_engine_pipelined_steps_vs_oracle(wh, pipe):
     rows are padded (H264MI_CPITCH), every picture vs the oracle's decode of
     the stream."""
     import bench
+    monkeypatch.setenv("BENCH_DEP_MODE", mode)
     w, h = wh
     streams = [gen.generate(2, 70 + i, nframes=10, w_mbs=w, h_mbs=h, crop_bottom=0, slices=2, gop=5)
                for i in range(3)]
@@ -254,6 +263,7 @@ def test_engine_pipelined_steps_vs_oracle(wh, pipe):
                 for s, k in enumerate(step):
                     got = run.eng.read(s, int(run.slot_of[k][s])).tobytes()
                     assert got == refs[s][k], f"stream {s} picture {k}"
+            assert run.eng.last_deps() == (1 if mode == "rows" else 2)
         assert run.eng.errors() == 0
     finally:
         run.free()
