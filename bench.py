@@ -310,15 +310,16 @@ def batch_ok(recs, pics, S, nmbs, ks):
 
 def golden_frames(config, seed, overrides):
     """The reference decoder's per-frame MD5s of generator stream (config,
-    seed) when a fixture covers it (overrides other than nframes: none)."""
-    if overrides:
-        return None
+    seed, overrides) when a fixture covers it (the fixture's overrides other
+    than nframes equal to `overrides`; the longest such fixture)."""
     gold = os.path.join(ROOT, "tests", "golden", "golden.json")
     if not os.path.exists(gold):
         return None
+    want = {k: v for k, v in (overrides or {}).items() if k != "nframes"}
     best = None
     for c in json.load(open(gold))["cases"].values():
-        if c["config"] == config and c["seed"] == seed and set(c["overrides"]) <= {"nframes"} \
+        ov = {k: v for k, v in c["overrides"].items() if k != "nframes"}
+        if c["config"] == config and c["seed"] == seed and ov == want \
                 and not c["no_reorder"] and (best is None or len(c["frames"]) > len(best)):
             best = c["frames"]
     return best
@@ -1057,33 +1058,49 @@ def ref_line_bytes(run, launch_ids):
     return tot
 
 
-def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0):
+def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0, overrides=None, pipe=1, dep=""):
     """One single-GPU measurement of another SURVEY §8d config with the same
-    step structure (records resident in HBM, one k_wgpp launch per step,
-    HIP events on every launch) and the same untimed verification against
-    the reference MD5s.  Returns a dict for the bench line."""
+    step structure (records resident in HBM, one k_wgpp launch per step --
+    `pipe` > 1: that many aligned steps per launch, dependency mode `dep`
+    forced or per launch by far_rows -- HIP events on every launch) and the
+    same untimed verification against the reference MD5s.  Returns a dict
+    for the bench line."""
     nframes = warmup + steps
-    streams, caps = prepare(config, seeds, nframes)
+    streams, caps = prepare(config, seeds, nframes, overrides)
     assert all(c.errors == 0 and c.npics >= nframes for c in caps), "leg stream preparation failed"
     S = len(caps)
     w, h = caps[0].w_mbs, caps[0].h_mbs
     # both knobs are read once, when the engine is created
-    os.environ["H264MI_MC_WAVES"] = str(mc_waves)
+    if pipe == 1:
+        os.environ["H264MI_MC_WAVES"] = str(mc_waves)
     if rpw:
         os.environ["H264MI_RPW"] = str(rpw)
+    saved_dep = os.environ.get("BENCH_DEP_MODE")
+    if dep:
+        os.environ["BENCH_DEP_MODE"] = dep
     try:
-        run = DeviceRun(L, caps, warmup, steps, 1, device=torch.cuda.current_device())
+        run = DeviceRun(L, caps, warmup, steps, pipe, device=torch.cuda.current_device())
     finally:
         os.environ.pop("H264MI_MC_WAVES", None)
         os.environ.pop("H264MI_RPW", None)
+        if dep:
+            if saved_dep is None:
+                os.environ.pop("BENCH_DEP_MODE", None)
+            else:
+                os.environ["BENCH_DEP_MODE"] = saved_dep
     try:
         dt, launch_us, sampled, _ = timed_run(run, None, torch, torch.cuda.synchronize, 1)
+        modes = sorted({run.dep_mode(i) for i in range(run.n_warm, len(run.launches)) if len(run.launches[i]) > 1})
         r_alg = alg_bytes(run, sampled) / max(len(sampled), 1)
-        refs = [golden_frames(config, sd, {}) for sd in seeds]
+        refs = [golden_frames(config, sd, overrides or {}) for sd in seeds]
         ok, n, missing, _ = run.verify(refs)
         gbs = r_alg / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
+        per_step = launch_us * len(sampled) / max(1, sum(len(run.launches[i]) for i in sampled))
         return {"size": f"{w * 16}x{h * 16}", "streams": S, "seeds": seeds, "steps": steps,
-                "mc_waves_per_row_workgroup": mc_waves,
+                **({"generator_overrides": overrides} if overrides else {}),
+                **({"steps_per_launch": run.P, "avg_kernel_us_per_step": round(per_step, 2),
+                    "dependency_modes": [{1: "rows", 2: "cols"}[m] for m in modes]} if pipe > 1 else {}),
+                "mc_waves_per_row_workgroup": mc_waves if pipe == 1 else 2,
                 "rows_per_workgroup": run.eng.rows_per_workgroup(S),
                 "frames_per_s": round(S * steps / dt, 1), "avg_launch_us": round(launch_us, 2),
                 "picture_latency_ms": round(launch_us / 1e3, 3),
@@ -1107,6 +1124,13 @@ def config_legs(L, torch):
         "cfg5_2160p_1stream_2mc": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2),
         "cfg5_2160p_1stream_2rows": run_leg(L, torch, 4, [100], 20, 4, rpw=2),
         "cfg5_2160p_1stream_2mc_2rows": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2, rpw=2),
+        # configs[3]'s rank-0 streams without off-picture motion: frame-pipelined
+        # launches on (MB row, MB column) waits (chosen per launch), and forced
+        # to whole rows beside it
+        "cfg3_realistic_motion_8streams": run_leg(L, torch, 3, list(range(100, 108)), 54, 3,
+                                                  overrides={"offpic_pct": 0}, pipe=3),
+        "cfg3_realistic_motion_8streams_rows": run_leg(L, torch, 3, list(range(100, 108)), 54, 3,
+                                                       overrides={"offpic_pct": 0}, pipe=3, dep="rows"),
     }
 
 

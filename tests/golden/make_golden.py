@@ -116,6 +116,11 @@ CASES["leg_cfg5_2160p_s100"] = (4, 100, dict(nframes=24), False)
 # seeds 100 + 8r .. 100 + 8r + 7 (tests/test_gpu_parity.py decodes each shard)
 for s in range(100, 164):
     CASES[f"bench_1080p_s{s}"] = (3, s, dict(nframes=60), False)
+# bench.py leg `cfg3_realistic_motion`: rank 0's streams without off-picture
+# motion (the generator's offpic_pct = 0), where frame-pipelined launches
+# wait on (MB row, MB column) cells
+for s in range(100, 108):
+    CASES[f"bench_1080p_offpic0_s{s}"] = (3, s, dict(nframes=60, offpic_pct=0), False)
 
 
 def find_patch(stream: bytes):

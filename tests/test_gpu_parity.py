@@ -234,6 +234,30 @@ def test_configs3_shard_vs_reference(rank, pipe, staggered, mode, monkeypatch):
         run.free()
 
 
+@pytest.mark.parametrize("pipe", [2, 3])
+def test_realistic_motion_shard_vs_reference(pipe):
+    """configs[3]'s rank-0 streams without off-picture motion (bench leg
+    cfg3_realistic_motion): aligned frame-pipelined launches, whose
+    dependency mode the bench picks per launch -- (MB row, MB column) cells
+    here -- every picture vs the reference MD5s."""
+    import bench
+    seeds = bench.shard_seeds(0, 8)
+    n = 60
+    ov = {"offpic_pct": 0}
+    _, caps = bench.prepare(3, seeds, n, ov)
+    run = bench.DeviceRun(_lib.mi(), caps, 3, 54 if pipe == 3 else 56, pipe)
+    try:
+        assert run.P == pipe
+        refs = [bench.golden_frames(3, sd, ov) for sd in seeds]
+        assert all(r is not None and len(r) == n for r in refs)
+        ok, checked, missing, _ = run.verify(refs)
+        assert run.eng.last_deps() == 2
+        assert ok and missing == 0 and checked > 0
+        assert run.eng.errors() == 0
+    finally:
+        run.free()
+
+
 @pytest.mark.parametrize("mode", ["rows", "cols"])
 @pytest.mark.parametrize("wh,pipe", [((13, 7), 2), ((12, 9), 2), ((20, 11), 2), ((13, 7), 3), ((20, 11), 4),
                                      ((24, 7), 3), ((8, 9), 2), ((3, 5), 3)])

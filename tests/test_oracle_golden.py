@@ -8,7 +8,7 @@ from _golden import cases, md5s, stream
 
 CASES = cases()
 FAST = [n for n in CASES if not n.startswith(("bench_", "leg_"))] + ["bench_1080p_s100", "bench_1080p_s105",
-                                                                     "leg_cfg2_720p_s1"]
+                                                                     "leg_cfg2_720p_s1", "bench_1080p_offpic0_s100"]
 
 
 @pytest.mark.parametrize("name", FAST)
