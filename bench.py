@@ -1124,6 +1124,8 @@ def config_legs(L, torch):
         "cfg5_2160p_1stream_2mc": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2),
         "cfg5_2160p_1stream_2rows": run_leg(L, torch, 4, [100], 20, 4, rpw=2),
         "cfg5_2160p_1stream_2mc_2rows": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2, rpw=2),
+        # the single 4K stream with three consecutive pictures per launch
+        "cfg5_2160p_1stream_pipe3": run_leg(L, torch, 4, [100], 21, 3, pipe=3),
         # configs[3]'s rank-0 streams without off-picture motion: frame-pipelined
         # launches on (MB row, MB column) waits (chosen per launch), and forced
         # to whole rows beside it
@@ -1193,7 +1195,9 @@ def main(argv=None):
     launch_bytes = alg_bytes(run, sampled) / max(len(sampled), 1)
     launch_ref_lines = ref_line_bytes(run, sampled) / max(len(sampled), 1)
     achieved = launch_bytes / (step_us * 1e-6) / 1e9 if step_us > 0 else 0.0
-    traffic = load_traffic()
+    # the committed PMC passes measured the default workload (configs[3], 8 streams, this
+    # pipe depth): another config or stream count reports traffic null, never that one's
+    traffic = load_traffic() if (a.config == 3 and a.streams == 8 and not a.gen and not a.aligned) else None
     frame_read_gbs = alg_bytes(run, range(run.n_warm, len(run.launches))) * world / dt / 1e9
 
     # the same streams with aligned GOPs, timed window P pictures only (the
@@ -1250,9 +1254,11 @@ def main(argv=None):
         # E2E_PIN A/B, profiles/r80_e2e_pin.txt: 4.53-4.68 vs 4.97-5.70 ms of
         # host CPU per picture, and steadier)
         # one-device rehearsal (BENCH_ONE_DEVICE=1): every rank's processes
-        # share one GPU, which admits 16 GPU processes -- fewer per rank
+        # share one GPU, which admits 16 GPU processes -- the ranks, their
+        # decoder processes and each rank's one-process shared-engine run
+        # (ranks finish at different times) stay within that
         procs = MAX_E2E_PROCS if os.environ.get("BENCH_ONE_DEVICE") != "1" or world == 1 \
-            else max(1, (16 - world) // world)
+            else max(1, (16 - 2 * world) // world - 1)
         e2e = end_to_end(streams, nframes, device=local, cpus=my_cpus if my_cpus else None, max_procs=procs,
                          release=dist.barrier if dist else None)
     if dist:

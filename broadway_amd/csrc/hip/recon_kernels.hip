@@ -1469,14 +1469,9 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     }
     unsigned long long *const sink = a.gjunk + ((p * H + r) & 127) * 64 + lane;
     const bool wt = COLP && pubp;       // write-through frame stores + progress granules
-#ifdef STUDY_COLP_PLAIN
-    const bool wst = false;             // study build (output not valid): plain frame stores
-#else
-    const bool wst = wt;
-#endif
     unsigned long long *const prog_me = PROG_AT(a.prog, p, H, r, w);
     auto fst = [&](void *ptr, uint32_t v) {
-        if (wst) st32<true>(ptr, v);
+        if (wt) st32<true>(ptr, v);
         else st32<false>(ptr, v);
     };
 
@@ -1496,9 +1491,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         if (wt && c >= 2 && ((c >> 1) % PROG_EVERY) == 0) {
             // MB c - 2's write-through stores (issued one MB of the partner
             // earlier) drained: publish this wave's progress, off the chain
-#ifndef STUDY_COLP_NOWAIT
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
             if (lane == 0) st_gran(prog_me, (uint32_t)c, tag);
         }
         if (prof) tc0 = clock64();
@@ -2023,15 +2016,8 @@ __device__ __forceinline__ void dep_wait_cols(const ReconArgs &a, int p, int mb,
         if (!okl) okl = dep_rows_ok(a, p, kl, lrlo, lrhi, lx, pass > 0, pc);
         if (!okc) okc = dep_rows_ok(a, p, kc, crlo, crhi, cx, pass > 0, pc);
         if (__builtin_amdgcn_ballot_w64(!(okl && okc)) == 0) break;
-#ifdef STUDY_DEP_POLLONCE
-        if (pass > 0) break;                // study build (output not valid): one poll, never wait
-#endif
         if (pass > 0) {
-#ifdef DEP_SLEEP_LONG
-            __builtin_amdgcn_s_sleep(32);       // ~0.85 us: about one MB of the producer's row
-#else
             __builtin_amdgcn_s_sleep(4);
-#endif
             if (++spins > (1u << 21)) { if (lane == 0) atomicOr(a.err + p, 32u); break; }
         }
     }

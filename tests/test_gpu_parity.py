@@ -245,7 +245,7 @@ def test_realistic_motion_shard_vs_reference(pipe):
     n = 60
     ov = {"offpic_pct": 0}
     _, caps = bench.prepare(3, seeds, n, ov)
-    run = bench.DeviceRun(_lib.mi(), caps, 3, 54 if pipe == 3 else 56, pipe)
+    run = bench.DeviceRun(_lib.mi(), caps, pipe, 60 - pipe - (60 - pipe) % pipe, pipe)
     try:
         assert run.P == pipe
         refs = [bench.golden_frames(3, sd, ov) for sd in seeds]
