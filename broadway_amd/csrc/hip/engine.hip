@@ -403,6 +403,10 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     // vs 303.9 us per step, 4 of 4 rounds)
     static const int mc_urg = getenv("H264MI_MC_URGENCY") ? atoi(getenv("H264MI_MC_URGENCY")) : 0;
     a.mc_urgency = mc_urg > 0 ? mc_urg : P > 2 ? 12 : 8;
+    // study knob: the top MB rows' urgent MC waves at the row waves' priority
+    // (H264MI_MC_TOP rows; 0 = off)
+    static const int mc_top = getenv("H264MI_MC_TOP") ? atoi(getenv("H264MI_MC_TOP")) : 0;
+    a.mc_top = mc_top;
     a.chk_inject = e->check ? e->check_inject : 0;
     a.chk_short_cols = e->check ? e->check_short_cols : 0;
     a.chk_short_rows = e->check ? e->check_short_rows : 0;

@@ -79,6 +79,7 @@ struct ReconArgs {
     // publish); 0 = 3 throughout
     int row_prio_split;
     int mc_urgency;          // MBs ahead of the row's deblocking under which MC waves issue at prio 2 (2-MC shape)
+    int mc_top;              // MB rows r < mc_top: urgent MC waves issue at prio 3 (the row waves' level)
     // dependency-checker builds (k_wgpp<..., CHK = true>): test hook that
     // deliberately breaks one hand-off so the tests can see the checker fire
     // (0: none; 1: MB 5 of every row hands the row waves a wrong ring tag)
@@ -1747,7 +1748,7 @@ struct McLoad {
 __device__ __forceinline__ uint32_t rec_dw(uint32_t v0, int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v0, i); }
 
 __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, int p, int mb, uint32_t v0, int lane,
-                                         McLoad &L)
+                                         McLoad &L, uint32_t *tsd = nullptr)
 {
     // k_prep outputs are indexed by the MB's position in the batch (picture p
     // of the launch), not by PicDesc.rec_base: records may sit anywhere in
@@ -1767,6 +1768,7 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
         L.l_x0 = mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2;
         const int l_y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
         L.l_ax = clip3(0, W16 - 12, L.l_x0 & ~3);
+        if (tsd) tsd[0] = (uint32_t)wall_clock64();
         {
             const uint8_t *ref = a.frames + (unsigned long long)(pd.frame_base + ((refs >> ((lb >> 2) * 8)) & 255)) * a.frame_bytes;
 #pragma unroll
@@ -1777,6 +1779,7 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
                 L.lw[k][0] = t.x; L.lw[k][1] = t.y; L.lw[k][2] = t.z;
             }
         }
+        if (tsd) tsd[1] = (uint32_t)wall_clock64();
         const int cb = (lane & 31) >> 1, ccomp = lane & 1;
         const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
         const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
@@ -1796,6 +1799,7 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
             }
         }
     }
+    if (tsd) tsd[2] = (uint32_t)wall_clock64();
     L.dbw = ldg32(pdb, (uint32_t)(lane & 15) * 4);
     L.r0 = L.r1 = L.r2 = L.r3 = 0;
     // lane 2b + h (< 48) takes rows 2h, 2h+1 of block bit b: 16 B of the
@@ -2321,7 +2325,16 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
         const int slot = c & (RK - 1);
         // claim the next MB now and fetch its record
         const int cn = next_mb(c);
+        // conditional: the waitcnt pass then makes mc_finish wait for this
+        // fresh load too (vmcnt(0)), which measured faster than letting the MC
+        // run on (an unconditional, clamped load: vmcnt(1), 317 vs 301 us per
+        // step, profiles/r119_ab_nv0.txt) -- the MC waves' pace is not what
+        // binds, their share of the CU is
+#ifndef MC_NV0_UNCOND
         const uint32_t nv0 = cn < a.w ? recrow[(size_t)cn * 24 + (lane < 24 ? lane : 0)] : 0;
+#else
+        const uint32_t nv0 = recrow[(size_t)min(cn, a.w - 1) * 24 + (lane < 24 ? lane : 0)];
+#endif
         if (c >= lead0) {
             // slot free (ring depth) and at most lead MBs ahead; before the
             // row's chain has begun (consumed < 1: MB 1 not taken yet) at
@@ -2345,8 +2358,10 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             // whose deblocking is far off -- the rows sharing a CU all start
             // their MC at once, and the top rows' MC gates their chains
             // (measured: P-only 350 vs 354 us per launch; 3 MC waves: slower)
-            if (c - __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < a.mc_urgency) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
+            if (c - __builtin_amdgcn_readfirstlane(lds_ld(&R.consumed)) < a.mc_urgency) {
+                if (r < a.mc_top) __builtin_amdgcn_s_setprio(3);
+                else __builtin_amdgcn_s_setprio(2);
+            } else __builtin_amdgcn_s_setprio(0);
         }
         // PROF stamps [4] / [5] of inter MBs (intra MBs: mc_intra's): loads
         // landed (a drain the normal kernel leaves to the loads' first use),
@@ -2395,7 +2410,21 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 6] = wall_clock64() - tdw;
         if (DEPM == DEP_COLS && CHK && c < a.w && D.n) chk_ref_rows(a, p, r * a.w + c, v0, lane, D);
         if (DEPM == DEP_ROWS && CHK && c < a.w && D.n) chk_ref_rows_rows(a, p, r * a.w + c, v0, lane, D);
-        if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld);
+        const unsigned long long tis = PROF ? wall_clock64() : 0;
+        uint32_t tsd[3] = {0, 0, 0};
+        if (c < a.w) mc_issue(a, pd, p, r * a.w + c, v0, lane, ld, PROF ? tsd : nullptr);
+        // PROF stamp [7] of the next MB: its loads' issue began (bits 0..31) / ended (32..63)
+        if (PROF && c < a.w && lane == 0) {
+            const unsigned long long te = wall_clock64();
+            a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 7] =
+                (tis & 0xFFFFFFFFull) | (te << 32);
+            // [6] with one step per launch (no dependency wait): issue phases, 16 bits each
+            // (100 MHz ticks from the issue start): address set-up, luma loads, chroma loads
+            if (DEPM == DEP_NONE)
+                a.prof[(size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 6] =
+                    (unsigned long long)((tsd[0] - (uint32_t)tis) & 0xFFFF) | ((unsigned long long)((tsd[1] - (uint32_t)tis) & 0xFFFF) << 16) |
+                    ((unsigned long long)((tsd[2] - (uint32_t)tis) & 0xFFFF) << 32);
+        }
     }
 }
 
