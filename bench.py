@@ -626,7 +626,22 @@ def load_ubench():
         return json.load(f)
 
 
-def latency_floor(w_mbs, h_mbs, steps, ub, launch_us):
+def load_dep_floor(cfg, streams, steps, gen):
+    """The data-dependent launch floor (tools/dep_sim.py with the lone-wave
+    costs -> profiles/dep_floor.json) when this run's workload is the one it
+    simulated, else None."""
+    p = os.path.join(ROOT, "profiles", "dep_floor.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    wl = d.get("workload", {})
+    if (wl.get("config"), wl.get("streams"), wl.get("steps_per_launch")) != (cfg, streams, steps) or gen or wl.get("gen_overrides"):
+        return None
+    return d
+
+
+def latency_floor(w_mbs, h_mbs, steps, ub, launch_us, dep=None):
     """The row chain's latency floor, beside the HBM
     roofline: a picture cannot finish before its last row has run W MBs of
     lone-wave vertical + horizontal passes after H - 1 row-to-row hand-offs,
@@ -649,7 +664,14 @@ def latency_floor(w_mbs, h_mbs, steps, ub, launch_us):
             "launch_floor_us": round(floor, 2), "steps_per_launch": steps,
             "measured_launch_us": round(launch_us, 2),
             "frac": round(floor / launch_us, 4) if launch_us else None,
-            "source": ub.get("source", "profiles/ubench.json")}
+            "source": ub.get("source", "profiles/ubench.json"),
+            # the same lone-wave costs with this workload's own data
+            # dependencies between the pictures of a launch (a later picture's
+            # MBs wait for the reference rows their windows read)
+            "data_dependent_launch_floor_us": dep["launch_us"]["row"] if dep else None,
+            "data_dependent_frac": round(dep["launch_us"]["row"] / launch_us, 4) if dep and launch_us else None,
+            "data_dependent_source": "profiles/dep_floor.json (tools/dep_sim.py, rows rule, lone-wave period and lag)"
+            if dep else None}
 
 
 def load_traffic():
@@ -1346,7 +1368,8 @@ def main(argv=None):
                          "traffic_source": traffic.get("source") if traffic else None,
                          # the bound this kernel actually has: the row chain's latency
                          "latency": latency_floor(w, h, P, load_ubench(),
-                                                  (split["p"][1] if split and split["p"][0] else step_us))},
+                                                  (split["p"][1] if split and split["p"][0] else step_us),
+                                                  load_dep_floor(a.config, a.streams, P, a.gen))},
             "kernels": {"k_wgpp": {"avg_launch_us": round(step_us, 2),
                                    "pictures_per_launch": round(S * a.steps / max(launches_timed, 1), 2),
                                    "steps_per_launch": P,

@@ -1607,6 +1607,11 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         // (measured: reading the left halo straight from the partner's region
         // inside V and releasing it after the MB
         // edge was 3 us per launch slower than this copy)
+#ifdef STUDY_V_DELAY
+        // study build: lengthen the vertical pass (the own chain only: the
+        // hand-off to the row below leaves after H)
+        __builtin_amdgcn_s_sleep(STUDY_V_DELAY);
+#endif
         if (dbf) deblock_dir(0, Pv, G.ry, G.ru, G.rv, junk, lane, vpre, c > 0, vhalo);
         wave_sync();
         PPT(1);
@@ -1632,6 +1637,11 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             deblock_dir(1, Ph, G.ry, G.ru, G.rv, junk, lane);
             wave_sync();
         }
+#ifdef STUDY_CHAIN_DELAY
+        // study build: lengthen the in-row chain by a fixed delay per MB (how
+        // much of the own chain reaches the launch time)
+        __builtin_amdgcn_s_sleep(STUDY_CHAIN_DELAY);
+#endif
         if (lane == 0) lds_st(&L.hdone, c + 1);
         if (prof && lane == 0) tvd = wall_clock64();
         PPT(2);

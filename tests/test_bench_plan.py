@@ -145,3 +145,19 @@ def test_device_run_pipe3_idr_last():
                 slots = [run.slot_of[st[s]][s] for st in launch]
                 assert len(set(slots)) == len(slots)
         run.free()
+
+
+def test_latency_floors_from_committed_profiles():
+    """roofline.latency: the lone-wave picture floor (profiles/ubench.json)
+    and the data-dependent launch floor (profiles/dep_floor.json), the latter
+    only for the workload it was simulated on."""
+    ub = bench.load_ubench()
+    assert ub is not None
+    dep = bench.load_dep_floor(3, 8, 3, "")
+    assert dep is not None and dep["launch_us"]["none"] <= dep["launch_us"]["row"]
+    assert bench.load_dep_floor(4, 1, 3, "") is None and bench.load_dep_floor(3, 8, 3, "offpic_pct=0") is None
+    lf = bench.latency_floor(120, 68, 3, ub, 883.0, dep)
+    assert abs(lf["picture_floor_us"] - (120 * ub["vh_us"] + 67 * (ub["patch_us"] + ub["hop_same_xcd_us"]))) < 0.01
+    assert lf["launch_floor_us"] < lf["data_dependent_launch_floor_us"] < 883.0
+    assert abs(lf["data_dependent_frac"] - dep["launch_us"]["row"] / 883.0) < 1e-3
+    assert bench.latency_floor(120, 68, 3, ub, 883.0)["data_dependent_frac"] is None

@@ -100,6 +100,17 @@ def main():
             ends.append(max(T[h - 1, w - 1] for T in Ts))
         out[rule] = np.mean(ends)
         print(f"{rule:7s} launch of {P} steps: {out[rule]:7.1f} us = {out[rule] / P:6.1f} per step (mean over {S} streams)")
+    if os.environ.get("SIM_JSON"):
+        # the data-dependent latency floor bench.py quotes beside its own
+        # (roofline.latency.data_dependent_*), for the workload simulated here
+        import json
+        with open(os.environ["SIM_JSON"], "w") as f:
+            json.dump({"workload": {"config": 3, "streams": S, "steps_per_launch": P, "pictures": [K0, K0 + P - 1],
+                                    "gen_overrides": ov},
+                       "period_us": PER, "lag_us": LAG,
+                       "launch_us": {k: round(v, 1) for k, v in out.items()},
+                       "source": "tools/dep_sim.py (SIM_PERIOD / SIM_LAG: the lone-wave costs of profiles/ubench.json)"},
+                      f, indent=1)
 
 
 if __name__ == "__main__":
