@@ -2560,7 +2560,9 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
             if (lane == 0) last = __hip_atomic_fetch_add(&L[q].fin, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             last = __builtin_amdgcn_readfirstlane(last);
             if (last == 1 && lane == 0) {
+#ifndef STUDY_NO_WBL2
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 st_sc1_u32(a.done + (size_t)p * a.h + r, a.epoch);
             }

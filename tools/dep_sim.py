@@ -10,6 +10,7 @@ steps of the launch are final, under three rules:
   row      rows 0..R+1 of the producer complete (the round-4 row tags)
   column   rows R_lo..R_hi through MB column X (+1 for the store lag) and row
            R_hi + 1 through X (recon_kernels.hip dep_wait)
+  picture  the whole producer picture (one release per picture)
 R_lo, R_hi, X are the lines of each MB's MC windows (mc_issue's geometry).
 Prints the launch time per rule for SIM_P steps of SIM_S streams."""
 import os
@@ -68,7 +69,7 @@ def main():
     _, caps = bench.prepare(3, seeds, K0 + P, {k: int(v) for k, v in ov.items()})
     w, h = caps[0].w_mbs, caps[0].h_mbs
     out = {}
-    for rule in ("none", "row", "column"):
+    for rule in ("none", "row", "column", "picture"):
         ends = []
         for cap in caps:
             Ts, slots = [], []
@@ -84,7 +85,10 @@ def main():
                         hit = inter[:, None] & (slot == slots[jj])
                         if not hit.any():
                             continue
-                        if rule == "row":
+                        if rule == "picture":
+                            # the whole producer picture complete
+                            t = np.where(hit, Tp[h - 1, w - 1], 0.0)
+                        elif rule == "row":
                             # rows 0..R_hi+1 complete: the last of them is the latest
                             rr = np.minimum(rhi + 1, h - 1)
                             t = np.where(hit, Tp[rr, w - 1], 0.0)
