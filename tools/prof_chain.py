@@ -233,3 +233,12 @@ if os.environ.get("PROF_ROW0"):
     print(f"row {r0}: c type  mc.start  mc.final  V.start  H.end")
     for c in range(w):
         print(f"{c:3d} {int(types[0, r0, c]):2d} {M0[:, r0, c].mean():8.1f} {M1[:, r0, c].mean():8.1f} {A[:, r0, c].mean():8.1f} {D[:, r0, c].mean():8.1f}")
+
+# the MC chain's wavefront (intra pictures): slot-final of MB (r, c) against
+# (r-1, c) -- the row lag of the intra prediction -- and against (r, c-1)
+if im.any():
+    rl = (M1[:, 2:h, 2] - M1[:, 1:h - 1, 2])
+    st("intra MC row lag (slot final, column 2)", rl.ravel())
+    rlc = (M1[:, 2:h, 2:w - 2] - M1[:, 1:h - 1, 2:w - 2])
+    st("intra MC row lag (all columns)", rlc.ravel())
+    print(f"  MC slot-final of the last MB: {M1[:, h - 1, w - 1].mean():.1f} us; deblock row {h - 2} end {D[:, h - 2, w - 1].mean():.1f} us")
