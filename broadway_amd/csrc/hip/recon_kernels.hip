@@ -957,7 +957,13 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, const int b
     const int m0 = (int)__builtin_amdgcn_sad_u8((uint32_t)p0, (uint32_t)q0, (uint32_t)-alpha);
     const int m1 = (int)__builtin_amdgcn_sad_u8((uint32_t)p1, (uint32_t)p0, (uint32_t)-beta);
     const int m2 = (int)__builtin_amdgcn_sad_u8((uint32_t)q1, (uint32_t)q0, (uint32_t)-beta);
+#ifndef FILT_SHORTCIRCUIT
+    // (bitwise: a short-circuit && became an exec-masked block around the
+    // sign test -- scalar exec bookkeeping on the chain, every edge)
+    const bool f = (bS != 0) & (max(m0, max(m1, m2)) < 0);
+#else
     const bool f = bS != 0 && max(m0, max(m1, m2)) < 0;
+#endif
     const bool ap = absd(p2, p0) < beta_ap, aq = absd(q2, q0) < beta_ap;
     // bS < 4
     const int tc0 = (int)__builtin_amdgcn_ubfe(tcs, (uint32_t)bS << 3, 8);    // bS = 4: offset 32 -> byte 0 (unused)
@@ -976,7 +982,7 @@ __device__ __forceinline__ void filt_line(int (&v)[20], const int k, const int b
     int r_q0 = f ? n_q0 : q0;
     if (MBEDGE) {
         // bS == 4: MB edges next to intra MBs only -- skipped unless some lane needs it
-        const bool b4 = f && bS >= 4;
+        const bool b4 = f & (bS >= 4);
         if (__builtin_amdgcn_ballot_w64(b4) != 0) {
             const int p3 = v[o], q3 = v[o + 7];
             const bool strong = d0 < ((alpha >> 2) + 2);
