@@ -243,10 +243,25 @@ __device__ void itrans4(int16_t *d)
     }
 }
 
+// the job lives in pinned host memory mapped into the device: one coalesced
+// read into LDS, the primitive on the LDS copy, one coalesced write back --
+// no H2D / D2H copies around the launch
+__device__ void k_omx_body(OmxJob &j, int t);
 __global__ __launch_bounds__(256) void k_omx(OmxJob *jp)
 {
-    OmxJob &j = *jp;
+    __shared__ OmxJob js;
+    static_assert(sizeof(OmxJob) % 4 == 0, "OmxJob copied in dwords");
     const int t = threadIdx.x;
+    const uint32_t *src = (const uint32_t *)jp;
+    uint32_t *dst = (uint32_t *)&js;
+    for (int i = t; i < (int)(sizeof(OmxJob) / 4); i += 256) dst[i] = src[i];
+    __syncthreads();
+    k_omx_body(js, t);
+    __syncthreads();
+    for (int i = t; i < (int)(sizeof(OmxJob) / 4); i += 256) ((uint32_t *)jp)[i] = dst[i];
+}
+__device__ void k_omx_body(OmxJob &j, int t)
+{
     switch (j.op) {
     case OP_I4:
         if (t < 16) j.out[t] = (uint8_t)i4_pixel(j, t & 3, t >> 2);
@@ -338,13 +353,12 @@ __global__ __launch_bounds__(256) void k_omx(OmxJob *jp)
 // ---- host side: one job per call on the thread's own stream
 struct OmxCtx {
     hipStream_t st = nullptr;
-    OmxJob *h = nullptr, *d = nullptr;
+    OmxJob *h = nullptr, *d = nullptr;      // pinned host job, its device address
     int ok = 0;
     ~OmxCtx()
     {
         if (st) (void)hipStreamDestroy(st);
         if (h) (void)hipHostFree(h);
-        if (d) (void)hipFree(d);
     }
 };
 thread_local OmxCtx g_ctx;
@@ -354,8 +368,8 @@ OmxJob *job_begin(int op)
     OmxCtx &c = g_ctx;
     if (!c.ok) {
         if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess ||
-            hipHostMalloc(&c.h, sizeof(OmxJob), hipHostMallocDefault) != hipSuccess ||
-            hipMalloc(&c.d, sizeof(OmxJob)) != hipSuccess)
+            hipHostMalloc(&c.h, sizeof(OmxJob), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&c.d, c.h, 0) != hipSuccess)
             return nullptr;
         c.ok = 1;
     }
@@ -364,14 +378,12 @@ OmxJob *job_begin(int op)
     return c.h;
 }
 
-// H2D of the job, k_omx, D2H; 0 or BadArgErr-independent failure (-1)
+// k_omx on the mapped job, waited for; 0 or BadArgErr-independent failure (-1)
 int job_run()
 {
     OmxCtx &c = g_ctx;
-    if (hipMemcpyAsync(c.d, c.h, sizeof(OmxJob), hipMemcpyHostToDevice, c.st) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_omx, dim3(1), dim3(256), 0, c.st, c.d);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (hipMemcpyAsync(c.h, c.d, sizeof(OmxJob), hipMemcpyDeviceToHost, c.st) != hipSuccess) return -1;
     return hipStreamSynchronize(c.st) == hipSuccess ? 0 : -1;
 }
 
