@@ -515,14 +515,24 @@ def end_to_end(streams, nframes, reps=E2E_REPS, device=0, cpus=None, max_procs=M
                 f.write(s)
             procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T", "-G"] + pin + [pth], stdin=subprocess.PIPE,
                                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
-        # start gate: wait until every process has warmed up, then release all
+        # start gate: wait until every process has warmed up, then release all.
+        # The ranks' barrier (release) is reached on every path, a failed
+        # warm-up included, so that no other rank waits in it forever
+        failed = None
         for pr in procs:
             line = pr.stdout.readline()
             if line.strip() != "ready":
-                pr.wait(timeout=60)
-                raise RuntimeError(f"h264mi_dec not ready: {line!r} {pr.stderr.read().strip()[-300:]}")
+                failed = (pr, line)
+                break
         if release is not None:
             release()
+        if failed is not None:
+            for pr in procs:
+                if pr.poll() is None:
+                    pr.kill()
+            pr, line = failed
+            pr.wait(timeout=60)
+            raise RuntimeError(f"h264mi_dec not ready: {line!r} {pr.stderr.read().strip()[-300:]}")
         for pr in procs:
             pr.stdin.write("g")
             pr.stdin.flush()
@@ -1291,7 +1301,11 @@ def main(argv=None):
             # all ranks' processes released together (the barrier in the
             # start gate): every rank's pictures over the union of all windows
             # (CLOCK_MONOTONIC is one clock on the host)
-            span = max(x["t_end_mono"] for x in e2es) - min(x["t_start_mono"] for x in e2es)
+            # (a rank whose processes reported no window: its longest single window)
+            if all(x.get("t_start_mono") is not None and x.get("t_end_mono") is not None for x in e2es):
+                span = max(x["t_end_mono"] for x in e2es) - min(x["t_start_mono"] for x in e2es)
+            else:
+                span = max(x["seconds"] for x in e2es)
             e2e = {"value": round(sum(x["pictures"] for x in e2es) / span, 2),
                    "seconds": round(span, 6), "window": "union of every rank's decode windows, common start gate",
                    "unit": "frames/s", "n_gpus": world,

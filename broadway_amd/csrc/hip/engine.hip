@@ -384,7 +384,8 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         e->epoch = 1;
     }
     a.epoch = e->epoch;
-    a.prof = e->d_prof;
+    // (a launch of more pictures than the stamp buffer holds runs unstamped)
+    a.prof = e->d_prof && (size_t)npics * ((size_t)e->h * 16 + (size_t)e->nmbs * PROF_MB) <= e->prof_cap ? e->d_prof : nullptr;
     a.prof_mode = e->d_prof && getenv("H264MI_PROF_MODE") ? atoi(getenv("H264MI_PROF_MODE")) : 0;
     // study knobs: MC lead over the row's deblocking (MBs; 0 / unset = the
     // ring depth), before the chain has begun (LEAD0, at least 4) and after
@@ -669,6 +670,18 @@ extern "C" int h264mi_kernel_occupancy(int *blocks_per_cu, int *lds_bytes, int *
     return 0;
 }
 
+// the profiling kernels' stamp buffer, sized for the engine's current
+// picture capacity (every picture of a launch: per-row and per-MB stamps)
+static int prof_alloc(h264mi_engine *e)
+{
+    (void)hipFree(e->d_prof);
+    e->d_prof = NULL;
+    e->prof_cap = (size_t)e->pipe_cap * e->h * 16 + (size_t)e->pipe_cap * e->nmbs * PROF_MB;
+    HIPCHECK(hipMalloc(&e->d_prof, sizeof(unsigned long long) * e->prof_cap));
+    HIPCHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * e->prof_cap));
+    return 0;
+}
+
 extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)
 {
     // (frame-pipelined launches name the earlier steps' target slots in a
@@ -683,6 +696,9 @@ extern "C" int h264mi_engine_set_steps(h264mi_engine *e, int steps)
     e->steps = steps;
     e->prepped_rec = NULL; e->prepped_pics = NULL;
     e->prep_parity = 0;
+    // a profiling buffer allocated for the old capacity would be overrun by
+    // the stamps of a launch of more pictures: resize it with the capacity
+    if (e->d_prof && prof_alloc(e)) return -1;
     HIPCHECK(hipStreamSynchronize(e->st));
     return 0;
 }
@@ -825,9 +841,7 @@ extern "C" int h264mi_engine_profile(h264mi_engine *e, int enable, unsigned long
                            hipMemcpyDeviceToHost));
     }
     if (enable && !e->d_prof) {
-        e->prof_cap = (size_t)e->pipe_cap * e->h * 16 + (size_t)e->pipe_cap * e->nmbs * PROF_MB;
-        HIPCHECK(hipMalloc(&e->d_prof, sizeof(unsigned long long) * e->prof_cap));
-        HIPCHECK(hipMemset(e->d_prof, 0, sizeof(unsigned long long) * e->prof_cap));
+        if (prof_alloc(e)) return -1;
     } else if (!enable && e->d_prof) {
         HIPCHECK(hipStreamSynchronize(e->st));
         (void)hipFree(e->d_prof);

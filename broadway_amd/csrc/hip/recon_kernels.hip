@@ -357,77 +357,117 @@ __device__ void mb_residual(const MbRec &r, const int16_t *base, int16_t *res,
 }
 
 // ---------------------------------------------------------------------------
-// inter prediction (reconstruct.c:1819-1941): luma 6-tap from a 9x9 window
-// per 4x4 block, chroma bilinear from a 3x3 window per 2x2 block.
+// inter prediction (h264bsdPredictSamples, reconstruct.c:1819-1941): luma
+// 6-tap from a 9x9 window per 4x4 block (the 16 positions of
+// h264bsdInterpolate*, :1004-1381), chroma bilinear from a 3x3 window per
+// 2x2 block (h264bsdInterpolateChromaHorVer and friends, :302-404).
+//
+// Packed arithmetic (round 6): four samples travel as the bytes of one
+// dword, two intermediate values as the 16-bit halves of one (v_pk_*_i16),
+// and the 6-tap sums are dot products:
+//   - horizontal half samples b of a row: v_dot4_i32_i8 of the row's bytes
+//     (biased by ^0x80 into int8; sum of taps 32 -> +4096) with the taps
+//     shifted to each output column, 9 dot products for 4 outputs;
+//   - vertical 6-tap sums V of columns 0..8 over the lane's six window rows:
+//     one v_pk_mad_i16 chain per column pair (u8 pairs from v_perm_b32);
+//   - centre j = the horizontal 6-tap over V (exact: the filter is linear),
+//     v_dot2_i32_i16 on the column pairs, 3-4 per output;
+//   - every output is (A + B + 1) >> 1 of two of {G, b, h, j} (A = B for
+//     the full / half positions): one v_lerp_u8 for the lane's four samples.
+// What no lane of the wave needs (b of row +0 / +1, h of column +0 / +1, j)
+// is skipped wave-uniformly: most inter MBs carry one MV (skip, 16x16), so
+// their waves compute one or two candidates.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int tap6(int a, int b, int c, int d, int e, int f)
+typedef short s2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s2v s2of(uint32_t x) { return __builtin_bit_cast(s2v, x); }
+__device__ __forceinline__ uint32_t uof(s2v x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) { return __builtin_amdgcn_perm(hi, lo, sel); }
+// two 16-bit lanes clipped to [0, 255] (v_pk_max_i16, v_pk_min_i16)
+__device__ __forceinline__ s2v clip_pk(s2v v)
 {
-    return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
+    return __builtin_elementwise_min(__builtin_elementwise_max(v, (s2v){0, 0}), (s2v){255, 255});
+}
+// the low bytes of two clipped pairs -> four bytes (lo.x, lo.y, hi.x, hi.y)
+__device__ __forceinline__ uint32_t pack4(s2v lo, s2v hi) { return perm(uof(hi), uof(lo), 0x06040200u); }
+// four clipped int32 -> four bytes
+__device__ __forceinline__ uint32_t pack4i(int a, int b, int c, int d)
+{
+    return perm(perm((uint32_t)d, (uint32_t)c, 0x0C0C0400u), perm((uint32_t)b, (uint32_t)a, 0x0C0C0400u), 0x05040100u);
+}
+constexpr uint32_t w4(int a, int b, int c, int d)
+{
+    return (uint32_t)(a & 255) | (uint32_t)(b & 255) << 8 | (uint32_t)(c & 255) << 16 | (uint32_t)(d & 255) << 24;
+}
+constexpr uint32_t w2(int a, int b) { return (uint32_t)(a & 0xFFFF) | (uint32_t)(b & 0xFFFF) << 16; }
+__device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) { return __builtin_amdgcn_sdot4((int)a, (int)b, c, false); }
+__device__ __forceinline__ int sdot2(s2v a, uint32_t b, int c) { return __builtin_amdgcn_sdot2(a, s2of(b), c, false); }
+
+// b of output columns 0..3 of one window row (bytes = columns 0..8, x..z):
+// clip((tap6(col x .. x+5) + 16) >> 5), four bytes
+__device__ __forceinline__ uint32_t hb4(uint32_t x, uint32_t y, uint32_t z)
+{
+    const uint32_t X = x ^ 0x80808080u, Y = y ^ 0x80808080u, Z = z ^ 0x80808080u;
+    const int k = 4096 + 16;            // 128 * (sum of taps) + rounding
+    const int b0 = sdot4(X, w4(1, -5, 20, 20), sdot4(Y, w4(-5, 1, 0, 0), k));
+    const int b1 = sdot4(X, w4(0, 1, -5, 20), sdot4(Y, w4(20, -5, 1, 0), k));
+    const int b2 = sdot4(X, w4(0, 0, 1, -5), sdot4(Y, w4(20, 20, -5, 1), k));
+    const int b3 = sdot4(X, w4(0, 0, 0, 1), sdot4(Y, w4(-5, 20, 20, -5), sdot4(Z, w4(1, 0, 0, 0), k)));
+    return pack4i(clip255(b0 >> 5), clip255(b1 >> 5), clip255(b2 >> 5), clip255(b3 >> 5));
 }
 
-// Register form of luma_row4 (same outputs, h264bsdPredictSamples' 16
-// positions, reconstruct.c:1863-1929): the 6 window rows the lane's output
-// row reads (rows yy..yy+5 of its block's window; row yy+2 holds G) come in
-// as 3 dwords each, realigned by xo bytes, and every candidate -- G, the
-// horizontal half-sample b of rows 0/+1, the vertical half-sample h of
-// columns x/x+1, the centre j -- is computed for all lanes alike; the
-// position only selects.  j (6 horizontal 6-taps per output, then one
-// vertical) runs only if some lane of the wave needs it (wave-uniform).
-// Replaces per-sample LDS byte reads under lane-divergent position branches.
-__device__ __forceinline__ void luma_row4_reg(const uint32_t (*wr)[3], int xo, int fx, int fy, bool need_j, int out[4])
+// one lane's four luma samples: row yy of 4x4 block b at fractional position
+// (fx, fy); R[i] = window row yy + i (bytes = columns 0..8).  Returns them
+// as four bytes (before the residual).  nb2 / nb3 / nh / nhx / nj: wave-
+// uniform, some lane needs b of row 2 / row 3, h of columns 2..5 / 3..6, j.
+__device__ __forceinline__ uint32_t luma_pred4(const uint4 (&R)[6], int fx, int fy, bool nb2, bool nb3, bool nh,
+                                               bool nhx, bool nj)
 {
-    // one window row at a time (9 samples live, not 54): the vertical taps
-    // of h (columns 2..6) and of j (over the rows' horizontal taps)
-    // accumulate as the rows stream in
-    const int tw[6] = {1, -5, 20, 20, -5, 1};
-    int hacc[5] = {0, 0, 0, 0, 0}, jacc[4] = {0, 0, 0, 0}, bh[4], bh1[4], G[5], Gy[4];
+    const uint32_t G2 = __builtin_amdgcn_alignbyte(R[2].y, R[2].x, 2u);     // row 2, columns 2..5
+    const uint32_t G2x = __builtin_amdgcn_alignbyte(R[2].y, R[2].x, 3u);    // row 2, columns 3..6
+    const uint32_t G3 = __builtin_amdgcn_alignbyte(R[3].y, R[3].x, 2u);     // row 3, columns 2..5
+    uint32_t B2 = 0, B3 = 0, Hc = 0, Hx = 0, J = 0;
+    if (nb2) B2 = hb4(R[2].x, R[2].y, R[2].z);
+    if (nb3) B3 = hb4(R[3].x, R[3].y, R[3].z);
+    if (nh || nhx || nj) {
+        // V of column pairs (0,1) (2,3) (4,5) (6,7) (8,-) over rows 0..5
+        s2v V[5];
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-        const uint32_t d0 = wr[i][0], d1 = wr[i][1], d2 = wr[i][2];
-        const uint32_t a0 = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)xo);
-        const uint32_t a1 = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)xo);
-        int sm[9];
+        for (int m = 0; m < 5; m++) {
+            if (!nj && (m == 0 || m == 4)) { V[m] = (s2v){0, 0}; continue; }
+            s2v P[6];
 #pragma unroll
-        for (int x = 0; x < 4; x++) { sm[x] = (a0 >> (8 * x)) & 255; sm[4 + x] = (a1 >> (8 * x)) & 255; }
-        sm[8] = (int)__builtin_amdgcn_ubfe(d2, (uint32_t)xo * 8, 8);
-#pragma unroll
-        for (int x = 0; x < 5; x++) hacc[x] += tw[i] * sm[x + 2];
-        if (i == 2) {
-#pragma unroll
-            for (int x = 0; x < 5; x++) G[x] = sm[x + 2];
+            for (int i = 0; i < 6; i++) {
+                const uint32_t src = m < 2 ? R[i].x : m < 4 ? R[i].y : R[i].z;
+                P[i] = s2of(m == 4 ? (src & 255u) : perm(0u, src, (m & 1) ? 0x0C030C02u : 0x0C010C00u));
+            }
+            V[m] = (P[0] + P[5]) + (P[2] + P[3]) * (short)20 - (P[1] + P[4]) * (short)5;
         }
-        if (i == 3) {
-#pragma unroll
-            for (int x = 0; x < 4; x++) Gy[x] = sm[x + 2];
-        }
-        if (i == 2 || i == 3 || need_j) {
-#pragma unroll
-            for (int x = 0; x < 4; x++) {
-                const int ht = tap6(sm[x], sm[x + 1], sm[x + 2], sm[x + 3], sm[x + 4], sm[x + 5]);
-                if (i == 2) bh[x] = clip255((ht + 16) >> 5);
-                if (i == 3) bh1[x] = clip255((ht + 16) >> 5);
-                if (need_j) jacc[x] += tw[i] * ht;
+        if (nh || nhx) {
+            const s2v h1 = clip_pk((V[1] + (short)16) >> (short)5), h2 = clip_pk((V[2] + (short)16) >> (short)5);
+            Hc = pack4(h1, h2);
+            if (nhx) {
+                const s2v h3 = clip_pk((V[3] + (short)16) >> (short)5);
+                Hx = __builtin_amdgcn_alignbyte(uof(h3), Hc, 1u);
             }
         }
+        if (nj) {
+            const int j0 = sdot2(V[0], w2(1, -5), sdot2(V[1], w2(20, 20), sdot2(V[2], w2(-5, 1), 512)));
+            const int j1 = sdot2(V[0], w2(0, 1), sdot2(V[1], w2(-5, 20), sdot2(V[2], w2(20, -5), sdot2(V[3], w2(1, 0), 512))));
+            const int j2 = sdot2(V[1], w2(1, -5), sdot2(V[2], w2(20, 20), sdot2(V[3], w2(-5, 1), 512)));
+            const int j3 = sdot2(V[1], w2(0, 1), sdot2(V[2], w2(-5, 20), sdot2(V[3], w2(20, -5), sdot2(V[4], w2(1, 0), 512))));
+            J = pack4i(clip255(j0 >> 10), clip255(j1 >> 10), clip255(j2 >> 10), clip255(j3 >> 10));
+        }
     }
-    int hv[5];
-#pragma unroll
-    for (int x = 0; x < 5; x++) hv[x] = clip255((hacc[x] + 16) >> 5);
-    const bool fy0 = fy == 0, fx0 = fx == 0, half = fx == 2 || fy == 2;
-#pragma unroll
-    for (int x = 0; x < 4; x++) {
-        const int jj = need_j ? clip255((jacc[x] + 512) >> 10) : 0;
-        const int g = G[x], gx = G[x + 1], gy = Gy[x];
-        const int bs = fy == 3 ? bh1[x] : bh[x];
-        const int hs = fx == 3 ? hv[x + 1] : hv[x];
-        int A, B;
-        if (fx0 && fy0) { A = g; B = g; }
-        else if (fy0) { A = bh[x]; B = fx == 1 ? g : fx == 2 ? bh[x] : gx; }
-        else if (fx0) { A = hv[x]; B = fy == 1 ? g : fy == 2 ? hv[x] : gy; }
-        else if (half) { A = jj; B = (fx == 2 && fy == 2) ? jj : (fy == 2 ? hs : bs); }
-        else { A = bs; B = hs; }
-        out[x] = (A + B + 1) >> 1;
-    }
+    // the position's two operands (8.4.2.2.1, equations 8-250 .. 8-261)
+    const bool fx0 = fx == 0, fy0 = fy == 0, half = fx == 2 || fy == 2;
+    const uint32_t bs = fy == 3 ? B3 : B2, hs = fx == 3 ? Hx : Hc;
+    uint32_t A, B;
+    if (fx0 && fy0) { A = G2; B = G2; }
+    else if (fy0) { A = B2; B = fx == 1 ? G2 : fx == 2 ? B2 : G2x; }
+    else if (fx0) { A = Hc; B = fy == 1 ? G2 : fy == 2 ? Hc : G3; }
+    else if (half) { A = J; B = (fx == 2 && fy == 2) ? J : (fy == 2 ? hs : bs); }
+    else { A = bs; B = hs; }
+    return __builtin_amdgcn_lerp(A, B, 0x01010101u);       // (A + B + 1) >> 1 per byte
 }
 
 // ---------------------------------------------------------------------------
@@ -514,10 +554,8 @@ struct McScratch {
     uint32_t coef[216];              // the MB's coded blocks (<= 27 x 32 B), staged by one coalesced load
     int16_t res[384];                // k_wgpp MC waves: the MB's residual (luma 16x16, Cb 8x8, Cr 8x8)
     union {
-        struct {                         // inter: reference windows
-            uint32_t wraw[16][9][3];     // luma windows: 12 bytes per row from an aligned column
-            uint32_t craw[2][16][3][2];  // chroma windows: 8 bytes per row
-            uint8_t wxo[16], cxo[2][16];
+        struct {                         // inter: luma reference windows
+            uint4 wrow[16][9];           // block, window row: columns 0..8 in bytes 0..8 (realigned)
         };
         struct {                         // intra (k_wg MC waves): prediction tiles with halo
             uint8_t ty[17 * TY_STRIDE], tu[9 * TC_STRIDE], tv[9 * TC_STRIDE];
@@ -1343,6 +1381,10 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                 }
                 if (lane == 0) lds_st(&R->consumed, c + 1);
             }
+        // a later step's DEP_COLS waits read this row's store progress: the
+        // row counts as stored (nothing is, in this study mode), so that they
+        // do not poll to their bounded-wait limit
+        if (COLP && pubp && lane == 0) st_gran(PROG_AT(a.prog, p, H, r, w), (uint32_t)W, a.epoch);
         return;
     }
     const PicDesc *pdp = a.pics + p;
@@ -1756,13 +1798,22 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
 // arithmetic as mc_core (reconstruct.c:1819-1941, :2222-2314).
 // ---------------------------------------------------------------------------
 struct McLoad {
-    uint32_t lw[3][3], cw[3][2];     // reference windows (luma rows lsub+4k, chroma rows)
+    uint32_t lw[3][3], cw[2][2];     // reference windows (luma rows lsub+4k; chroma rows yy, yy+1)
     uint32_t dbw, r0, r1, r2, r3;    // k_prep outputs (r*: half a residual block, lanes 0..47)
+    uint32_t mvl, mvc;               // the lane's luma / chroma block MV (x | y << 16)
     int l_x0, l_ax, c_x0, c_ax;      // window geometry (per lane)
 };
 
+// dword vectors at 4-byte alignment (the windows start on any dword)
+typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 __device__ __forceinline__ uint32_t rec_dw(uint32_t v0, int i) { return (uint32_t)__builtin_amdgcn_readlane((int)v0, i); }
 
+// Reference windows are addressed from the stream's first slot (a uniform
+// 64-bit base in SGPRs) with 32-bit per-lane offsets: slot * frame_bytes
+// (frame_bytes a multiple of 256, so one 24-bit multiply) + row * pitch +
+// column, one v_mad_u32_u24 per row.  A stream's slots span far less than
+// 4 GiB (17 slots of 2160p: 211 MB).
 __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, int p, int mb, uint32_t v0, int lane,
                                          McLoad &L, uint32_t *tsd = nullptr)
 {
@@ -1778,40 +1829,45 @@ __device__ __forceinline__ void mc_issue(const ReconArgs &a, const PicDesc &pd, 
     if (rtype < MBT_I4x4) {
         const int mbx = mb % a.w, mby = mb / a.w;
         const int W16 = a.w * 16, H16 = a.h * 16, CW = W16 / 2, CH = H16 / 2;
+        const gcu8p sb = uni(a.frames + (unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane(pd.frame_base) * a.frame_bytes);
+        const uint32_t fbu = (uint32_t)(a.frame_bytes >> 8);
         const int lb = lane >> 2, lsub = lane & 3;
         const uint32_t mvl = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + lb) << 2, (int)v0);
+        L.mvl = mvl;
         const int mvx = (int)(int16_t)(mvl & 0xFFFF), mvy = (int)(int16_t)(mvl >> 16);
         L.l_x0 = mbx * 16 + blk_x(lb) * 4 + (mvx >> 2) - 2;
         const int l_y0 = mby * 16 + blk_y(lb) * 4 + (mvy >> 2) - 2;
         L.l_ax = clip3(0, W16 - 12, L.l_x0 & ~3);
         if (tsd) tsd[0] = (uint32_t)wall_clock64();
         {
-            const uint8_t *ref = a.frames + (unsigned long long)(pd.frame_base + ((refs >> ((lb >> 2) * 8)) & 255)) * a.frame_bytes;
+            const uint32_t rs = __builtin_amdgcn_ubfe(refs, (uint32_t)(lb >> 2) * 8, 8);
+            const uint32_t o = (__umul24(rs, fbu) << 8) + (uint32_t)L.l_ax;
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 const int y = clip3(0, H16 - 1, l_y0 + min(lsub + 4 * k, 8));
-                const uint32_t *src = (const uint32_t *)(ref + (size_t)y * W16 + L.l_ax);
-                const uint3 t = *(const uint3 *)src;         // one dwordx3 load (4-byte aligned)
-                L.lw[k][0] = t.x; L.lw[k][1] = t.y; L.lw[k][2] = t.z;
+                const u32x3a4 t = *(const __attribute__((address_space(1))) u32x3a4 *)(sb + (o + __umul24((uint32_t)y, (uint32_t)W16)));
+                L.lw[k][0] = t.x; L.lw[k][1] = t.y; L.lw[k][2] = t.z;       // one dwordx3 load
             }
         }
         if (tsd) tsd[1] = (uint32_t)wall_clock64();
-        const int cb = (lane & 31) >> 1, ccomp = lane & 1;
+        // chroma: lane -> block cb, component lane & 1; lanes 0..31 load
+        // window rows 0, 1 (output row 0), lanes 32..63 rows 1, 2 (output row 1)
+        const int cb = (lane & 31) >> 1, ccomp = lane & 1, cyy = lane >> 5;
         const uint32_t mvc = (uint32_t)__builtin_amdgcn_ds_bpermute((7 + cb) << 2, (int)v0);
+        L.mvc = mvc;
         const int cmx = (int)(int16_t)(mvc & 0xFFFF), cmy = (int)(int16_t)(mvc >> 16);
         L.c_x0 = mbx * 8 + blk_x(cb) * 2 + (cmx >> 3);
-        const int c_y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3);
+        const int c_y0 = mby * 8 + blk_y(cb) * 2 + (cmy >> 3) + cyy;
         L.c_ax = clip3(0, CW - 8, L.c_x0 & ~3);
         {
-            const uint8_t *ref = a.frames + (unsigned long long)(pd.frame_base + ((refs >> ((cb >> 2) * 8)) & 255)) * a.frame_bytes +
-                                 (unsigned long long)W16 * H16 + (unsigned long long)ccomp * a.cpitch * CH;
+            const uint32_t rs = __builtin_amdgcn_ubfe(refs, (uint32_t)(cb >> 2) * 8, 8);
+            const uint32_t o = (__umul24(rs, fbu) << 8) + (uint32_t)(W16 * H16) +
+                               (uint32_t)(ccomp * a.cpitch * CH) + (uint32_t)L.c_ax;
 #pragma unroll
-            for (int wy = 0; wy < 3; wy++) {
+            for (int wy = 0; wy < 2; wy++) {
                 const int y = clip3(0, CH - 1, c_y0 + wy);
-                const uint32_t *src = (const uint32_t *)(ref + (size_t)y * a.cpitch + L.c_ax);
-                uint2 t;
-                __builtin_memcpy(&t, src, 8);                 // one dwordx2 load (4-byte aligned)
-                L.cw[wy][0] = t.x; L.cw[wy][1] = t.y;
+                const u32x2a4 t = *(const __attribute__((address_space(1))) u32x2a4 *)(sb + (o + __umul24((uint32_t)y, (uint32_t)a.cpitch)));
+                L.cw[wy][0] = t.x; L.cw[wy][1] = t.y;                      // one dwordx2 load
             }
         }
     }
@@ -1835,10 +1891,9 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     const uint32_t d0 = rec_dw(v0, 0), cbits = rec_dw(v0, 2);
     const int rtype = d0 & 255;
     const bool has_res = rtype != MBT_IPCM && cbits != 0;
-    if (lane < 24) M.srec[lane] = v0;
     if (lane < 16) ((uint32_t *)db)[lane] = L.dbw;
     if (lane == 15 && (L.dbw >> 24)) atomicOr(a.err + p, 1u);        // k_prep's range-error byte
-    if ((has_res || rtype < MBT_I4x4) && lane < 48) {
+    if (has_res && lane < 48) {
         const int b = lane >> 1, h = lane & 1;
         uint32_t *d = (uint32_t *)s_res;
         const int o = b < 16 ? (blk_y(b) * 4 + h * 2) * 8 + blk_x(b) * 2
@@ -1850,72 +1905,98 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     if (rtype >= MBT_I4x4) { wave_sync(); return rtype; }
     const int W16 = a.w * 16, CW = W16 / 2;
     const int lb = lane >> 2, lsub = lane & 3;
+    // luma windows realigned into LDS: row wy of block lb = columns 0..8 in
+    // bytes 0..8 (h264bsdFillBlock's clamp, reconstruct.c:2222-2314, for
+    // windows that leave the picture horizontally; rows were clamped by the
+    // loads)
     const bool l_in = L.l_x0 >= 0 && L.l_x0 + 8 <= W16 - 1;
+    uint4 own[3];
+    {
+        const uint32_t xo = (uint32_t)(L.l_x0 - L.l_ax);
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int wy = lsub + 4 * k;
-        if (wy >= 9) break;
-        uint32_t e0 = L.lw[k][0], e1 = L.lw[k][1], e2 = L.lw[k][2];
-        if (!l_in) {
-            uint32_t o[3] = {0, 0, 0};
+        for (int k = 0; k < 3; k++) {
+            const uint32_t e0 = L.lw[k][0], e1 = L.lw[k][1], e2 = L.lw[k][2];
+            uint4 o;
+            o.x = __builtin_amdgcn_alignbyte(e1, e0, xo);
+            o.y = __builtin_amdgcn_alignbyte(e2, e1, xo);
+            o.z = __builtin_amdgcn_alignbyte(0u, e2, xo);
+            o.w = 0;
+            if (!l_in) {
+                uint32_t q[3] = {0, 0, 0};
 #pragma unroll
-            for (int i = 0; i < 9; i++) {
-                const int kk = clip3(0, W16 - 1, L.l_x0 + i) - L.l_ax;
-                const uint32_t w = kk < 4 ? e0 : (kk < 8 ? e1 : e2);
-                o[i >> 2] |= ((w >> ((kk & 3) * 8)) & 255u) << ((i & 3) * 8);
-            }
-            e0 = o[0]; e1 = o[1]; e2 = o[2];
-        }
-        M.wraw[lb][wy][0] = e0; M.wraw[lb][wy][1] = e1; M.wraw[lb][wy][2] = e2;
-    }
-    if (lsub == 0) M.wxo[lb] = (uint8_t)(l_in ? L.l_x0 - L.l_ax : 0);
-    if (lane < 32) {
-        const int cb = lane >> 1, ccomp = lane & 1;
-        const bool c_in = L.c_x0 >= 0 && L.c_x0 + 2 <= CW - 1;
-#pragma unroll
-        for (int wy = 0; wy < 3; wy++) {
-            uint32_t e0 = L.cw[wy][0], e1 = L.cw[wy][1];
-            if (!c_in) {
-                uint32_t o = 0;
-#pragma unroll
-                for (int i = 0; i < 3; i++) {
-                    const int kk = clip3(0, CW - 1, L.c_x0 + i) - L.c_ax;
-                    const uint32_t w = kk < 4 ? e0 : e1;
-                    o |= ((w >> ((kk & 3) * 8)) & 255u) << (i * 8);
+                for (int i = 0; i < 9; i++) {
+                    const int kk = clip3(0, W16 - 1, L.l_x0 + i) - L.l_ax;
+                    const uint32_t w = kk < 4 ? e0 : (kk < 8 ? e1 : e2);
+                    q[i >> 2] |= ((w >> ((kk & 3) * 8)) & 255u) << ((i & 3) * 8);
                 }
-                e0 = o;
+                o.x = q[0]; o.y = q[1]; o.z = q[2];
             }
-            M.craw[ccomp][cb][wy][0] = e0; M.craw[ccomp][cb][wy][1] = e1;
+            own[k] = o;
+            if (k < 2 || lsub == 0) M.wrow[lb][lsub + 4 * k] = o;
         }
-        M.cxo[ccomp][cb] = (uint8_t)(c_in ? L.c_x0 - L.c_ax : 0);
     }
     wave_sync();
-    const MbRec &r = *(const MbRec *)M.srec;
-    {   // luma: lane -> (block, row)
-        const int b = lane >> 2, yy = lane & 3;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        int o[4];
-        const int fx = mvx & 3, fy = mvy & 3;
-        const bool need_j = __builtin_amdgcn_ballot_w64(fx != 0 && fy != 0 && (fx == 2 || fy == 2)) != 0;
-        luma_row4_reg(&M.wraw[b][yy], M.wxo[b], fx, fy, need_j, o);
+    uint32_t res_any = has_res;
+    {   // luma: lane -> (block b, row yy) = (lb, lsub): window rows yy .. yy + 5
+        const int b = lb, yy = lsub;
+        const int fx = L.mvl & 3, fy = (L.mvl >> 16) & 3;
+        const bool nb2 = __builtin_amdgcn_ballot_w64(fx != 0 && fy < 2) != 0;
+        const bool nb3 = __builtin_amdgcn_ballot_w64(fx != 0 && fy == 3) != 0;
+        const bool nh = __builtin_amdgcn_ballot_w64(fy != 0 && fx < 2) != 0;
+        const bool nhx = __builtin_amdgcn_ballot_w64(fy != 0 && fx == 3) != 0;
+        const bool nj = __builtin_amdgcn_ballot_w64((fx == 2 && fy != 0) || (fy == 2 && fx != 0)) != 0;
+        uint4 R[6];
+        R[0] = own[0];
+        R[4] = own[1];
+        R[2] = M.wrow[b][yy + 2];
+        R[3] = M.wrow[b][yy + 3];
+        if (nh || nhx || nj) {
+            R[1] = M.wrow[b][yy + 1];
+            R[5] = M.wrow[b][yy + 5];
+        } else {
+            R[1] = R[5] = make_uint4(0, 0, 0, 0);
+        }
+        uint32_t pk = luma_pred4(R, fx, fy, nb2, nb3, nh, nhx, nj);
         const int bx = blk_x(b) * 4, by = blk_y(b) * 4 + yy;
-        uint32_t pk = 0;
-#pragma unroll
-        for (int x = 0; x < 4; x++) pk |= (uint32_t)clip255(o[x] + s_res[by * 16 + bx + x]) << (8 * x);
+        if (res_any) {
+            const uint2 rr = *(const uint2 *)&s_res[by * 16 + bx];
+            const s2v lo = s2of(perm(0u, pk, 0x0C010C00u)) + s2of(rr.x);
+            const s2v hi = s2of(perm(0u, pk, 0x0C030C02u)) + s2of(rr.y);
+            pk = pack4(clip_pk(lo), clip_pk(hi));
+        }
         *(uint32_t *)&px[by * 16 + bx] = pk;
     }
-    {   // chroma: lane -> (block, comp, row), 2 samples
-        const int b = lane >> 2, comp = (lane >> 1) & 1, yy = lane & 1;
-        const int mvx = r.mv[b][0], mvy = r.mv[b][1];
-        const int fx = mvx & 7, fy = mvy & 7;
-        const uint8_t *w = (const uint8_t *)&M.craw[comp][b][0][0] + M.cxo[comp][b];
-        const int cx = blk_x(b) * 2, cy = blk_y(b) * 2 + yy;
+    {   // chroma: lane -> (block cb, comp, row cyy), 2 samples, from the
+        // lane's own window rows (no LDS staging)
+        const int cb = (lane & 31) >> 1, comp = lane & 1, cyy = lane >> 5;
+        const int fx = L.mvc & 7, fy = (L.mvc >> 16) & 7;
+        const bool c_in = L.c_x0 >= 0 && L.c_x0 + 2 <= CW - 1;
+        // (xo reaches 5 at the right edge: c_ax stops at CW - 8; a 64-bit
+        // shift, not v_alignbyte, whose shift is taken mod 4)
+        const uint32_t xo8 = (uint32_t)(L.c_x0 - L.c_ax) * 8u;
+        uint32_t a0 = (uint32_t)((((uint64_t)L.cw[0][1] << 32) | L.cw[0][0]) >> xo8);
+        uint32_t a1 = (uint32_t)((((uint64_t)L.cw[1][1] << 32) | L.cw[1][0]) >> xo8);
+        if (!c_in) {
+            uint32_t q0 = 0, q1 = 0;
 #pragma unroll
-        for (int x = 0; x < 2; x++) {
-            const int A = w[yy * 8 + x], B = w[yy * 8 + x + 1], C = w[(yy + 1) * 8 + x], D = w[(yy + 1) * 8 + x + 1];
-            const int v = ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
-            px[256 + comp * 64 + cy * 8 + cx + x] = (uint8_t)clip255(v + s_res[256 + comp * 64 + cy * 8 + cx + x]);
+            for (int i = 0; i < 3; i++) {
+                const int kk = clip3(0, CW - 1, L.c_x0 + i) - L.c_ax;
+                const uint32_t w0 = kk < 4 ? L.cw[0][0] : L.cw[0][1], w1 = kk < 4 ? L.cw[1][0] : L.cw[1][1];
+                q0 |= ((w0 >> ((kk & 3) * 8)) & 255u) << (i * 8);
+                q1 |= ((w1 >> ((kk & 3) * 8)) & 255u) << (i * 8);
+            }
+            a0 = q0; a1 = q1;
         }
+        // (A, B, C, D) of output columns 0 and 1 as bytes; weights alike
+        const uint32_t q0 = perm(a1, a0, 0x05040100u), q1 = perm(a1, a0, 0x06050201u);
+        const uint32_t gx = 8 - fx, gy = 8 - fy;
+        const uint32_t wts = (gx * gy) | (fx * gy) << 8 | (gx * fy) << 16 | (fx * fy) << 24;
+        const uint32_t v0 = __builtin_amdgcn_udot4(q0, wts, 32u, false) >> 6, v1 = __builtin_amdgcn_udot4(q1, wts, 32u, false) >> 6;
+        uint32_t pr = v0 | (v1 << 16);
+        const int cx = blk_x(cb) * 2, cy = blk_y(cb) * 2 + cyy;
+        const int po = 256 + comp * 64 + cy * 8 + cx;
+        if (res_any) pr = uof(clip_pk(s2of(pr) + s2of(*(const uint32_t *)&s_res[po])));
+        *(uint16_t *)&px[po] = (uint16_t)perm(0u, pr, 0x0C0C0200u);
     }
     wave_sync();
     return rtype;

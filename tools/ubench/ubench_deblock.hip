@@ -96,7 +96,8 @@ __global__ __launch_bounds__(64) void k_intra(unsigned long long *out, int iters
 
 // mc_finish (the MC wave's inter MB: window staging, 6-tap luma, bilinear
 // chroma, residual add) of a lone wave, loads already landed; fx/fy
-// fractional positions cycle over all 16 luma / 64 chroma cases
+// fractional positions cycle over all 16 luma / 64 chroma cases (mode 3: one
+// position per MB, as skip / 16x16 MBs, cycling)
 __global__ __launch_bounds__(64) void k_mc(unsigned long long *out, int iters, const uint8_t *frame, uint8_t *dbrec,
                                            int16_t *res, unsigned *err, int fmode)
 {
@@ -127,6 +128,11 @@ __global__ __launch_bounds__(64) void k_mc(unsigned long long *out, int iters, c
     McLoad L;
     unsigned long long acc = 0;
     for (int it = 0; it < iters; it++) {
+        if (fmode == 3 && lane >= 7 && lane < 23) {
+            // one MV per MB (skip / 16x16), its position cycling over the 16
+            const int fx = it & 3, fy = (it >> 2) & 3;
+            v0 = (uint32_t)(uint16_t)(4 * 3 + fx) | ((uint32_t)(uint16_t)(4 * -2 + fy) << 16);
+        }
         const int mb = 30 * 120 + 40 + (it & 15);
         mc_issue(a, pd, 0, mb, v0, lane, L);
         drain_vm();
@@ -225,10 +231,10 @@ int main()
         (void)hipMalloc(&res, 120 * 68 * 768);
         (void)hipMemset(res, 0, 120 * 68 * 768);
         (void)hipMalloc(&err, 64);
-        for (int fm = 0; fm < 3; fm++) {
+        for (int fm = 0; fm < 4; fm++) {
             hipLaunchKernelGGL(k_mc, dim3(1), dim3(64), 0, 0, d, 500, frame, dbrec, res, err, fm);
             (void)hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
-            printf("mc_finish inter MB (%s): %llu cycles (%.3f us)\n", fm == 0 ? "16 positions" : fm == 1 ? "full-sample" : "half b/h only",
+            printf("mc_finish inter MB (%s): %llu cycles (%.3f us)\n", fm == 0 ? "16 positions" : fm == 1 ? "full-sample" : fm == 2 ? "half b/h only" : "one MV per MB, all positions",
                    h[0], h[0] / mhz);
         }
     }
