@@ -569,9 +569,9 @@ int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int
         pd.cur_slot = (uint32_t)cur_slot[i];
         {
             const MbRec *r = (const MbRec *)recs[i];
-            int n = 0;
-            for (int m = 0; m < e->nmbs; m++) n += r[m].type >= MBT_I4x4;
-            pd.flags = 2 * n > e->nmbs ? PD_INTRA_HEAVY : 0;
+            int n = 0, db = 0;
+            for (int m = 0; m < e->nmbs; m++) { n += r[m].type >= MBT_I4x4; db |= r[m].avail & DB_INNER; }
+            pd.flags = (2 * n > e->nmbs ? PD_INTRA_HEAVY : 0) | (db ? 0 : PD_NO_DEBLOCK);
         }
         pd.coef_base = (uint32_t)cbase;
         pd.rsv[0] = pd.rsv[1] = pd.rsv[2] = 0;

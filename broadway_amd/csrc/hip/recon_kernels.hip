@@ -126,6 +126,7 @@ struct ReconArgs {
 #define CHK_REGION  256u
 #define CHK_PROG    512u
 #define CHK_REFROW  1024u
+#define CHK_NODB    2048u   // a PD_NO_DEBLOCK picture holds an MB that filters (row_drain)
 
 __constant__ uint8_t cZigzag[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
 __constant__ uint8_t cLevelScale[6][3] = {
@@ -1366,6 +1367,61 @@ struct __attribute__((aligned(16))) PPLds {
 // sample of MB row r, column x is final once row r's MBs 0..x+1 and row
 // r+1's MBs 0..x have stored (row r+1 stores row r's rows 12..15 after its
 // top-edge filter; MB x+1 stores MB x's columns 12..15 after its left edge).
+// row_pp's path for rows without deblocking (see there): store each MB's
+// ring slot to the frame as its MC lands, release the slot before it (the
+// intra prediction of MB c has read MB c - 1's), and -- when a later step of
+// the launch reads this picture (wt: write-through stores) -- publish both
+// row waves' store progress.  Out of line, so that it leaves row_pp's
+// register allocation alone; LDS and global pointers address-space typed
+// (a generic pointer argument would make every access FLAT).  ydst / cdst:
+// this lane's luma / chroma dword of MB 0 in the frame.
+typedef __attribute__((address_space(1))) uint8_t *g_u8p;
+typedef __attribute__((address_space(1))) unsigned long long *g_u64p;
+template <int RK, bool CHK>
+__device__ __attribute__((noinline)) void row_drain(__attribute__((address_space(3))) MbRing<RK> *Rl, g_u8p ydst, g_u8p cdst,
+                                                    int W, bool wt, g_u64p prog0, g_u64p prog1, uint32_t tag, g_u32 *perr_g,
+                                                    int lane, const __attribute__((address_space(1))) uint32_t *recw)
+{
+    MbRing<RK> &R = *(MbRing<RK> *)Rl;
+    unsigned *perr = (unsigned *)perr_g;
+    const int orow = lane >> 2, oq = lane & 3, li = lane & 31;
+    const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;
+    for (int c = 0; c < W; c++) {
+        const int slot = c & (RK - 1);
+        if (wt && c >= 2 && (c & 1) == 0) {
+            // MBs 0..c-1 stored and drained: both parities' progress
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) { st_gran((unsigned long long *)prog0, (uint32_t)c, tag); st_gran((unsigned long long *)prog1, (uint32_t)c, tag); }
+        }
+        unsigned spins = 0;
+        while (__builtin_amdgcn_readfirstlane(lds_ld(&R.flag[slot])) != c + 1) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) { if (lane == 0) atomicOr(perr, 16u); break; }
+        }
+        wave_sync();
+        if (CHK && __builtin_amdgcn_readfirstlane(*(const uint16_t *)&R.db[slot][CHK_TAG_OFF]) != c && lane == 0)
+            atomicOr(perr, CHK_RING);
+        // (checker: the host's PD_NO_DEBLOCK -- this MB filters nothing)
+        if (CHK && ((recw[c * 24] >> 24) & DB_INNER) && lane == 0) atomicOr(perr, CHK_NODB);
+        const uint32_t vy = *(const uint32_t *)&R.px[slot][orow * 16 + oq * 4];
+        const uint32_t vc = *(const uint32_t *)&R.px[slot][256 + ccomp * 64 + crow * 8 + cq * 4];
+        if (wt) st_sc1_u32((uint32_t *)(ydst + c * 16), vy);
+        else *(__attribute__((address_space(1))) uint32_t *)(ydst + c * 16) = vy;
+        if (lane < 32) {
+            if (wt) st_sc1_u32((uint32_t *)(cdst + c * 8), vc);
+            else *(__attribute__((address_space(1))) uint32_t *)(cdst + c * 8) = vc;
+        }
+        wave_sync();
+        // MB c done: the intra prediction of MB c has read MB c - 1's slot
+        if (lane == 0) lds_st(&R.consumed, c);
+    }
+    if (lane == 0) lds_st(&R.consumed, W);
+    if (wt) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) { st_gran((unsigned long long *)prog0, (uint32_t)W, tag); st_gran((unsigned long long *)prog1, (uint32_t)W, tag); }
+    }
+}
+
 template <bool PROF, bool UPL, bool MEL, int RK, bool CHK, bool COLP = false>
 __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, const int lane, MbRing<RK> *R,
                        const unsigned long long *mbx_up, unsigned long long *mbx_me, bool pubp = false)
@@ -1456,6 +1512,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
     // 6..7, the dword holding columns 12..15 / 4..7) -- patch lane pj = ls
     // publishes its own result, no cross-lane move; slots 8..23 the others.
     uint32_t prov_off;      // the granule's provisional dword in the region (rows 12..15, cols 0..15)
+    uint32_t ent_glb;       // ... and its frame offset (rows 12..15 / chroma 6..7)
     int gi;
     {
         const int ls = le;
@@ -1475,6 +1532,8 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             comp = (ls - 20) >> 1; row = (ls - 20) & 1; qq = 0;
         }
         gi = luma ? yrow * 4 + yq : 16 + comp * 4 + row * 2 + qq;
+        // its place in the frame, from MB c's luma / chroma origin
+        ent_glb = luma ? (uint32_t)((12 + yrow) * W16 + yq * 4) : (uint32_t)(comp * CP * CH + (6 + row) * CP + qq * 4);
         prov_off = luma ? (uint32_t)((int)(G.ry - Lb) + (16 + yrow) * RY_S + 4 + yq * 4)
                         : (uint32_t)((int)((comp ? G.rv : G.ru) - Lb) + (8 + row) * RC_S + 4 + qq * 4);
     }
@@ -1556,9 +1615,19 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         const uint32_t avn = ldg32(uni(a.rec + rec_base + r * W + min(c + 1, W - 1)), 0);
         const int avail = (h0 >> 24) & 255;
         const bool dbf = avail & DB_INNER;
+        // The top MB edge is filtered (filterTopMbEdgeFlag, deblocking.c:
+        // 288-319): only then does H(c) need the row above's final rows
+        // 12..15, and only then does this MB store them (after its top-edge
+        // filter).  Otherwise -- disable_deblocking_filter_idc 1, or 2 with
+        // the MB above in another slice -- the MB above stores them itself
+        // and this MB does not wait on the row above at all.
+        const bool top_on = has_up && (avail & DB_INNER) && (avail & DB_TOP);
+        // the MB below's record dword 0 (its top-edge flags: who stores this
+        // MB's rows 12..15); a VMEM load, like avn
+        const uint32_t avd = has_down ? ldg32(uni(a.rec + rec_base + (r + 1) * W + c), 0) : 0u;
         // speculative read of the row above's entry c (lanes 0..23 used)
         const unsigned long long *tga = mbx_up + c * 32 + (lane < 24 ? lane : (lane & 15));
-        unsigned long long gr = ld_granT<UPL>(tga);
+        unsigned long long gr = top_on ? ld_granT<UPL>(tga) : 0ull;
         // ---- off the chain: my region is free once MB c-1's wave read MB c-2's
         {
             unsigned spins = 0;
@@ -1665,7 +1734,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
         PPT(1);
         if (prof && lane == 0) { if (c == 0) tva = wall_clock64(); pmb[1] = (tva & 0xFFFFFFFFull) | (wall_clock64() << 32); }
         // ---- top halo (row above's entry c final), horizontal edges
-        if (has_up) {
+        if (top_on) {
             unsigned spins = 0;
             const bool mine = lane < 24;
             // (measured: four staggered polls in flight made the hand-off
@@ -1718,7 +1787,11 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                 const uint32_t newp = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) | ((uint32_t)v[3] << 24);
                 if (is_patch) ent = newp;
             }
-            st_granT<MEL>(mbx_me + (size_t)c * 32 + gi, ent, tag);
+            // rows 12..15 (chroma 6..7) are final: to the MB below, which
+            // filters its top edge and stores them, or straight to the frame
+            const uint32_t bflags = (uint32_t)__builtin_amdgcn_readfirstlane((int)avd) >> 24;
+            if ((bflags & (DB_INNER | DB_TOP)) == (DB_INNER | DB_TOP)) st_granT<MEL>(mbx_me + (size_t)c * 32 + gi, ent, tag);
+            else if (lane < 24) fst((gi < 16 ? ybase + c * 16 : cbase + c * 8) + ent_glb, ent);
             if (prof && lane == 0) pmb[2] = (wall_clock64() & 0xFFFFFFFFull) | (tvd << 32);
         }
         // ---- off the chain again: frame stores, once per sample
@@ -1728,8 +1801,8 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             const uint32_t vb = *(const uint32_t *)(Lb + sb_lds);
             uint8_t *const yb = ybase + c * 16 - 4 * W16 - 4;
             uint8_t *const cb = cbase + c * 8 - 2 * CP - 4;
-            const bool oka = (!sa_left || c > 0) && (!sa_top || has_up);
-            const bool okb = (!sb_left || c > 0) && (!sb_top || has_up);
+            const bool oka = (!sa_left || c > 0) && (!sa_top || top_on);
+            const bool okb = (!sb_left || c > 0) && (!sb_top || top_on);
             fst(oka ? (void *)(yb + sa_glb) : (void *)sink, va);
             fst(okb ? (void *)(cb + sb_glb) : (void *)((uint32_t *)sink + 1), vb);
         } else {
@@ -1750,7 +1823,7 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
                         fst(cbase + c * 8 - 4 + comp * CP * CH + row * CP, *(const uint32_t *)&(comp ? G.rv : G.ru)[(row + 2) * RC_S]);
                 }
             }
-            if (has_up) {
+            if (top_on) {
                 if (lane >= 32 && lane < 48) {
                     const int k = lane - 32;
                     fst(ybase + c * 16 + (k & 3) * 4 + (-4 + (k >> 2)) * W16, *(const uint32_t *)&G.ry[(k >> 2) * RY_S + 4 + (k & 3) * 4]);
@@ -2620,7 +2693,32 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     unsigned long long *const me = mel ? lmbx + q * W32 : a.mbx + ((size_t)p * a.h + r) * W32;
     if (wid < 2) {
         __builtin_amdgcn_s_setprio(3);
-        if (DEPM == DEP_COLS) row_pp<PROF, false, false, RK, CHK, true>(a, p, r, L[q], wid, lane, &R[q], up, me, j + 1 < a.P);
+        // pictures without deblocking (PicDesc PD_NO_DEBLOCK: no MB filters
+        // any edge -- every slice disable_deblocking_filter_idc 1, the
+        // reference's recommended `-flags -loop` encode, README.markdown:
+        // 32-35; GetMbFilteringFlags drops every edge, deblocking.c:288-319).
+        // Every MB's MC output is then final: row wave 0 stores each ring slot
+        // straight to the frame as it lands (row_drain: no region, no in-row
+        // chain, no row above), row wave 1 has nothing to do.  A host flag,
+        // not a scan of the records here: any load on the row waves' way in
+        // measurably delays the filtered pictures' first rows.
+        const bool nodb = __builtin_amdgcn_readfirstlane(a.pics[p].flags) & PD_NO_DEBLOCK;
+        if (nodb) {
+            if (wid == 0) {
+                const int fslot = __builtin_amdgcn_readfirstlane(a.pics[p].frame_base + a.pics[p].cur_slot);
+                const int W16 = a.w * 16, CP = a.cpitch, CH = a.h * 8;
+                uint8_t *cur = a.frames + (unsigned long long)fslot * a.frame_bytes;
+                const int orow = lane >> 2, oq = lane & 3, li = lane & 31;
+                const int ccomp = (li >> 4) & 1, crow = (li >> 1) & 7, cq = li & 1;
+                uint8_t *ydst = cur + (size_t)r * 16 * W16 + orow * W16 + oq * 4;
+                uint8_t *cdst = cur + (size_t)W16 * a.h * 16 + (size_t)r * 8 * CP + ccomp * CP * CH + crow * CP + cq * 4;
+                const bool wt = DEPM == DEP_COLS && j + 1 < a.P;
+                row_drain<RK, CHK>((__attribute__((address_space(3))) MbRing<RK> *)&R[q], (g_u8p)ydst, (g_u8p)cdst, a.w, wt,
+                                   (g_u64p)PROG_AT(a.prog, p, a.h, r, 0), (g_u64p)PROG_AT(a.prog, p, a.h, r, 1), a.epoch,
+                                   (g_u32 *)(a.err + p), lane,
+                                   (const __attribute__((address_space(1))) uint32_t *)(a.rec + a.pics[p].rec_base + r * a.w));
+            }
+        } else if (DEPM == DEP_COLS) row_pp<PROF, false, false, RK, CHK, true>(a, p, r, L[q], wid, lane, &R[q], up, me, j + 1 < a.P);
         else if (!upl && !mel) row_pp<PROF, false, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else if (!upl) row_pp<PROF, false, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
         else if (mel) row_pp<PROF, true, true, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);

@@ -98,12 +98,17 @@ typedef struct PicDesc {
     uint32_t frame_base;    /* index of this stream's slot 0 in the frame pool */
     uint32_t cur_slot;      /* slot being reconstructed */
     uint32_t flags;         /* bit2 (PD_INTRA_HEAVY): more than half the picture's MBs are intra
-                               (a scheduling hint: intra MC waves first); bits 0, 1 unused */
+                               (a scheduling hint: intra MC waves first); bit3 (PD_NO_DEBLOCK): no
+                               MB of the picture filters any edge (no record has DB_INNER: every
+                               slice disable_deblocking_filter_idc 1) -- the MC output is final and
+                               is stored without the deblocking row chain.  Set only when true: a
+                               picture with filtering flagged so would come out unfiltered (the
+                               dependency checker flags that, CHK_NODB).  Bits 0, 1 unused */
     uint32_t coef_base;     /* added to MbRec.coef (records are picture-relative) */
     uint32_t rsv[3];
 } PicDesc;
 
-enum { PD_INTRA_HEAVY = 4 };
+enum { PD_INTRA_HEAVY = 4, PD_NO_DEBLOCK = 8 };
 
 /* Device frame-slot layout (the engine's HBM frame pool): I420, luma rows
  * w*16 bytes apart, then the Cb and Cr planes with their rows padded to a

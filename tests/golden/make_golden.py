@@ -121,6 +121,12 @@ for s in range(100, 164):
 # wait on (MB row, MB column) cells
 for s in range(100, 108):
     CASES[f"bench_1080p_offpic0_s{s}"] = (3, s, dict(nframes=60, offpic_pct=0), False)
+# bench.py leg `cfg3_no_loop_filter`: rank 0's streams with the loop filter
+# off in every slice (disable_deblocking_filter_idc 1) -- the reference's own
+# recommended encode (README.markdown:32-35, `-flags -loop`), where no MB row
+# waits on the row above
+for s in range(100, 108):
+    CASES[f"bench_1080p_noloop_s{s}"] = (3, s, dict(nframes=60, dbf_idc1_pct=100), False)
 
 
 def find_patch(stream: bytes):

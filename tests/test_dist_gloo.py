@@ -56,7 +56,7 @@ def test_two_rank_sharding_and_max():
         assert sorted(flat) == list(range(100, 116))  # config 4: seeds 100.. 8 per GPU
 
 
-def _bench_worker(rank, world, port, q):
+def _bench_worker(rank, world, port, q, one_device=False):
     """One rank of `bench.py --gpus 2 --dry-run` (torch.distributed.run's
     environment): sharding, host parse, warmup + timed step loop, the
     max-over-ranks timing and the summed verification counts, no device."""
@@ -67,6 +67,8 @@ def _bench_worker(rank, world, port, q):
     sys.path.insert(0, root)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
                       WORLD_SIZE=str(world))
+    if one_device:
+        os.environ["BENCH_ONE_DEVICE"] = "1"
     import bench
     out = io.StringIO()
     with contextlib.redirect_stdout(out):
@@ -120,6 +122,34 @@ def test_bench_dry_run_two_ranks():
         assert cores[r] and len(cores[r]) == plan[r]["host_cores"]
         assert cores[r] <= os.sched_getaffinity(0)
     assert not cores[0] & cores[1]
+
+
+@pytest.mark.timeout(180)
+def test_bench_one_device_rehearsal_disjoint_cores():
+    """BENCH_ONE_DEVICE=1 (the N-rank rehearsal on one GPU): every rank's GPU
+    is device 0, but each rank still pins its end-to-end decoder processes to
+    its own disjoint share of that device's host cores."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=160) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    line = json.loads(res[0].strip().splitlines()[-1])
+    plan = {p["rank"]: p for p in line["end_to_end_plan"]}
+    assert sorted(plan) == [0, 1]
+    assert all(plan[r]["device"] == 0 for r in (0, 1))
+    cores = {r: set(bench.parse_cpulist(plan[r]["cpus"])) for r in (0, 1)}
+    assert cores[0] and cores[1] and not cores[0] & cores[1]
 
 
 def test_e2e_core_plan_numa():

@@ -258,6 +258,74 @@ def test_realistic_motion_shard_vs_reference(pipe):
         run.free()
 
 
+@pytest.mark.parametrize("pipe,staggered,check", [(1, True, False), (3, True, False), (3, False, False),
+                                                   (3, True, True), (1, False, True)])
+def test_no_loop_filter_shard_vs_reference(pipe, staggered, check, monkeypatch):
+    """configs[3]'s rank-0 streams with the loop filter off in every slice
+    (disable_deblocking_filter_idc 1: the reference's recommended `-flags
+    -loop` encode, README.markdown:32-35; bench leg cfg3_no_loop_filter).  No
+    MB row waits on the row above: every MB stores its own final rows 12..15
+    (row_pp top_on).  Every picture vs the reference MD5s, with one and three
+    pictures per launch, GOP-staggered and aligned, and under the dependency
+    checker (no bit)."""
+    import bench
+    if check:
+        monkeypatch.setenv("H264MI_CHECK", "1")
+    seeds = bench.shard_seeds(0, 8)
+    n = 60
+    ov = {"dbf_idc1_pct": 100}
+    _, caps = bench.prepare(3, seeds, n, ov)
+    assert all(c.errors == 0 for c in caps)
+    phases = bench.gop_phases(8, n, pipe, warmup=4) if staggered else None
+    # aligned: whole launches from picture `pipe` on (as the bench leg)
+    warm = 4 if staggered else pipe
+    steps = n - 4 if staggered else n - pipe - (n - pipe) % pipe
+    run = bench.DeviceRun(_lib.mi(), caps, warm, steps, pipe, phases=phases)
+    try:
+        assert run.P == pipe
+        refs = [bench.golden_frames(3, sd, ov) for sd in seeds]
+        assert all(r is not None and len(r) == n for r in refs)
+        ok, checked, missing, _ = run.verify(refs)
+        assert ok and missing == 0 and checked >= 8 * (warm + steps)
+        assert run.check_resident(refs)[0]
+        if check:
+            assert run.eng.kernel_name() == "k_wgpp_check"
+            assert run.eng.error_bits() == 0
+        assert run.eng.errors() == 0
+    finally:
+        run.free()
+
+
+@pytest.mark.parametrize("idc1,idc2,pipe", [(0, 100, 1), (0, 100, 3), (50, 50, 1), (50, 50, 2), (30, 40, 3)])
+def test_slice_boundary_row_decoupling_vs_oracle(idc1, idc2, pipe):
+    """Slices with the loop filter off (idc 1) or off across slice boundaries
+    (idc 2), one slice per MB row or a slice boundary inside a row: MBs
+    whose top edge is not filtered neither wait on nor store the row above,
+    whose MBs then store their own rows 12..15.  Every picture vs the oracle's
+    decode of the stream, one to three pictures per launch."""
+    import bench
+    w, h = 13, 9
+    streams = [gen.generate(2, 80 + i, nframes=9, w_mbs=w, h_mbs=h, crop_bottom=0, slices=s, gop=5,
+                            dbf_idc1_pct=idc1, dbf_idc2_pct=idc2)
+               for i, s in enumerate((h, 5, 4))]
+    caps = [Capture(s) for s in streams]
+    refs = [O.decode(s)[0] for s in streams]
+    n = min(c.npics for c in caps)
+    n -= n % pipe
+    run = bench.DeviceRun(_lib.mi(), caps, 0, n, pipe)
+    try:
+        for i, launch in enumerate(run.launches):
+            run.launch(i)
+            run.eng.sync()
+            for step in launch:
+                for s, k in enumerate(step):
+                    got = run.eng.read(s, int(run.slot_of[k][s])).tobytes()
+                    assert got == refs[s][k], f"stream {s} picture {k}"
+        assert run.eng.errors() == 0
+    finally:
+        run.free()
+
+
 @pytest.mark.parametrize("mode", ["rows", "cols"])
 @pytest.mark.parametrize("wh,pipe", [((13, 7), 2), ((12, 9), 2), ((20, 11), 2), ((13, 7), 3), ((20, 11), 4),
                                      ((24, 7), 3), ((8, 9), 2), ((3, 5), 3)])

@@ -198,11 +198,13 @@ def main(tag):
     # a step is one launch of the main kernel; the standalone k_prep launch
     # (the pipeline's first step) is spread over them
     step /= kernels[step_kernels[0]]["launches"]
-    out = {"tag": tag, "kernels": kernels, "hbm_bytes_per_step": int(step),
+    # (every launch of the main kernel averaged -- pre-roll, warmup and the
+    # untimed legs included; the timed window's own bytes are timed_window)
+    out = {"tag": tag, "kernels": kernels, "hbm_bytes_per_launch_all_launches": int(step),
            "note": "FETCH_SIZE doubled per the gfx950 correction; the factor 2.0 is measured for this kernel's 4-, 8-, 12- and 16-B per-lane loads (tools/ubench/fetch_calib.hip, profiles/r34_fetch_calib.json)"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     json.dump({"source": f"profiles/{tag}_pmc.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
-               "hbm_bytes_per_step": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+               "hbm_bytes_per_launch_all_launches": int(step)}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     tw = trace_window(src)
     if tw:
         out["trace_window"] = tw
