@@ -65,7 +65,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MBREC = 96
 DB_INNER = 64            # MbRec.avail: the MB filters its edges (include/h264mi_records.h)
 MAX_E2E_PROCS = 8          # end-to-end leg: decoder processes (the box allows 16 GPU processes)
-E2E_REPS = 18              # end-to-end leg: passes over each 60-picture stream (>= 3 s at ~360 frames/s per process)
+E2E_REPS = 21              # end-to-end leg: passes over each 60-picture stream (>= 3 s at ~400 frames/s per process)
 
 
 def parse_args(argv=None):

@@ -2013,11 +2013,16 @@ __device__ __forceinline__ int mc_finish(const ReconArgs &a, int p, uint32_t v0,
     {   // luma: lane -> (block b, row yy) = (lb, lsub): window rows yy .. yy + 5
         const int b = lb, yy = lsub;
         const int fx = L.mvl & 3, fy = (L.mvl >> 16) & 3;
-        const bool nb2 = __builtin_amdgcn_ballot_w64(fx != 0 && fy < 2) != 0;
-        const bool nb3 = __builtin_amdgcn_ballot_w64(fx != 0 && fy == 3) != 0;
-        const bool nh = __builtin_amdgcn_ballot_w64(fy != 0 && fx < 2) != 0;
-        const bool nhx = __builtin_amdgcn_ballot_w64(fy != 0 && fx == 3) != 0;
-        const bool nj = __builtin_amdgcn_ballot_w64((fx == 2 && fy != 0) || (fy == 2 && fx != 0)) != 0;
+        // which candidates some lane needs, by position bit fy * 4 + fx:
+        // b of row 2 (fx != 0, fy < 2), b of row 3 (fx != 0, fy == 3), h of
+        // columns 2..5 (fy != 0, fx < 2), 3..6 (fy != 0, fx == 3), j (a half
+        // position off the axes)
+        const uint32_t pm = 1u << (fy * 4 + fx);
+        const bool nb2 = __builtin_amdgcn_ballot_w64((pm & 0x00EEu) != 0) != 0;
+        const bool nb3 = __builtin_amdgcn_ballot_w64((pm & 0xE000u) != 0) != 0;
+        const bool nh = __builtin_amdgcn_ballot_w64((pm & 0x3330u) != 0) != 0;
+        const bool nhx = __builtin_amdgcn_ballot_w64((pm & 0x8880u) != 0) != 0;
+        const bool nj = __builtin_amdgcn_ballot_w64((pm & 0x4E40u) != 0) != 0;
         uint4 R[6];
         R[0] = own[0];
         R[4] = own[1];

@@ -22,7 +22,10 @@ P = int(os.environ.get("PROF_P", "3"))
 LA = int(os.environ.get("PROF_LAUNCH", "2"))
 seeds = [100 + i for i in range(S)]
 n = P * (LA + 1)
-streams, caps = bench.prepare(3, seeds, n + 1)
+# PROF_OV: generator overrides, e.g. "dbf_idc1_pct=100" (rows without
+# deblocking keep no row stamps: the MC stamps set the time base then)
+ov = dict((k, int(v)) for k, v in (x.split("=") for x in os.environ.get("PROF_OV", "").split(",") if x))
+streams, caps = bench.prepare(3, seeds, n + 1, ov or None)
 w, h = caps[0].w_mbs, caps[0].h_mbs
 run = bench.DeviceRun(L, caps, 0, n, P)
 eng = run.eng
@@ -42,7 +45,8 @@ rows = a[:npics * h * 16].reshape(h, npics, 16)
 mb = a[npics * h * 16:].reshape(npics, h, w, 8)
 start = rows[:, :, 0].astype(np.int64)              # [r, p]
 end = rows[:, :, 1].astype(np.int64)
-base = start[start > 0].min()
+mc3 = mb[..., 3]
+base = start[start > 0].min() if (start > 0).any() else int((mc3[mc3 > 0] & np.uint64(0xFFFFFFFF)).min())
 st = (start - base) / 100.0
 en = (end - base) / 100.0
 dep = mb[..., 6].astype(np.int64) / 100.0           # [p, r, c] us
@@ -72,7 +76,7 @@ Cst = us(lo(mb[..., 0]))
 A, B = us(lo(mb[..., 1])), us(hi(mb[..., 1]))
 E, D = us(lo(mb[..., 2])), us(hi(mb[..., 2]))
 rows_, cols_ = slice(8, h - 1), slice(2, w - 2)
-for j in range(P):
+for j in range(P if (start > 0).any() else 0):     # (rows without deblocking have no chain)
     ps = slice(j * S, (j + 1) * S)
     per = np.diff(Cst[ps, rows_, :], axis=2)[:, :, 2:w - 3]
     V = (B - A)[ps, rows_, cols_]
