@@ -474,6 +474,35 @@ def node_cpus(node: int):
         return None
 
 
+def l3_groups(cpus):
+    """`cpus` split by last-level cache (sysfs cache/index3 shared_cpu_list;
+    an EPYC CCD): a decoder process whose threads share one L3 hands the
+    speculative workers' records and coefficients to its calling thread
+    without crossing the fabric.  Falls back to one group."""
+    groups, seen = [], set()
+    for c in sorted(cpus):
+        if c in seen:
+            continue
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/cache/index3/shared_cpu_list") as f:
+                g = sorted(set(parse_cpulist(f.read())) & set(cpus))
+        except (OSError, ValueError):
+            return [sorted(cpus)]
+        seen.update(g)
+        groups.append(g)
+    return groups or [sorted(cpus)]
+
+
+def process_cpus(cpus, nprocs):
+    """Each end-to-end decoder process's core set: its own L3 domain when the
+    share has at least one per process (round-robin over the domains), else
+    the whole share."""
+    groups = [g for g in l3_groups(cpus) if len(g) >= 2]
+    if len(groups) >= nprocs:
+        return [groups[i] for i in range(nprocs)]
+    return [sorted(cpus)] * nprocs
+
+
 def e2e_core_plan(local: int, numa, allowed):
     """Host cores for each local rank's end-to-end decoder processes
     (each GPU has its own host parse threads on a NUMA-local core
@@ -523,12 +552,17 @@ def end_to_end(streams, nframes, reps=E2E_REPS, device=0, cpus=None, max_procs=M
     # are the bound on this path (tools/e2e_env_sweep.sh: 1.89k -> 2.08k fps)
     env = dict(os.environ)
     env.setdefault("H264MI_BLOCKING_SYNC", "1")
-    # 8 decoder processes on the box's 16-core share: the calling thread plus
-    # 2 slice workers each (profiles/r51_host_ab.txt: 5.9 vs 6.4 ms host CPU
-    # per picture with 3 workers, same rate); the library default stays 3
-    env.setdefault("H264MI_PARSE_THREADS", "2")
+    # 8 decoder processes, each pinned to one L3 domain (process_cpus): the
+    # calling thread plus 3 slice workers each -- with the workers on their
+    # caller's L3, a fourth parse thread keeps the box's 16-core share busy
+    # (profiles/r154_e2e_threads.txt: 15.6 vs 13.4 cores, 3.55k vs 3.09k
+    # fps; r153: L3 pinning 3.51k fps at 4.13 ms vs 3.31k at 4.41 unpinned
+    # within the NUMA share; round 3's r51 had 2 workers better unpinned)
+    env.setdefault("H264MI_PARSE_THREADS", "3")
     env["H264MI_DEVICE"] = str(device)
-    pin = [f"-A{format_cpulist(cpus)}"] if cpus else []
+    # each process on one L3 domain of the share (E2E_L3=0: the whole share)
+    per_proc = process_cpus(cpus, len(streams[:max_procs])) if cpus and os.environ.get("E2E_L3", "1") == "1" \
+        else [cpus] * len(streams[:max_procs])
     td = tempfile.mkdtemp(prefix="h264e2e")
     try:
         procs = []
@@ -536,6 +570,7 @@ def end_to_end(streams, nframes, reps=E2E_REPS, device=0, cpus=None, max_procs=M
             pth = os.path.join(td, f"s{i}.h264")
             with open(pth, "wb") as f:
                 f.write(s)
+            pin = [f"-A{format_cpulist(per_proc[i])}"] if per_proc[i] else []
             procs.append(subprocess.Popen([exe, "-Onone", f"-r{reps}", "-T", "-G"] + pin + [pth], stdin=subprocess.PIPE,
                                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env))
         # start gate: wait until every process has warmed up, then release all.
@@ -595,6 +630,7 @@ def end_to_end(streams, nframes, reps=E2E_REPS, device=0, cpus=None, max_procs=M
                "longest_single_window_s": round(max(secs), 6),
                "host_cores_assigned": len(cpus) if cpus else None,
                "cpus": format_cpulist(cpus) if cpus else None,
+               "per_process_cpus": [format_cpulist(x) for x in per_proc] if cpus else None,
                "sample": f"{len(streams)} x {nframes}-frame 1080p streams x {reps} passes, one h264mi_dec process "
                          f"(H264SwDec* C-ABI) per stream: host parse + H2D + kernels + D2H of every picture; "
                          f"{pics} frames in {t:.2f} s"}
