@@ -1790,7 +1790,9 @@ __device__ void row_pp(const ReconArgs &a, int p, int r, PPLds &L, const int w, 
             // rows 12..15 (chroma 6..7) are final: to the MB below, which
             // filters its top edge and stores them, or straight to the frame
             const uint32_t bflags = (uint32_t)__builtin_amdgcn_readfirstlane((int)avd) >> 24;
-            if ((bflags & (DB_INNER | DB_TOP)) == (DB_INNER | DB_TOP)) st_granT<MEL>(mbx_me + (size_t)c * 32 + gi, ent, tag);
+            // (lanes 0..23 hold the 24 granules once; the lanes above would
+            // store duplicates of them)
+            if ((bflags & (DB_INNER | DB_TOP)) == (DB_INNER | DB_TOP)) { if (lane < 24) st_granT<MEL>(mbx_me + (size_t)c * 32 + gi, ent, tag); }
             else if (lane < 24) fst((gi < 16 ? ybase + c * 16 : cbase + c * 8) + ent_glb, ent);
             if (prof && lane == 0) pmb[2] = (wall_clock64() & 0xFFFFFFFFull) | (tvd << 32);
         }
@@ -2564,7 +2566,7 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             const int kk = lane & 7;
             const uint8_t *px = R.px[slot];
             const uint32_t v = *(const uint32_t *)&px[kk < 4 ? 240 + kk * 4 : kk < 6 ? 312 + (kk - 4) * 4 : 376 + (kk - 6) * 4];
-            if (r + 1 < a.h) st_granT<MEL>(mbx_me + c * 32 + 24 + kk, v, a.epoch);
+            if (r + 1 < a.h && lane < 8) st_granT<MEL>(mbx_me + c * 32 + 24 + kk, v, a.epoch);
         }
         // PROF stamp [3]: MC start in bits 0..31, flag set (slot final) in bits 32..63 (100 MHz)
         if (PROF && lane == 0)
