@@ -917,6 +917,7 @@ extern "C" void *h264mi_engine_frame_ptr(h264mi_engine *e, int stream, int slot)
     return e->d_frames + e->frame_bytes * ((size_t)stream * e->nslots + slot);
 }
 
+extern "C" int h264mi_engine_abi(void) { return H264MI_ENGINE_ABI; }
 extern "C" size_t h264mi_engine_frame_bytes(h264mi_engine *e) { return e ? e->pic_bytes : 0; }
 extern "C" size_t h264mi_engine_slot_bytes(h264mi_engine *e) { return e ? e->frame_bytes : 0; }
 extern "C" int h264mi_engine_chroma_pitch(h264mi_engine *e) { return e ? e->cpitch : 0; }

@@ -117,6 +117,17 @@ struct ReconArgs {
 #define PROG_STRIDE 16          // u64 per row wave
 #endif
 #define PROG_AT(base, pic, h, r, w) ((base) + (((size_t)(pic) * (h) + (r)) * 2 + (w)) * PROG_STRIDE)
+// DEP_COLS finality rule, the one place it is stated (dep_rows_ok waits on
+// it, chk_access checks the loads against it).  It follows row_pp's store
+// map: MB x of row R is final once row R has stored MBs 0..x + DEPC_SAME_ROW - 1
+// (MB x + 1 stores MB x's columns 12..15 after its left edge) and row R + 1
+// MBs 0..x + DEPC_ROW_BELOW - 1 (MB (R + 1, x) stores row R's rows 12..15
+// after its top edge).  Where row_pp stores less late -- MB x's own rows
+// 12..15 when the MB below filters no top edge (top_on), whole MBs in
+// row_drain -- the rule is conservative.  A store moved later in row_pp must
+// move these.
+#define DEPC_SAME_ROW 2
+#define DEPC_ROW_BELOW 1
 // a row wave publishes its progress every PROG_EVERY of its MBs
 #ifndef PROG_EVERY
 #define PROG_EVERY 2
@@ -2123,7 +2134,7 @@ __device__ __forceinline__ bool dep_rows_ok(const ReconArgs &a, int p, int k, in
     const int pk = p - (k + 1) * a.S;
     bool ok = true;
     for (int R = rlo; R <= rhi + 1 && R < a.h; R++) {
-        const uint32_t need = (uint32_t)min(R <= rhi ? X + 2 : X + 1, a.w);
+        const uint32_t need = (uint32_t)min(R <= rhi ? X + DEPC_SAME_ROW : X + DEPC_ROW_BELOW, a.w);
         const unsigned long long c = R < PC_ROWS ? pc[k * PC_ROWS + R] : 0ull;
         uint32_t vx = (uint32_t)c, vy = (uint32_t)(c >> 32);
         if (min(vx, vy) < need && load) {
@@ -2369,7 +2380,8 @@ __device__ __forceinline__ bool chk_access(const ReconArgs &a, int pk, uint32_t 
         const int yb = min((int)(e / (uint32_t)pitch), rows - 1);
         const int xe = ya == yb ? min((int)(e % (uint32_t)pitch), width - 1) / mbw : (width - 1) / mbw;
         for (int R = ya / mbh; R <= yb / mbh; R++)
-            ok &= chk_row_final(a, pk, R, (uint32_t)min(xe + 2, a.w)) && chk_row_final(a, pk, R + 1, (uint32_t)min(xe + 1, a.w));
+            ok &= chk_row_final(a, pk, R, (uint32_t)min(xe + DEPC_SAME_ROW, a.w)) &&
+                  chk_row_final(a, pk, R + 1, (uint32_t)min(xe + DEPC_ROW_BELOW, a.w));
     }
     return ok;
 }

@@ -164,6 +164,18 @@ u32  broadwayGetMinorVersion(void);         /* Decoder.c:169 */
 /* ---------------------------------------------------------------------- */
 typedef struct h264mi_engine h264mi_engine;
 
+/* Engine C-ABI revision, bumped whenever a function or a record field keeps
+ * its name but changes meaning, so that an integration built against an
+ * older revision can refuse to run (compare H264MI_ENGINE_ABI at build time
+ * with h264mi_engine_abi() at run time):
+ *   5  h264mi_engine_frame_bytes returns the packed I420 size of one picture;
+ *      slots are h264mi_engine_slot_bytes apart and their chroma rows
+ *      h264mi_engine_chroma_pitch (H264MI_CPITCH) apart -- before, it was the
+ *      slot stride of unpadded I420 slots
+ *   6  PicDesc.flags bit 3 (PD_NO_DEBLOCK) for device-resident callers */
+#define H264MI_ENGINE_ABI 6
+int h264mi_engine_abi(void);
+
 /* Reconstruction engine for `nstreams` independent streams of one size
  * (w_mbs x h_mbs macroblocks), each with `nslots` frame slots in HBM. */
 h264mi_engine *h264mi_engine_create(int device, int w_mbs, int h_mbs, int nstreams, int nslots);
