@@ -2638,7 +2638,10 @@ struct WgppLds {
     static constexpr int RK = RPW == 1 ? (NMC == 2 ? RING1_2MC : RING1) : RINGG;
     static constexpr size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
     static constexpr size_t offM = a16(sizeof(PPLds) * RPW);
-    static constexpr size_t offR = offM + a16(sizeof(McScratch) * RPW * NMC);
+    // MC scratch per row: NMC, plus one for row wave 1 of the 2-MC single-row
+    // shape, which turns MC wave in pictures without deblocking (k_wgpp)
+    static constexpr int NMS = NMC + (NMC == 2 && RPW == 1 ? 1 : 0);
+    static constexpr size_t offR = offM + a16(sizeof(McScratch) * RPW * NMS);
     static constexpr size_t offX = offR + a16(sizeof(MbRing<RK>) * RPW);
     static size_t bytes(int w, bool dep3 = false)
     {
@@ -2685,9 +2688,14 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
     }
     const int jg = blockIdx.x / S, s = blockIdx.x - jg * S;
     const int j = jg / hg, g = jg - j * hg, p = j * S + s;
+    // a picture without deblocking (PD_NO_DEBLOCK; see below) in the 2-MC
+    // single-row shape: its rows are MC-bound, so row wave 1 runs as a third
+    // MC wave (MB claims only: P pictures, not intra-heavy ones)
+    const uint32_t pflags = __builtin_amdgcn_readfirstlane(a.pics[p].flags);
+    const int xmc = (Lay::NMS > NMC && (pflags & PD_NO_DEBLOCK) && !(pflags & PD_INTRA_HEAVY) && MC_DYN) ? 1 : 0;
     for (int q = 0; q < RPW; q++) {
         if (threadIdx.x < RK) { R[q].flag[threadIdx.x] = 0; R[q].lprog[threadIdx.x] = -1; R[q].cprog[threadIdx.x] = -1; }
-        if (threadIdx.x == 0) { R[q].consumed = 0; R[q].claim = NMC; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
+        if (threadIdx.x == 0) { R[q].consumed = 0; R[q].claim = NMC + xmc; L[q].hdone = 0; L[q].copied = 0; L[q].pdone = 0; L[q].fin = 0; }
     }
     for (int e = threadIdx.x; e < I4TAB_N; e += 64 * (NMC + 2) * RPW)
         L[0].i4tab[e] = i4_entry((e >> 4) % 9, e & 3, (e >> 2) & 3, e >= 9 * 16);
@@ -2721,7 +2729,7 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
         // chain, no row above), row wave 1 has nothing to do.  A host flag,
         // not a scan of the records here: any load on the row waves' way in
         // measurably delays the filtered pictures' first rows.
-        const bool nodb = __builtin_amdgcn_readfirstlane(a.pics[p].flags) & PD_NO_DEBLOCK;
+        const bool nodb = pflags & PD_NO_DEBLOCK;
         if (nodb) {
             if (wid == 0) {
                 const int fslot = __builtin_amdgcn_readfirstlane(a.pics[p].frame_base + a.pics[p].cur_slot);
@@ -2736,6 +2744,10 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
                                    (g_u64p)PROG_AT(a.prog, p, a.h, r, 0), (g_u64p)PROG_AT(a.prog, p, a.h, r, 1), a.epoch,
                                    (g_u32 *)(a.err + p), lane,
                                    (const __attribute__((address_space(1))) uint32_t *)(a.rec + a.pics[p].rec_base + r * a.w));
+            } else if (xmc) {
+                // the third MC wave: MB NMC first, then claims (R.claim starts at NMC + 1)
+                if (RPW == 1)
+                    mc_row<NMC, PROF, false, false, RK, CHK, DEPM>(a, p, r, NMC, lane, M[Lay::NMS - 1], R[q], L[0].i4tab, up, me, pc);
             }
         } else if (DEPM == DEP_COLS) row_pp<PROF, false, false, RK, CHK, true>(a, p, r, L[q], wid, lane, &R[q], up, me, j + 1 < a.P);
         else if (!upl && !mel) row_pp<PROF, false, false, RK, CHK>(a, p, r, L[q], wid, lane, &R[q], up, me);
@@ -2774,7 +2786,7 @@ __attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NM
         return;
     }
     static_assert(PREP, "k_wgpp's MC waves take k_prep outputs");
-    McScratch &Mw = M[q * NMC + wid - 2];
+    McScratch &Mw = M[q * Lay::NMS + wid - 2];
     if (!upl && !mel) mc_row<NMC, PROF, false, false, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
     else if (!upl) mc_row<NMC, PROF, false, true, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
     else if (mel) mc_row<NMC, PROF, true, true, RK, CHK, DEPM>(a, p, r, wid - 2, lane, Mw, R[q], L[0].i4tab, up, me, pc);
