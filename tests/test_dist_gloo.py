@@ -169,6 +169,26 @@ def test_e2e_core_plan_numa():
     assert mine == list(range(8)) and plan[1] == list(range(8, 16))
 
 
+def test_e2e_process_cpus_one_l3_each(monkeypatch):
+    """End-to-end decoder processes: one L3 domain (CCD) each when the share
+    has one per process, round-robin in order; otherwise the whole share."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    share = list(range(64))
+    monkeypatch.setattr(bench, "l3_groups", lambda cpus: [list(range(k, k + 8)) for k in range(0, 64, 8)])
+    per = bench.process_cpus(share, 8)
+    assert per == [list(range(k, k + 8)) for k in range(0, 64, 8)]
+    assert bench.process_cpus(share, 4) == per[:4]
+    monkeypatch.setattr(bench, "l3_groups", lambda cpus: [sorted(cpus)])
+    assert bench.process_cpus(share, 8) == [share] * 8
+    # this container's real sysfs: every group lies inside the share
+    monkeypatch.undo()
+    allowed = sorted(os.sched_getaffinity(0))
+    for g in bench.l3_groups(allowed):
+        assert g and set(g) <= set(allowed)
+
+
 def test_bench_gpus_mismatch_refused(monkeypatch):
     """--gpus N inside a torch.distributed environment of another size fails
     loudly instead of reporting the wrong n_gpus."""

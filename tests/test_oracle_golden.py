@@ -39,3 +39,6 @@ def test_fixture_inventory():
     names = set(CASES)
     assert {"cfg1_plumbing_640x368", "cfg2_720p_ionly_s1", "cfg5_2160p_s200"} <= names
     assert all(len(CASES[f"bench_1080p_s{s}"]["frames"]) == 60 for s in range(100, 108))
+    # the loop-filter-off encode of the same streams (bench leg cfg3_no_loop_filter)
+    assert all(len(CASES[f"bench_1080p_noloop_s{s}"]["frames"]) == 60 and
+               CASES[f"bench_1080p_noloop_s{s}"]["overrides"].get("dbf_idc1_pct") == 100 for s in range(100, 108))
