@@ -1,8 +1,8 @@
 // OpenMAX DL omxVCM4P10_* primitives (include/h264mi_omx.h) on the GPU.
 //
 // Each call packs its inputs -- neighbour samples, the reference window, the
-// edge region, unpacked coefficients -- into one job, runs k_omx over it on
-// the calling thread's own HIP stream and unpacks the result into the
+// edge region, unpacked coefficients -- into one job, has the calling thread's
+// resident job server (k_omx_server) run it and unpacks the result into the
 // caller's strided buffers.  The arithmetic restates the reference
 // implementations under Decoder/omxdl/reference/vc/m4p10/src (file cited per
 // primitive); their argument checks are mirrored on the host, before any
@@ -350,15 +350,96 @@ __device__ void k_omx_body(OmxJob &j, int t)
     }
 }
 
-// ---- host side: one job per call on the thread's own stream
+// ---- the per-thread job server.  A launch per call costs 16-17 us of launch
+// and stream-synchronisation latency against ~1 us of work, so each calling
+// thread keeps one workgroup resident that serves its jobs: the host writes the
+// job and a request number into pinned coherent memory, the server (polling
+// that number over PCIe) runs the primitive and writes the job and an
+// acknowledgement back; no launch, no stream wait.  The server leaves after
+// `idle` wall-clock ticks without a request or when asked to stop (the STOP
+// bit of req), and says so in `gone` before a last look at req; a host that
+// sees `gone` waits for the server's stream, and relaunches it from the last
+// request it saw if its own request was not served, so a request racing the
+// exit is never lost.
+struct OmxCtl {
+    uint32_t req, pad0[15];                 // host -> server (own 64-byte line): request number | STOP
+    uint32_t ack, gone, pad1[14];           // server -> host: last request done; GONE | last request seen
+};
+#define OMX_GONE 0x80000000u
+#define OMX_STOP 0x80000000u
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t *p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void k_omx_server(OmxJob *jp, OmxCtl *ctl, uint32_t last, uint64_t idle)
+{
+    __shared__ OmxJob js;
+    __shared__ uint32_t s_req, s_quit;
+    const int t = threadIdx.x;
+    const int nw = (int)(sizeof(OmxJob) / 4);
+    uint64_t t0 = wall_clock64();
+    for (;;) {
+        if (t == 0) {
+            uint32_t r, quit = 0;
+            for (;;) {
+                r = ld_sys(&ctl->req);
+                if (r & OMX_STOP) { quit = 1; r &= ~OMX_STOP; break; }
+                if (r != last) break;
+                if (wall_clock64() - t0 > idle) { quit = 1; break; }
+            }
+            if (quit) {                     // announce, then one last look at req
+                st_sys(&ctl->gone, OMX_GONE | last);
+                r = ld_sys(&ctl->req) & ~OMX_STOP;
+            }
+            s_req = r;
+            s_quit = quit;
+        }
+        __syncthreads();
+        const uint32_t r = s_req, quit = s_quit;
+        if (r == last) break;               // quitting with nothing pending: every wave leaves here
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        const uint32_t *src = (const uint32_t *)jp;
+        uint32_t *dst = (uint32_t *)&js;
+        for (int i = t; i < nw; i += 256) dst[i] = src[i];
+        __syncthreads();
+        k_omx_body(js, t);
+        __syncthreads();
+        for (int i = t; i < nw; i += 256) ((uint32_t *)jp)[i] = dst[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __syncthreads();
+        last = r;
+        if (t == 0) {
+            st_sys(&ctl->ack, r);
+            if (quit) st_sys(&ctl->gone, OMX_GONE | r);
+        }
+        if (quit) break;
+        t0 = wall_clock64();
+    }
+}
+
+// ---- host side: one job server per calling thread, on its own stream
 struct OmxCtx {
     hipStream_t st = nullptr;
     OmxJob *h = nullptr, *d = nullptr;      // pinned host job, its device address
-    int ok = 0;
+    OmxCtl *hc = nullptr, *dc = nullptr;    // pinned control words
+    uint32_t seq = 0;                       // last request posted (below the STOP bit)
+    uint64_t idle = 0;                      // server idle limit in wall-clock ticks
+    int ok = 0, server = 1, running = 0;
     ~OmxCtx()
     {
+        if (running) {
+            __atomic_store_n(&hc->req, seq | OMX_STOP, __ATOMIC_RELEASE);
+            (void)hipStreamSynchronize(st);
+        }
         if (st) (void)hipStreamDestroy(st);
         if (h) (void)hipHostFree(h);
+        if (hc) (void)hipHostFree(hc);
     }
 };
 thread_local OmxCtx g_ctx;
@@ -367,10 +448,18 @@ OmxJob *job_begin(int op)
 {
     OmxCtx &c = g_ctx;
     if (!c.ok) {
+        int dev = 0, khz = 0;
         if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess ||
             hipHostMalloc(&c.h, sizeof(OmxJob), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer((void **)&c.d, c.h, 0) != hipSuccess)
+            hipHostGetDevicePointer((void **)&c.d, c.h, 0) != hipSuccess ||
+            hipHostMalloc(&c.hc, sizeof(OmxCtl), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&c.dc, c.hc, 0) != hipSuccess || hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0)
             return nullptr;
+        memset(c.hc, 0, sizeof(OmxCtl));
+        const char *e = getenv("H264MI_OMX_SERVER");    // 0: one k_omx launch per call
+        c.server = !(e && e[0] == '0');
+        c.idle = (uint64_t)khz * 20;                    // 20 ms without a request
         c.ok = 1;
     }
     memset(c.h, 0, offsetof(OmxJob, in));
@@ -378,13 +467,46 @@ OmxJob *job_begin(int op)
     return c.h;
 }
 
-// k_omx on the mapped job, waited for; 0 or BadArgErr-independent failure (-1)
+int server_launch(OmxCtx &c, uint32_t last)
+{
+    __atomic_store_n(&c.hc->gone, 0u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(k_omx_server, dim3(1), dim3(256), 0, c.st, c.d, c.dc, last, c.idle);
+    if (hipGetLastError() != hipSuccess) return -1;
+    c.running = 1;
+    return 0;
+}
+
+// the job on the mapped page, run and waited for; 0 or a failure independent
+// of the arguments (-1)
 int job_run()
 {
     OmxCtx &c = g_ctx;
-    hipLaunchKernelGGL(k_omx, dim3(1), dim3(256), 0, c.st, c.d);
-    if (hipGetLastError() != hipSuccess) return -1;
-    return hipStreamSynchronize(c.st) == hipSuccess ? 0 : -1;
+    if (!c.server) {
+        hipLaunchKernelGGL(k_omx, dim3(1), dim3(256), 0, c.st, c.d);
+        if (hipGetLastError() != hipSuccess) return -1;
+        return hipStreamSynchronize(c.st) == hipSuccess ? 0 : -1;
+    }
+    c.seq = (c.seq + 1) & ~OMX_STOP;
+    if (!c.seq) c.seq = 1;
+    const uint32_t want = c.seq;
+    __atomic_store_n(&c.hc->req, want, __ATOMIC_RELEASE);
+    if (!c.running && server_launch(c, want - 1)) return -1;
+    for (uint64_t spin = 0;; spin++) {
+        if (__atomic_load_n(&c.hc->ack, __ATOMIC_ACQUIRE) == want) return 0;
+        const uint32_t g = __atomic_load_n(&c.hc->gone, __ATOMIC_ACQUIRE);
+        if (g & OMX_GONE) {                 // the server left; if it left before seeing this request, relaunch
+            if (hipStreamSynchronize(c.st) != hipSuccess) { c.running = 0; return -1; }
+            c.running = 0;
+            if (__atomic_load_n(&c.hc->ack, __ATOMIC_ACQUIRE) == want) return 0;
+            if (server_launch(c, g & ~OMX_GONE)) return -1;
+            spin = 0;
+        }
+        if ((spin & 0xFFFF) == 0xFFFF) {    // a faulted server shows on its stream
+            const hipError_t q = hipStreamQuery(c.st);
+            if (q != hipSuccess && q != hipErrorNotReady) { c.running = 0; return -1; }
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 inline bool misaligned(const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) != 0; }

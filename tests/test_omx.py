@@ -6,6 +6,8 @@ Randomised inputs, fixed seeds; outputs, updated pair-buffer pointers and
 return codes must be identical.  Argument-error cases run without a GPU."""
 import ctypes as C
 import os
+import threading
+import time
 
 import numpy as np
 import pytest
@@ -412,3 +414,45 @@ def test_argument_errors_match_reference(libs):
     ]
     for name, args in cases:
         assert getattr(ours, name)(*args) == getattr(ref, name)(*args) == BADARG, name
+
+
+# ------------------------------------------------ the per-thread job server
+def _i4_worker(libs, seed, n, pause_s, out):
+    rng = np.random.default_rng(seed)
+    try:
+        for it in range(n):
+            mode = it % 9
+            avail = I4_NEEDS[mode] | int(rng.choice([0, 1, 2, 32, 64, 1 | 64, 1 | 2 | 32 | 64]))
+            r_o, r_r, pairs = _both(libs, "omxVCM4P10_PredictIntra_4x4", _intra_case(rng, 4, mode, avail))
+            _check(r_o, r_r, pairs, ("i4", seed, mode, avail))
+            assert r_o == 0
+            if pause_s:
+                time.sleep(pause_s)
+        out[seed] = "ok"
+    except BaseException as e:  # reported by the main thread
+        out[seed] = repr(e)
+
+
+@pytest.mark.gpu
+def test_job_server_threads_idle_exit_and_launch_mode(libs):
+    """csrc/hip/omx.hip's job server: each calling thread has its own resident
+    server; four threads call concurrently, one of them pausing longer than the
+    server's 20 ms idle limit between calls (the server leaves and is relaunched
+    from the last request it saw), and one more runs the launch-per-call mode
+    (H264MI_OMX_SERVER=0, read when the thread's context is made).  Every
+    result equals the reference's."""
+    out = {}
+    ths = [threading.Thread(target=_i4_worker, args=(libs, s, 400, 0.0, out)) for s in (11, 12, 13)]
+    ths.append(threading.Thread(target=_i4_worker, args=(libs, 14, 12, 0.03, out)))
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    os.environ["H264MI_OMX_SERVER"] = "0"
+    try:
+        t = threading.Thread(target=_i4_worker, args=(libs, 15, 100, 0.0, out))
+        t.start()
+        t.join(timeout=120)
+    finally:
+        del os.environ["H264MI_OMX_SERVER"]
+    assert out == {s: "ok" for s in (11, 12, 13, 14, 15)}, out

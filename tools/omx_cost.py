@@ -1,6 +1,7 @@
 """Diagnostics (not a test): what one call of the OpenMAX DL surface costs
-(csrc/hip/omx.hip: each call packs its job, runs k_omx on the calling
-thread's HIP stream and waits for it).  Times N back-to-back calls of four
+(csrc/hip/omx.hip: each call packs its job into pinned memory; the calling
+thread's resident job server runs it, or with H264MI_OMX_SERVER=0 one k_omx
+launch per call, waited for).  Times N back-to-back calls of four
 primitives on aligned host buffers and prints microseconds per call, plus what
 an OMXDL-configured h264bsd would spend per 1080p P picture at the call counts
 of configs[3]'s MB mix.  Usage: python tools/omx_cost.py [N]"""
@@ -8,6 +9,7 @@ import ctypes as C
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -52,24 +54,48 @@ def main(n):
         "DequantTransformResidualFromPairAndAdd (4x4)": lambda: (ppair.__setattr__("value", P(pair)),
                                                                  lib.omxVCM4P10_DequantTransformResidualFromPairAndAdd(C.byref(ppair), P(pred), None, P(out4), 4, 4, 28, 1))[1],
     }
-    res = {}
-    for name, f in calls.items():
-        for _ in range(20):
-            f()
-        t = time.perf_counter()
-        for _ in range(n):
-            r = f()
-        dt = (time.perf_counter() - t) / n * 1e6
-        res[name] = {"us_per_call": round(dt, 2), "ret": int(r)}
+    def timed(res):
+        for name, f in calls.items():
+            for _ in range(20):
+                f()
+            t = time.perf_counter()
+            for _ in range(n):
+                r = f()
+            dt = (time.perf_counter() - t) / n * 1e6
+            res[name] = {"us_per_call": round(dt, 2), "ret": int(r)}
+
+    def in_thread(server):
+        # the mode is read when a thread's context is made: one fresh thread per mode
+        res = {}
+        os.environ["H264MI_OMX_SERVER"] = "1" if server else "0"
+        th = threading.Thread(target=timed, args=(res,))
+        th.start()
+        th.join()
+        return res
+
+    # the Python/ctypes floor: the same call shape rejected on the host
+    # (dstStep 4 below the width 16: BadArgErr before any device work)
+    bad = lambda: lib.omxVCM4P10_InterpolateLuma(P(src, 8 * 64 + 8), 64, P(dst), 4, 2, 2, Size(16, 16))
+    for _ in range(20):
+        bad()
+    t = time.perf_counter()
+    for _ in range(n):
+        rb = bad()
+    floor = (time.perf_counter() - t) / n * 1e6
+    launch = in_thread(False)
+    res = in_thread(True)
     # an OMXDL h264bsd's calls per 1080p P picture (8,160 MBs): per inter MB one
     # luma + two chroma interpolations per partition (configs[3] mix: ~2
     # partitions per MB), per MB 4 luma + 4 chroma deblocking edge calls, per
     # coded 4x4 block one residual call (~8 per MB)
     per_mb = 2 * 3 + 8 + 8
     us = np.mean([v["us_per_call"] for v in res.values()])
-    out = {"calls": res, "calls_per_1080p_picture_est": per_mb * 8160,
+    us_l = np.mean([v["us_per_call"] for v in launch.values()])
+    out = {"calls": res, "python_ctypes_floor_us": round(floor, 2), "floor_ret": int(rb), "calls_per_1080p_picture_est": per_mb * 8160,
            "seconds_per_1080p_picture_est": round(per_mb * 8160 * us * 1e-6, 2),
-           "note": "synchronous k_omx launch per call; the product path (k_wgpp) reconstructs a 1080p P picture in ~0.3 ms"}
+           "launch_per_call": {"calls": launch, "seconds_per_1080p_picture_est": round(per_mb * 8160 * us_l * 1e-6, 2)},
+           "note": "calls: the thread's resident job server; launch_per_call: H264MI_OMX_SERVER=0. "
+                   "The product path (k_wgpp) reconstructs a 1080p P picture in ~0.3 ms"}
     print(json.dumps(out, indent=1))
 
 
