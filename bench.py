@@ -1161,8 +1161,9 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0, overrides
     assert all(c.errors == 0 and c.npics >= nframes for c in caps), "leg stream preparation failed"
     S = len(caps)
     w, h = caps[0].w_mbs, caps[0].h_mbs
-    # both knobs are read once, when the engine is created
-    if pipe == 1:
+    # both knobs are read once, when the engine is created; mc_waves 0: the
+    # engine's own per-launch choice (engine.hip launch_nmc)
+    if pipe == 1 and mc_waves:
         os.environ["H264MI_MC_WAVES"] = str(mc_waves)
     if rpw:
         os.environ["H264MI_RPW"] = str(rpw)
@@ -1191,7 +1192,7 @@ def run_leg(L, torch, config, seeds, steps, warmup, mc_waves=3, rpw=0, overrides
                 **({"generator_overrides": overrides} if overrides else {}),
                 **({"steps_per_launch": run.P, "avg_kernel_us_per_step": round(per_step, 2),
                     "dependency_modes": [{1: "rows", 2: "cols"}[m] for m in modes]} if pipe > 1 else {}),
-                "mc_waves_per_row_workgroup": mc_waves if pipe == 1 else 2,
+                "mc_waves_per_row_workgroup": run.eng.last_mc_waves() if hasattr(run.eng, "last_mc_waves") else mc_waves,
                 "rows_per_workgroup": run.eng.rows_per_workgroup(S),
                 "frames_per_s": round(S * steps / dt, 1), "avg_launch_us": round(launch_us, 2),
                 "picture_latency_ms": round(launch_us / 1e3, 3),
@@ -1209,8 +1210,8 @@ def config_legs(L, torch):
     stream, the config-3 mix) with the MC-wave count of the row workgroup
     swept (2 vs 3: the sizing choice of this design)."""
     return {
-        "cfg2_720p_ionly_4streams": run_leg(L, torch, 1, [1, 2, 3, 4], 20, 4),
-        "cfg2_720p_ionly_1stream": run_leg(L, torch, 1, [1], 20, 4),
+        "cfg2_720p_ionly_4streams": run_leg(L, torch, 1, [1, 2, 3, 4], 20, 4, mc_waves=0),
+        "cfg2_720p_ionly_1stream": run_leg(L, torch, 1, [1], 20, 4, mc_waves=0),
         "cfg5_2160p_1stream": run_leg(L, torch, 4, [100], 20, 4),
         "cfg5_2160p_1stream_2mc": run_leg(L, torch, 4, [100], 20, 4, mc_waves=2),
         "cfg5_2160p_1stream_2rows": run_leg(L, torch, 4, [100], 20, 4, rpw=2),

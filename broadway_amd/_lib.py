@@ -147,6 +147,9 @@ def mi() -> C.CDLL:
         L.h264mi_engine_hint_deps.restype = i32
         L.h264mi_engine_last_deps.argtypes = [vp]
         L.h264mi_engine_last_deps.restype = i32
+    if hasattr(L, "h264mi_engine_last_mc_waves"):
+        L.h264mi_engine_last_mc_waves.argtypes = [vp]
+        L.h264mi_engine_last_mc_waves.restype = i32
     L.h264mi_engine_decode_device_next.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.h264mi_engine_decode_device_next.restype = i32
     L.h264mi_engine_decode_device_steps.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp]

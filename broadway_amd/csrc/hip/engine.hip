@@ -39,6 +39,7 @@ struct h264mi_engine {
     unsigned long long *d_gjunk;  // 64 KiB store sink (ReconArgs::gjunk)
     const char *last_kernel;      // name of the last batch's reconstruction kernel (diagnostics)
     int last_dep;                 // the last batch's dependency mode (DEP_NONE / DEP_ROWS / DEP_COLS)
+    int last_nmc;                 // the last batch's MC waves per row workgroup
     uint8_t *d_dbrec;         // 64 B per batch MB (x2: k_prep double buffer)
     int16_t *d_res;           // 384 x int16 per batch MB (x2)
     // k_prep (deblocking records + residuals) writes buffer half prep_parity;
@@ -55,7 +56,8 @@ struct h264mi_engine {
     int prep_wgs;                      // tail workgroups per launch (H264MI_PREP_WGS, default 2048)
     unsigned long long rows_launched;
     int prep_at_pct;                   // tail prep waits for this % of the launch's rows (H264MI_PREP_AT; 0: no wait)
-    int mc_waves;                      // MC waves per row workgroup: 0 = per launch (below), 2 or 3 forced (H264MI_MC_WAVES)
+    int mc_waves;                      // MC waves per row workgroup: 0 = per launch (below), 2, 3 or 6 forced (H264MI_MC_WAVES)
+    int intra_mc6;                     // intra-heavy launches may take 6 MC waves (launch_nmc; H264MI_INTRA_MC6=0: 3)
     int launch_intra;                  // next launch: 1 = has an intra-heavy picture, 0 = none, -1 = unknown
     int dep_mode;                      // frame-pipelined launches: DEP_ROWS / DEP_COLS (H264MI_DEP_MODE; default rows)
     int launch_dep;                    // next launch's mode (h264mi_engine_hint_deps), 0 = dep_mode
@@ -135,7 +137,9 @@ static void engine_config(h264mi_engine *e)
     const char *pa = getenv("H264MI_PREP_AT");
     e->prep_at_pct = pa ? atoi(pa) : 0;
     const char *mw = getenv("H264MI_MC_WAVES");
-    e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3) ? atoi(mw) : 0;
+    e->mc_waves = mw && (atoi(mw) == 2 || atoi(mw) == 3 || atoi(mw) == 6) ? atoi(mw) : 0;
+    const char *m6 = getenv("H264MI_INTRA_MC6");
+    e->intra_mc6 = m6 ? atoi(m6) != 0 : 1;
     e->launch_intra = -1;
     {
         const char *dm = getenv("H264MI_DEP_MODE");
@@ -167,6 +171,12 @@ static void engine_config(h264mi_engine *e)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 1>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<6, true, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<6, false, true, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<6, false, true, 1, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, false, true, 2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1>),
@@ -193,7 +203,7 @@ static void engine_config(h264mi_engine *e)
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&k_wgpp<2, true, true, 1, false, DEP_COLS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
+    const size_t row_lds = sizeof(PPLds) + (size_t)(e->mc_waves == 2 ? 2 : e->mc_waves == 6 ? 6 : 3) * sizeof(McScratch) + sizeof(MbRing<RINGG>);
     e->rpw_max = e->mc_waves == 2 ? 2 : 3;
     while (e->rpw_max > 1 && (size_t)(e->rpw_max - 1) * e->w * 256 + (size_t)e->rpw_max * row_lds > 156 * 1024)
         e->rpw_max--;
@@ -327,6 +337,7 @@ static int rows_per_wg(const h264mi_engine *e, int S)
     int rpw = e->rpw_env ? e->rpw_env : (S * e->h > 3 * e->ncu ? 3 : 1);
     if (rpw > e->rpw_max) rpw = e->rpw_max;
     if (e->mc_waves == 2 && rpw > 2) rpw = 2;
+    if (e->mc_waves == 6) rpw = 1;
     return rpw;
 }
 
@@ -342,13 +353,19 @@ static int rows_per_wg(const h264mi_engine *e, int S)
 // two steps per stream always takes 2: twice the rows compete for workgroup
 // slots, and 768 of them beat the third wave even with an IDR among the
 // pictures (configs[3] GOP mix: launches holding an IDR 671 vs 754 us,
-// profiles/r75_ab_idr_second.txt).
-static int launch_nmc(const h264mi_engine *e, int rpw, int P)
+// profiles/r75_ab_idr_second.txt).  An intra-heavy launch whose rows all fit
+// two 8-wave workgroups per CU takes six MC waves: an intra row's pace is its
+// MC waves' throughput (each wave holds an MB through the left-neighbour
+// waits of its 4x4 blocks), 720p I pictures 341.6 / 324.0 / 320.2 / 316.7 us
+// with 3 / 4 / 5 / 6 (profiles/r162_*, r163_*); above that the rows would
+// wait for slots.
+static int launch_nmc(const h264mi_engine *e, int rpw, int P, int npics)
 {
     if (e->mc_waves) return e->mc_waves;
     if (rpw > 1) return 3;
     if (P > 1) return 2;
-    return e->launch_intra == 0 ? 2 : 3;
+    if (e->launch_intra == 0) return 2;
+    return e->launch_intra > 0 && e->intra_mc6 && npics * e->h <= 2 * e->ncu ? 6 : 3;
 }
 
 static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, const int16_t *d_coef,
@@ -461,12 +478,13 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
     e->last_dep = dep3 ? dmode : DEP_NONE;
     const int rpw = dep3 ? 1 : rows_per_wg(e, S);
     const dim3 grid(npics * ((e->h + rpw - 1) / rpw) + a.prep_wgs);
-    const int nmc = dep3 ? 2 : launch_nmc(e, rpw, P);
+    const int nmc = dep3 ? 2 : launch_nmc(e, rpw, P, npics);
+    e->last_nmc = nmc;
     e->launch_intra = -1;                     // a hint covers one launch
     const size_t lmbx = nmc == 2 && (!a.prof || rpw == 1) ? (rpw == 2 ? WgppLds<2, 2>::bytes(e->w)
                                                                       : WgppLds<2, 1>::bytes(e->w, dep3 && dmode == DEP_COLS))
                         : rpw == 3 ? WgppLds<3, 3>::bytes(e->w) : rpw == 2 ? WgppLds<3, 2>::bytes(e->w)
-                        : WgppLds<3, 1>::bytes(e->w);
+                        : nmc == 6 ? WgppLds<6, 1>::bytes(e->w) : WgppLds<3, 1>::bytes(e->w);
     if (dep3) {
         e->last_kernel = e->check ? "k_wgpp_check" : a.prof ? "k_wgpp_prof" : "k_wgpp";
 #define DEP_LAUNCH(M)                                                                                          \
@@ -489,6 +507,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         if (rpw == 3) hipLaunchKernelGGL((k_wgpp<3, true, true, 3>), grid, dim3(960), lmbx, e->st, a);
         else if (rpw == 2) hipLaunchKernelGGL((k_wgpp<3, true, true, 2>), grid, dim3(640), lmbx, e->st, a);
         else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, true, true, 1>), grid, dim3(256), lmbx, e->st, a);
+        else if (nmc == 6) hipLaunchKernelGGL((k_wgpp<6, true, true, 1>), grid, dim3(512), lmbx, e->st, a);
         else hipLaunchKernelGGL((k_wgpp<3, true, true, 1>), grid, dim3(320), lmbx, e->st, a);
         if (rec) (void)hipEventRecord(t2, e->st);
     } else if (e->check) {
@@ -500,6 +519,7 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         else if (rpw == 2 && nmc == 2) hipLaunchKernelGGL((k_wgpp<2, false, true, 2, true>), grid, dim3(512), lmbx, e->st, a);
         else if (rpw == 2) hipLaunchKernelGGL((k_wgpp<3, false, true, 2, true>), grid, dim3(640), lmbx, e->st, a);
         else if (nmc == 2) hipLaunchKernelGGL((k_wgpp<2, false, true, 1, true>), grid, dim3(256), lmbx, e->st, a);
+        else if (nmc == 6) hipLaunchKernelGGL((k_wgpp<6, false, true, 1, true>), grid, dim3(512), lmbx, e->st, a);
         else hipLaunchKernelGGL((k_wgpp<3, false, true, 1, true>), grid, dim3(320), lmbx, e->st, a);
         if (rec) (void)hipEventRecord(t2, e->st);
     } else if (nmc == 2) {
@@ -510,6 +530,9 @@ static int launch_batch(h264mi_engine *e, int S, int P, const MbRec *d_rec, cons
         else
             hipExtLaunchKernelGGL((k_wgpp<2, false, true, 1>), grid, dim3(256), lmbx, e->st, rec ? t0 : nullptr,
                                   rec ? t2 : nullptr, 0, a);
+    } else if (nmc == 6) {
+        hipExtLaunchKernelGGL((k_wgpp<6, false, true, 1>), grid, dim3(512), lmbx, e->st, rec ? t0 : nullptr,
+                              rec ? t2 : nullptr, 0, a);
     } else if (rpw == 3) {
         // the timing events ride on the kernel's own dispatch packet
         // (hipExtLaunchKernelGGL): no marker packets between launches
@@ -606,6 +629,7 @@ extern "C" int h264mi_engine_hint_deps(h264mi_engine *e, int mode)
     return 0;
 }
 extern "C" int h264mi_engine_last_deps(h264mi_engine *e) { return e ? e->last_dep : -1; }
+extern "C" int h264mi_engine_last_mc_waves(h264mi_engine *e) { return e ? e->last_nmc : -1; }
 
 extern "C" int h264mi_engine_decode_device(h264mi_engine *e, int npics, const void *d_recs, const int16_t *d_coef,
                                            const void *d_pics)

@@ -767,19 +767,20 @@ __device__ __forceinline__ void prog_set(int *p, int v, int lane)
 // the left column comes from the left MB's ring slot, part by part (LeftNb):
 // prediction + residual (res: the MB's residual staged in LDS) + clip, all
 // written straight into the ring slot px (I4x4 luma into the tile as well:
-// each block predicts from the blocks before it).  Chroma first (it waits
-// only for the left MB's chroma), then luma: an I4x4 block in column 0
-// waits for the left MB's block beside it, so the next MB's blocks follow
+// each block predicts from the blocks before it).  `part` 1 = luma, 2 =
+// chroma (mc_intra runs luma first and publishes its bottom row before the
+// chroma); chroma waits only for the left MB's chroma, an I4x4 block in
+// column 0 for the left MB's block beside it, so the next MB's blocks follow
 // this one's 3 steps behind.  Every lane issues all of its LDS reads of a
 // phase before it uses any, so a phase costs one LDS round trip
 // (Intra16x16 :626-686, Intra4x4 :700-832, IntraChroma :844-914,
 // AddResidual :926-988).
 __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
                                            uint8_t *ty, uint8_t *tu, uint8_t *tv, const uint32_t *i4tab, uint8_t *junk,
-                                           uint8_t *px, int lane, const LeftNb &N)
+                                           uint8_t *px, int lane, const LeftNb &N, int part = 3)
 {
     const bool aA = avail & AV_A, aB = avail & AV_B;
-    {   // chroma: lane -> (comp, row, pair), straight into the slot
+    if (part & 2) {   // chroma: lane -> (comp, row, pair), straight into the slot
         if (aA) {
             prog_wait(N.cprog, N.ltag | 1, lane, N.perr, N.chk);
             if (lane < 16) {
@@ -834,7 +835,8 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
         *(uint16_t *)&px[o] = (uint16_t)(pv[0] | (pv[1] << 8));
         prog_set(N.my_cprog, N.mytag | 1, lane);
     }
-    if (mbtype == MBT_I16) {
+    if (!(part & 1)) {
+    } else if (mbtype == MBT_I16) {
         if (aA) {
             prog_wait(N.lprog, N.ltag | 10, lane, N.perr, N.chk);
             if (lane < 16) ty[(lane + 1) * TY_STRIDE + TX0 - 1] = N.lp[lane * 16 + 15];
@@ -1254,12 +1256,22 @@ typedef __attribute__((address_space(3))) McScratch lds_McScratch;
 typedef const __attribute__((address_space(3))) uint32_t lds_cu32;
 typedef const __attribute__((address_space(1))) MbRec g_MbRec;
 typedef __attribute__((address_space(1))) unsigned g_u32;
-template <bool UPL, int RK, bool CHK>
+// LF (the 6-MC-wave intra-heavy instance): luma first, its bottom row
+// published before the chroma runs (below).  PROF builds pass the MB's
+// profiling stamps in `pq` (and the caller publishes the luma bottom row with
+// the chroma); LF builds pass where this MB's luma bottom row goes (the row
+// below's mailbox entry, NULL in the last row) -- one pointer argument either
+// way: a second one costs the callers' spills.  The other instances keep
+// chroma first and one wait for the row above (luma-first measured slower in
+// P pictures: configs[3] 295.1 vs 287.9 us per step, profiles/r167_*)
+template <bool UPL, bool MEL, int RK, bool CHK, bool PROF, bool LF>
 __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigned long long *mbx_up, g_u32 *perr_g,
                                                    int W, int c, uint32_t tag, bool has_up, int lane, lds_McScratch *Ml,
                                                    __attribute__((address_space(3))) MbRing<RK> *Rl, lds_cu32 *i4tab_l,
-                                                   __attribute__((address_space(1))) unsigned long long *pst)
+                                                   unsigned long long *pq)
 {
+    __attribute__((address_space(1))) unsigned long long *const pst = PROF ? (__attribute__((address_space(1))) unsigned long long *)pq : nullptr;
+    unsigned long long *const pub = PROF || !LF ? nullptr : pq;
     // pst (profiling build): [0] left ready | top ready, [1] prediction done | slot written
     unsigned long long st0 = 0, st1 = 0;
     McScratch &M = *(McScratch *)Ml;
@@ -1293,39 +1305,94 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     const unsigned long long *g = mbx_up + min(max(c + dsel, 0), W - 1) * 32 + dw;
     const bool mine = need_top && ((lane >= 24 && lane < 32 && aB) || (lane == 32 && needC) || (lane >= 33 && lane < 36 && aD));
     unsigned long long gr = need_top ? ld_granT<UPL>(g) : 0ull;
-    if (pst) st0 = wall_clock64();
-    if (need_top) {
-        unsigned spins = 0;
-        while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-            if (mine) gr = ld_granT<UPL>(g);
+    if constexpr (!LF) {
+        if (pst) st0 = wall_clock64();
+        if (need_top) {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
+                if (mine) gr = ld_granT<UPL>(g);
+            }
         }
-    }
-    const uint32_t top = (uint32_t)gr;
-    if (pst) st0 = (st0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
-    {   // tile halo: the row above (dwords), its top-left / top-right (the left
-        // column is read from the left MB's slot as it lands, intra_tile)
-        if (lane >= 24 && lane < 32) {
-            const int k = lane - 24;
-            if (aB) *(uint32_t *)(k < 4 ? &M.ty[TX0 + k * 4] : k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
-        } else if (lane == 32) {
-            if (needC) *(uint32_t *)&M.ty[TX0 + 16] = top;
-        } else if (lane < 36) {
-            if (aD) (lane == 33 ? M.ty[TX0 - 1] : lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
+        const uint32_t top = (uint32_t)gr;
+        if (pst) st0 = (st0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
+        {   // tile halo: the row above (dwords), its top-left / top-right (the left
+            // column is read from the left MB's slot as it lands, intra_tile)
+            if (lane >= 24 && lane < 32) {
+                const int k = lane - 24;
+                if (aB) *(uint32_t *)(k < 4 ? &M.ty[TX0 + k * 4] : k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
+            } else if (lane == 32) {
+                if (needC) *(uint32_t *)&M.ty[TX0 + 16] = top;
+            } else if (lane < 36) {
+                if (aD) (lane == 33 ? M.ty[TX0 - 1] : lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
+            }
         }
+        wave_sync();
+        uint8_t *px = R.px[slot];
+        const int ls = (c - 1) & (RK - 1);
+        LeftNb N;
+        N.lp = R.px[ls];
+        N.lprog = &R.lprog[ls]; N.cprog = &R.cprog[ls];
+        N.my_lprog = &R.lprog[slot]; N.my_cprog = &R.cprog[slot];
+        N.ltag = (c - 1) << 4; N.mytag = c << 4;
+        N.perr = perr;
+        N.chk = CHK;
+        intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
+    } else {
+        if (pst) st0 = wall_clock64();
+        // luma first: its top granules (B dwords 24..27, C, D's luma byte) are
+        // waited for and its bottom row is published before the chroma runs, so
+        // the row below's luma -- the intra chain from row to row -- does not
+        // wait behind this MB's chroma; the chroma granules follow
+        const bool lumal = (lane >= 24 && lane < 28) || lane == 32 || lane == 33;
+        auto top_wait = [&](bool mine_part) {
+            unsigned spins = 0;
+            while (__builtin_amdgcn_ballot_w64(mine_part && (uint32_t)(gr >> 32) != tag) != 0) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
+                if (mine_part) gr = ld_granT<UPL>(g);
+            }
+        };
+        if (need_top) top_wait(mine && lumal);
+        if (pst) st0 = (st0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
+        {   // luma tile halo: the row above (dwords), its top-left / top-right (the
+            // left column is read from the left MB's slot as it lands, intra_tile)
+            const uint32_t top = (uint32_t)gr;
+            if (lane >= 24 && lane < 28) {
+                if (aB) *(uint32_t *)&M.ty[TX0 + (lane - 24) * 4] = top;
+            } else if (lane == 32) {
+                if (needC) *(uint32_t *)&M.ty[TX0 + 16] = top;
+            } else if (lane == 33) {
+                if (aD) M.ty[TX0 - 1] = (uint8_t)(top >> 24);
+            }
+        }
+        wave_sync();
+        uint8_t *px = R.px[slot];
+        const int ls = (c - 1) & (RK - 1);
+        LeftNb N;
+        N.lp = R.px[ls];
+        N.lprog = &R.lprog[ls]; N.cprog = &R.cprog[ls];
+        N.my_lprog = &R.lprog[slot]; N.my_cprog = &R.cprog[slot];
+        N.ltag = (c - 1) << 4; N.mytag = c << 4;
+        N.perr = perr;
+        N.chk = CHK;
+        intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N, 1);
+        if (pub && lane < 4)        // luma bottom row -> the row below (entry c, dwords 24..27)
+            st_granT<MEL>(pub + 24 + lane, *(const uint32_t *)&px[240 + lane * 4], tag);
+        if (need_top) top_wait(mine && !lumal);
+        {   // chroma tile halo
+            const uint32_t top = (uint32_t)gr;
+            if (lane >= 28 && lane < 32) {
+                const int k = lane - 24;
+                if (aB) *(uint32_t *)(k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
+            } else if (lane == 34 || lane == 35) {
+                if (aD) (lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
+            }
+        }
+        wave_sync();
+        intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N, 2);
     }
-    wave_sync();
-    uint8_t *px = R.px[slot];
-    const int ls = (c - 1) & (RK - 1);
-    LeftNb N;
-    N.lp = R.px[ls];
-    N.lprog = &R.lprog[ls]; N.cprog = &R.cprog[ls];
-    N.my_lprog = &R.lprog[slot]; N.my_cprog = &R.cprog[slot];
-    N.ltag = (c - 1) << 4; N.mytag = c << 4;
-    N.perr = perr;
-    N.chk = CHK;
-    intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
     if (pst) st1 = wall_clock64();
     if (pst && lane == 0) { pst[0] = st0; pst[1] = (st1 & 0xFFFFFFFFull) | (wall_clock64() << 32); }
 }
@@ -2568,17 +2635,20 @@ __device__ __forceinline__ void mc_row(const ReconArgs &a, int p, int r, int c0,
             ((uint32_t *)R.px[slot])[lane] = src[lane];
             if (lane < 32) ((uint32_t *)R.px[slot])[64 + lane] = src[64 + lane];
         } else if (type >= MBT_I4x4) {
-            mc_intra<UPL, RK, CHK>((g_MbRec *)(a.rec + pd.rec_base + r * a.w + c), mbx_up, (g_u32 *)(a.err + p), a.w, c, a.epoch,
+            mc_intra<UPL, MEL, RK, CHK, PROF, NMC == 6>((g_MbRec *)(a.rec + pd.rec_base + r * a.w + c), mbx_up, (g_u32 *)(a.err + p), a.w, c, a.epoch,
                               r > 0, lane, (lds_McScratch *)&Mw, (__attribute__((address_space(3))) MbRing<RK> *)&R,
                               (lds_cu32 *)i4tab,
-                              (__attribute__((address_space(1))) unsigned long long *)(PROF ? a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4 : nullptr));
+                              PROF ? (unsigned long long *)(a.prof + (size_t)a.npics * a.h * 16 + ((size_t)(p * a.h + r) * a.w + c) * PROF_MB + 4)
+                                   : NMC == 6 && r + 1 < a.h ? mbx_me + c * 32 : nullptr);
         }
         wave_sync();
-        {   // unfiltered bottom row -> the row below's intra neighbours (entry c, dwords 24..31)
+        {   // unfiltered bottom row -> the row below's intra neighbours (entry c,
+            // dwords 24..31; an intra MB published its luma dwords 24..27 itself)
             const int kk = lane & 7;
             const uint8_t *px = R.px[slot];
             const uint32_t v = *(const uint32_t *)&px[kk < 4 ? 240 + kk * 4 : kk < 6 ? 312 + (kk - 4) * 4 : 376 + (kk - 6) * 4];
-            if (r + 1 < a.h && lane < 8) st_granT<MEL>(mbx_me + c * 32 + 24 + kk, v, a.epoch);
+            const int k0 = NMC == 6 && !PROF && (type == MBT_I4x4 || type == MBT_I16) ? 4 : 0;
+            if (r + 1 < a.h && lane < 8 && kk >= k0) st_granT<MEL>(mbx_me + c * 32 + 24 + kk, v, a.epoch);
         }
         // PROF stamp [3]: MC start in bits 0..31, flag set (slot final) in bits 32..63 (100 MHz)
         if (PROF && lane == 0)
@@ -2666,7 +2736,7 @@ struct WgppLds {
 // single-step launches carry none of it
 template <int NMC, bool PROF, bool PREP, int RPW, bool CHK = false, int DEPM = DEP_NONE>
 __global__ __launch_bounds__(64 * (NMC + 2) * RPW)
-__attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC == 3 || RPW > 1 ? 4 : WGPP2_WAVES_PER_EU))) void k_wgpp(ReconArgs a)
+__attribute__((amdgpu_waves_per_eu(NMC == 3 && RPW == 1 ? WGPP_WAVES_PER_EU : NMC >= 3 || RPW > 1 ? 4 : WGPP2_WAVES_PER_EU))) void k_wgpp(ReconArgs a)
 {
     using Lay = WgppLds<NMC, RPW>;
     constexpr int RK = Lay::RK;
@@ -2800,12 +2870,17 @@ template __global__ void k_wgpp<3, false, true, 3>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 2>(ReconArgs);
 template __global__ void k_wgpp<2, true, true, 1>(ReconArgs);
 template __global__ void k_wgpp<3, true, true, 3>(ReconArgs);
+// intra-heavy single-step launches whose rows all fit two workgroups per CU:
+// six MC waves per row (engine launch_nmc)
+template __global__ void k_wgpp<6, false, true, 1>(ReconArgs);
+template __global__ void k_wgpp<6, true, true, 1>(ReconArgs);
 // dependency-checker instantiations (H264MI_CHECK=1)
 template __global__ void k_wgpp<3, false, true, 1, true>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 1, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 2, true>(ReconArgs);
 template __global__ void k_wgpp<2, false, true, 2, true>(ReconArgs);
 template __global__ void k_wgpp<3, false, true, 3, true>(ReconArgs);
+template __global__ void k_wgpp<6, false, true, 1, true>(ReconArgs);
 // frame-pipelined launches (single-row, 2 MC waves: launch_batch), by
 // dependency mode; the profiling builds for tools/prof_steps.py
 template __global__ void k_wgpp<2, false, true, 1, false, DEP_ROWS>(ReconArgs);

@@ -128,6 +128,12 @@ class Engine:
             return -1
         return int(self._L.h264mi_engine_last_deps(self._h))
 
+    def last_mc_waves(self) -> int:
+        """MC waves per row workgroup of the last launch (-1: an older build)."""
+        if not hasattr(self._L, "h264mi_engine_last_mc_waves"):
+            return -1
+        return int(self._L.h264mi_engine_last_mc_waves(self._h))
+
     def hint_intra(self, intra_heavy: bool) -> None:
         """Shape hint for the next device-resident launch: does some picture
         have more than half its MBs intra (include/h264mi.h)."""

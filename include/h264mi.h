@@ -194,6 +194,9 @@ int h264mi_engine_decode(h264mi_engine *e, int npics, const int *stream, const i
  * the launch uses 3.  A hint covers one launch.  Returns 0, or -1 on a bad
  * argument. */
 int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy);
+/* MC waves per row workgroup of the last launch: 2 or 3, or 6 for an
+ * intra-heavy launch whose rows all fit two workgroups per CU (diagnostics) */
+int h264mi_engine_last_mc_waves(h264mi_engine *e);
 /* the next frame-pipelined launch's dependency mode: 1 whole MB rows of the
  * earlier steps' pictures (MbRec.i4 rows from h264mi_capture), 2 (MB row, MB
  * column) cells (geometry in the kernel), 0 the engine's default

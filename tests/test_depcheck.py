@@ -134,3 +134,24 @@ def test_checker_catches_short_reference_rows(monkeypatch):
         assert run.eng.error_bits() & CHK_REFROW
     finally:
         run.free()
+
+
+def test_checker_intra_heavy_six_mc_waves_clean(monkeypatch):
+    """Config 2 (720p I-only, 4 streams): intra-heavy one-step launches whose
+    rows fit two workgroups per CU take six MC waves and the luma-first intra
+    path (engine.hip launch_nmc, recon_kernels.hip mc_intra LF) -- under the
+    checker, every picture vs the reference MD5s, no checker bit."""
+    import bench
+    monkeypatch.setenv("H264MI_CHECK", "1")
+    seeds = [1, 2, 3, 4]
+    _, caps = bench.prepare(1, seeds, 6)
+    run = bench.DeviceRun(_lib.mi(), caps, 0, 6, 1)
+    try:
+        refs = [bench.golden_frames(1, sd, {}) for sd in seeds]
+        ok, checked, missing, _ = run.verify(refs)
+        assert run.eng.kernel_name() == "k_wgpp_check"
+        assert run.eng.last_mc_waves() == 6
+        assert run.eng.error_bits() == 0, f"dependency checker flags {run.eng.error_bits():#x}"
+        assert (ok, checked, missing) == (True, 24, 0)
+    finally:
+        run.free()

@@ -29,9 +29,9 @@ def main():
     elif which == "offpic0":
         r = bench.run_leg(L, torch, 3, seeds, steps, warm, overrides={"offpic_pct": 0}, pipe=pipe, mc_waves=2)
     elif which == "cfg2":
-        r = bench.run_leg(L, torch, 1, [1, 2, 3, 4], 20, 4)
+        r = bench.run_leg(L, torch, 1, [1, 2, 3, 4], 20, 4, mc_waves=0)
     elif which == "cfg2s1":
-        r = bench.run_leg(L, torch, 1, [1], 20, 4)
+        r = bench.run_leg(L, torch, 1, [1], 20, 4, mc_waves=0)
     elif which == "cfg5":
         r = bench.run_leg(L, torch, 4, [100], 21, 3, pipe=3)
     else:
