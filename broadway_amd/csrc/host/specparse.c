@@ -274,6 +274,14 @@ static void queue_slices(SpecPool *sp, const uint8_t *buf, uint32_t pos, uint32_
         if (nal_scan(buf + pos, len - pos, &init, &size, &rb, &emul) || size < 2 || rb == 0) break;
         const uint8_t t = buf[pos + init] & 31;
         if (t != NAL_SLICE && t != NAL_IDR) break;     /* a non-slice NAL ends the access unit */
+        /* so does a slice with first_mb_in_slice 0 (ue(v) '1': the top bit of
+         * the byte after the NAL header, never an emulation-prevention byte)
+         * after the first job: the next picture.  Its slices would only be
+         * scanned, copied, unescaped and declined by run_job (their header is
+         * not this picture's); with arbitrary slice order a later slice of
+         * this picture may start at MB 0 too, and is then parsed by the
+         * calling thread instead */
+        if (sp->njobs > 0 && size > 1 && (buf[pos + init + 1] & 0x80)) break;
         SpecJob *j = &sp->jobs[sp->njobs];
         if (j->raw_cap < rb) {
             free(j->raw);
