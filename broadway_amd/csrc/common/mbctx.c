@@ -18,7 +18,7 @@ static int neighbour_of(const PicCtx *pc, int cur, int n)
     default:   if (col == 0) return -1; a = cur - w - 1; break;
     }
     if (a < 0) return -1;
-    if (pc->mb[a].slice != pc->mb[cur].slice) return -1;
+    if (pc->slice[a] != pc->slice[cur]) return -1;
     return a;
 }
 
@@ -37,13 +37,13 @@ void mbctx_begin_mb(PicCtx *pc, int cur)
     {
         /* neighbour_of for the four, one division */
         const int w = pc->w, col = cur % w;
-        const uint16_t sl = pc->mb[cur].slice;
+        const uint16_t sl = pc->slice[cur];
         const int a = col > 0 ? cur - 1 : -1, b = cur - w;
         const int c = col < w - 1 ? cur - w + 1 : -1, d = col > 0 ? cur - w - 1 : -1;
-        pc->nb[NB_A] = a >= 0 && pc->mb[a].slice == sl ? a : -1;
-        pc->nb[NB_B] = b >= 0 && pc->mb[b].slice == sl ? b : -1;
-        pc->nb[NB_C] = c >= 0 && pc->mb[c].slice == sl ? c : -1;
-        pc->nb[NB_D] = d >= 0 && pc->mb[d].slice == sl ? d : -1;
+        pc->nb[NB_A] = a >= 0 && pc->slice[a] == sl ? a : -1;
+        pc->nb[NB_B] = b >= 0 && pc->slice[b] == sl ? b : -1;
+        pc->nb[NB_C] = c >= 0 && pc->slice[c] == sl ? c : -1;
+        pc->nb[NB_D] = d >= 0 && pc->slice[d] == sl ? d : -1;
     }
     const MbInfo *A = pc->nb[NB_A] >= 0 ? &pc->mb[pc->nb[NB_A]] : NULL;
     const MbInfo *B = pc->nb[NB_B] >= 0 ? &pc->mb[pc->nb[NB_B]] : NULL;

@@ -16,7 +16,6 @@
 typedef struct MbInfo {
     uint8_t  type;        /* MBT_* from mbrec.h */
     uint8_t  qp;          /* QPY as stored for deblocking (0 for I_PCM) */
-    uint16_t slice;       /* slice tag; SLICE_NONE if not yet decoded */
     int8_t   refidx[4];   /* per 8x8, -1 for intra */
     int8_t   i4mode[16];  /* Intra4x4PredMode (z-scan); valid for MBT_I4x4 */
     uint8_t  tc[16];      /* luma TotalCoeff (z-scan) */
@@ -30,6 +29,9 @@ typedef struct PicCtx {
     int      w, h;        /* picture size in MBs */
     int      cip;         /* constrained_intra_pred_flag */
     MbInfo  *mb;          /* w*h entries */
+    uint16_t *slice;      /* w*h slice tags, SLICE_NONE if not yet decoded: apart from
+                           * the 112-byte MbInfo, so that a picture's reset and a
+                           * committed slice touch 2 bytes per MB, not a cache line */
     /* neighbour cache of the MB being parsed (mbctx_begin_mb): nb[n] is
      * mbctx_neighbour(cur, n) while nb_key == cur + 1 (0: no cache; a
      * zero-initialised context has none) */

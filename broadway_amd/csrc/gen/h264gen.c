@@ -839,7 +839,7 @@ static void gen_slice(Gen *g, int idr, int first, int last, const SliceCfg *sc)
     for (int cur = first; cur <= last; cur++) {
         MbInfo *m = &g->pc.mb[cur];
         memset(m, 0, sizeof(*m));
-        m->slice = sc->tag;
+        g->pc.slice[cur] = sc->tag;
         g->cur_mb = cur;
         int base_mv[2] = {g->gmx + rnd_range(&g->rng, -p->mv_jitter, p->mv_jitter),
                           g->gmy + rnd_range(&g->rng, -p->mv_jitter, p->mv_jitter)};
@@ -907,7 +907,7 @@ static void gen_picture(Gen *g, int idx)
         }
         g->poc_lsb = (2 * d) & 255;
     }
-    for (int i = 0; i < nmb; i++) g->pc.mb[i].slice = SLICE_NONE;
+    for (int i = 0; i < nmb; i++) g->pc.slice[i] = SLICE_NONE;
     g->gmx += rnd_range(&g->rng, -6, 6);
     g->gmy += rnd_range(&g->rng, -4, 4);
     g->gmx = clampi(g->gmx, -256, 256);
@@ -962,9 +962,11 @@ int h264gen_generate(const GenParams *p, uint8_t **out, size_t *out_len)
     g.range_mb = -1;
     g.pc.w = p->w_mbs; g.pc.h = p->h_mbs; g.pc.cip = p->cip;
     g.pc.mb = (MbInfo *)calloc((size_t)p->w_mbs * p->h_mbs, sizeof(MbInfo));
-    if (!g.pc.mb) return -1;
+    g.pc.slice = (uint16_t *)calloc((size_t)p->w_mbs * p->h_mbs, sizeof(uint16_t));
+    if (!g.pc.mb || !g.pc.slice) { free(g.pc.mb); free(g.pc.slice); return -1; }
     for (int i = 0; i < p->nframes; i++) gen_picture(&g, i);
     free(g.pc.mb);
+    free(g.pc.slice);
     *out = g.out.buf;
     *out_len = g.out.len;
     return 0;

@@ -165,7 +165,7 @@ int h264dec_conceal(H264Dec *d, int is_i)
         }
     int first = 0;
     while (first < nmbs && !pb->decoded[first]) first++;
-    for (int i = 0; i < nmbs; i++) pb->rec[i].slice = pb->pc.mb[i].slice;
+    for (int i = 0; i < nmbs; i++) pb->rec[i].slice = pb->pc.slice[i];
 
     if (first == nmbs) {
         /* whole picture lost: grey, or a copy of the reference; no filtering */

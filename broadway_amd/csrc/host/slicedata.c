@@ -22,18 +22,19 @@ int picbuild_init(PicBuild *pb, int w_mbs, int h_mbs)
     pb->w = w_mbs; pb->h = h_mbs; pb->nmbs = w_mbs * h_mbs;
     pb->rec = (MbRec *)calloc((size_t)pb->nmbs, sizeof(MbRec));
     pb->pc.mb = (MbInfo *)calloc((size_t)pb->nmbs, sizeof(MbInfo));
+    pb->pc.slice = (uint16_t *)calloc((size_t)pb->nmbs, sizeof(uint16_t));
     pb->decoded = (uint8_t *)calloc((size_t)pb->nmbs, 1);
     pb->cap = (uint32_t)pb->nmbs * 8 + 64;
     pb->coef = (int16_t *)malloc((size_t)pb->cap * 32);
     pb->pc.w = w_mbs; pb->pc.h = h_mbs;
-    if (!pb->rec || !pb->pc.mb || !pb->coef || !pb->decoded) { picbuild_free(pb); return -1; }
+    if (!pb->rec || !pb->pc.mb || !pb->pc.slice || !pb->coef || !pb->decoded) { picbuild_free(pb); return -1; }
     return 0;
 }
 
 void picbuild_free(PicBuild *pb)
 {
-    free(pb->rec); free(pb->pc.mb); free(pb->coef); free(pb->decoded);
-    pb->rec = NULL; pb->pc.mb = NULL; pb->coef = NULL; pb->decoded = NULL;
+    free(pb->rec); free(pb->pc.mb); free(pb->pc.slice); free(pb->coef); free(pb->decoded);
+    pb->rec = NULL; pb->pc.mb = NULL; pb->pc.slice = NULL; pb->coef = NULL; pb->decoded = NULL;
 }
 
 /* a private PicBuild that receives one slice at a time (specparse.c): the
@@ -54,7 +55,7 @@ void picbuild_reuse(PicBuild *pb, int cip)
 void picbuild_reset(PicBuild *pb, int cip)
 {
     /* h264bsdResetStorage (storage.c:442-462): no MB decoded, no slice id */
-    for (int i = 0; i < pb->nmbs; i++) pb->pc.mb[i].slice = SLICE_NONE;
+    memset(pb->pc.slice, 0xFF, sizeof(uint16_t) * (size_t)pb->nmbs);      /* SLICE_NONE */
     picbuild_reset_counts(pb, cip);
 }
 
@@ -110,8 +111,8 @@ static void finish_rec(PicBuild *pb, int cur, const SliceHdr *sh, const Pps *pps
     if (sh->dbf_idc != 1) {
         av |= DB_INNER;
         int col = cur % pb->w;
-        if (col > 0 && (sh->dbf_idc != 2 || pc->mb[cur - 1].slice == tag)) av |= DB_LEFT;
-        if (cur >= pb->w && (sh->dbf_idc != 2 || pc->mb[cur - pb->w].slice == tag)) av |= DB_TOP;
+        if (col > 0 && (sh->dbf_idc != 2 || pc->slice[cur - 1] == tag)) av |= DB_LEFT;
+        if (cur >= pb->w && (sh->dbf_idc != 2 || pc->slice[cur - pb->w] == tag)) av |= DB_TOP;
     }
     r->avail = av;
     r->offA = (int8_t)(sh->off_a_div2 * 2);
@@ -459,7 +460,7 @@ static int slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps
             for (uint32_t i = 0; i < run; i++, cur++) {
                 if (pb->decoded[cur]) return -1;      /* primary picture, already decoded */
                 memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
-                pb->pc.mb[cur].slice = tag;
+                pb->pc.slice[cur] = tag;
                 mbctx_begin_mb(&pb->pc, cur);
                 pb->mb_decode_err = 0;
                 decode_skip(pb, cur, qp, ref_slot);
@@ -476,7 +477,7 @@ static int slice_data(PicBuild *pb, BitReader *br, const SliceHdr *sh, const Pps
         if (cur >= pb->nmbs) return -1;
         if (pb->decoded[cur]) return -1;
         memset(&pb->pc.mb[cur], 0, sizeof(MbInfo));
-        pb->pc.mb[cur].slice = tag;                   /* SetMbParams precedes the parse */
+        pb->pc.slice[cur] = tag;                   /* SetMbParams precedes the parse */
         mbctx_begin_mb(&pb->pc, cur);
         pb->mb_decode_err = 0;
         if (parse_mb(pb, br, cur, sh, pps, ref_slot, &qp)) return -1;
@@ -502,13 +503,13 @@ void picbuild_mark_slice_corrupted(PicBuild *pb, int first_mb)
         const int keep_back = pb->w > 10 ? pb->w : 10;
         int i = pb->last_mb_addr - 1, n = 0;
         while (i > cur) {
-            if (pb->pc.mb[i].slice == tag && ++n >= keep_back) break;
+            if (pb->pc.slice[i] == tag && ++n >= keep_back) break;
             i--;
         }
         cur = i;
     }
     for (; cur < pb->nmbs; cur++) {
-        if (pb->pc.mb[cur].slice != tag || !pb->decoded[cur]) break;
+        if (pb->pc.slice[cur] != tag || !pb->decoded[cur]) break;
         pb->decoded[cur] = 0;
     }
 }

@@ -416,7 +416,7 @@ static int commit(SpecPool *sp, SpecJob *j, H264Dec *d, const uint8_t *buf, uint
         pb->rec[i] = q->rec[i];
         pb->rec[i].coef += off;
         pb->rec[i].slice = tag;
-        pb->pc.mb[i].slice = tag;
+        pb->pc.slice[i] = tag;
         pb->decoded[i] = 1;
     }
     pb->ndecoded += count;
