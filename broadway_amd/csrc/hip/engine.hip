@@ -611,6 +611,49 @@ int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int
     return launch_batch(e, npics, 1, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
 }
 
+int engine_decode_direct(h264mi_engine *e, int stream, int cur_slot, const void *rec, const int16_t *coef,
+                         uint32_t ncoef, int intra_heavy)
+{
+    if (!e || stream < 0 || stream >= e->nstreams || cur_slot < 0 || cur_slot >= e->nslots) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    // the descriptor staging is reused: wait until the previous upload consumed it
+    HIPCHECK(hipEventSynchronize(e->ev_staged));
+    if ((size_t)ncoef + 16 > e->coef_cap) {
+        HIPCHECK(hipStreamSynchronize(e->st));
+        (void)hipFree(e->d_coef);
+        (void)hipHostFree(e->h_coef);
+        e->coef_cap = e->h_coef_cap = ncoef + ncoef / 2 + 1024;
+        HIPCHECK(hipMalloc(&e->d_coef, e->coef_cap * 32));
+        HIPCHECK(hipHostMalloc(&e->h_coef, e->h_coef_cap * 32, hipHostMallocDefault));
+    }
+    PicDesc &pd = e->h_pics[0];
+    pd.rec_base = 0;
+    pd.frame_base = (uint32_t)(stream * e->nslots);
+    pd.cur_slot = (uint32_t)cur_slot;
+    {
+        const MbRec *r = (const MbRec *)rec;
+        int n = 0, db = 0;
+        for (int m = 0; m < e->nmbs; m++) { n += r[m].type >= MBT_I4x4; db |= r[m].avail & DB_INNER; }
+        pd.flags = (2 * n > e->nmbs ? PD_INTRA_HEAVY : 0) | (db ? 0 : PD_NO_DEBLOCK);
+    }
+    pd.coef_base = 0;
+    pd.rsv[0] = pd.rsv[1] = pd.rsv[2] = 0;
+    HIPCHECK(hipMemcpyAsync(e->d_rec, rec, sizeof(MbRec) * e->nmbs, hipMemcpyHostToDevice, e->st));
+    if (ncoef) HIPCHECK(hipMemcpyAsync(e->d_coef, coef, (size_t)ncoef * 32, hipMemcpyHostToDevice, e->st));
+    HIPCHECK(hipMemcpyAsync(e->d_pics, e->h_pics, sizeof(PicDesc), hipMemcpyHostToDevice, e->st));
+    HIPCHECK(hipEventRecord(e->ev_staged, e->st));
+    e->launch_intra = intra_heavy >= 0 ? intra_heavy : (pd.flags & PD_INTRA_HEAVY) != 0;
+    return launch_batch(e, 1, 1, e->d_rec, e->d_coef, e->d_pics, NULL, NULL, NULL);
+}
+
+int engine_records_wait(h264mi_engine *e)
+{
+    if (!e) return -1;
+    HIPCHECK(hipSetDevice(e->dev));
+    HIPCHECK(hipEventSynchronize(e->ev_staged));
+    return 0;
+}
+
 // the next launch's content, for callers holding their records on the device
 // (launch_nmc): 1 = some picture has more than half its MBs intra, 0 = none
 extern "C" int h264mi_engine_hint_intra(h264mi_engine *e, int intra_heavy)

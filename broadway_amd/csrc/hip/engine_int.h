@@ -20,6 +20,13 @@
 int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int *cur_slot,
                        const void *const *recs, const int16_t *const *coefs, const uint32_t *ncoef,
                        int intra_heavy);
+/* one host picture whose records and coefficient blocks are in pinned host
+ * memory: uploaded straight from them (no staging copy); the caller keeps
+ * them unchanged until engine_records_wait returns */
+int engine_decode_direct(h264mi_engine *e, int stream, int cur_slot, const void *rec, const int16_t *coef,
+                         uint32_t ncoef, int intra_heavy);
+/* the last batch's uploads have completed (its host records may change) */
+int engine_records_wait(h264mi_engine *e);
 /* wait for everything queued on the engine's stream (sleeping when the engine
  * was created under H264MI_BLOCKING_SYNC); no flag accounting */
 int engine_wait(h264mi_engine *e);

@@ -165,6 +165,7 @@ int h264dec_conceal(H264Dec *d, int is_i)
         }
     int first = 0;
     while (first < nmbs && !pb->decoded[first]) first++;
+    h264dec_pb_writable(d);
     for (int i = 0; i < nmbs; i++) pb->rec[i].slice = pb->pc.slice[i];
 
     if (first == nmbs) {
@@ -210,6 +211,7 @@ int h264dec_conceal(H264Dec *d, int is_i)
     }
     int rc = d->be.decode(d->be.ctx, pb, d->cur_slot);
     if (!rc && !on_backend) rc = d->be.read(d->be.ctx, d->cur_slot, img) < 0 ? -1 : 0;
+    h264dec_pb_writable(d);                 /* pass 1's records are uploaded */
     for (int i = 0; i < nmbs; i++) if (pb->decoded[i]) pb->rec[i].avail = saved[i];
     free(saved);
     if (rc) { free(img); return -1; }

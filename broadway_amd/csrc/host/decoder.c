@@ -53,6 +53,13 @@ int h264dec_init(H264Dec *d, int no_output_reordering, H264Backend be)
     return 0;
 }
 
+/* the backend may still be uploading the last picture's records from d->pb
+ * (H264Backend.records_wait): wait before writing them */
+void h264dec_pb_writable(H264Dec *d)
+{
+    if (d->pb.pinned && d->be.records_wait) (void)d->be.records_wait(d->be.ctx);
+}
+
 static void out_frames_free(H264Dec *d)
 {
     if (d->out_frames && d->be.host_free) d->be.host_free(d->be.ctx, d->out_frames);
@@ -64,7 +71,10 @@ void h264dec_release(H264Dec *d)
 {
     spec_destroy(d->spec);
     d->spec = NULL;
-    if (d->pb_ready) picbuild_free(&d->pb);
+    if (d->pb_ready) {
+        h264dec_pb_writable(d);
+        picbuild_free(&d->pb);
+    }
     free(d->rbsp);
     out_frames_free(d);
     if (d->be.destroy) d->be.destroy(d->be.ctx);
@@ -312,9 +322,15 @@ static int check_au_boundary(H264Dec *d, const NalHdr *nal, const BitReader *br,
 static int ensure_picbuild(H264Dec *d, const Sps *sps)
 {
     if (d->pb_ready && d->pb.w == sps->w_mbs && d->pb.h == sps->h_mbs) return 0;
-    if (d->pb_ready) picbuild_free(&d->pb);
+    if (d->pb_ready) {
+        h264dec_pb_writable(d);
+        picbuild_free(&d->pb);
+    }
     d->pb_ready = 0;
-    if (picbuild_init(&d->pb, sps->w_mbs, sps->h_mbs)) return -1;
+    /* pinned records when the backend uploads from them (records_wait) */
+    const int pinned = d->be.records_wait && d->be.host_alloc && d->be.host_free;
+    if (picbuild_init_alloc(&d->pb, sps->w_mbs, sps->h_mbs, pinned ? d->be.host_alloc : NULL,
+                            pinned ? d->be.host_free : NULL, d->be.ctx)) return -1;
     d->pb_ready = 1;
     return 0;
 }
@@ -445,7 +461,7 @@ static int decode_nal(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic
             if (!d->valid_slice_in_au) {
                 d->cur_slot = dpb_alloc_current(&d->dpb);
                 if (d->cur_slot < 0) return DEC_FAIL(DEC_ERROR);
-                picbuild_reset(&d->pb, 0);
+                h264dec_pb_writable(d), picbuild_reset(&d->pb, 0);
                 d->pb.cur_slot = d->cur_slot;
                 SliceHdr tmp = d->sh;
                 int ref_slot[MAX_REFS];
@@ -533,7 +549,7 @@ static int decode_nal(H264Dec *d, const uint8_t *buf, uint32_t len, uint32_t pic
                 return DEC_FAIL(DEC_ERROR);
             d->cur_slot = dpb_alloc_current(&d->dpb);
             if (d->cur_slot < 0) return DEC_FAIL(DEC_ERROR);
-            picbuild_reset(&d->pb, pps->cip);
+            h264dec_pb_writable(d), picbuild_reset(&d->pb, pps->cip);
             d->pb.cur_slot = d->cur_slot;
         }
         d->sh = sh;

@@ -27,8 +27,14 @@ typedef struct H264Backend {
     /* (re)allocate frame slots for a w x h (MBs) stream with nslots frames */
     int  (*configure)(void *ctx, int w_mbs, int h_mbs, int nslots);
     /* reconstruct + deblock the picture described by pb into slot cur_slot
-     * (may run asynchronously; records are consumed before returning) */
+     * (may run asynchronously; records are consumed before returning, except
+     * from a PicBuild allocated with host_alloc when records_wait is set) */
     int  (*decode)(void *ctx, const PicBuild *pb, int cur_slot);
+    /* optional: the decoder then allocates its picture's records and
+     * coefficients with host_alloc (pinned), decode uploads straight from
+     * them, and the decoder calls this before it writes that PicBuild again
+     * (the upload of the last picture has completed on return) */
+    int  (*records_wait)(void *ctx);
     /* copy slot as planar I420 (w*16 * h*16 * 3/2 bytes) to host memory;
      * 0 ok, -1 failure, 1 copied but the device flagged an error in a
      * reconstruction since the last read */
@@ -136,6 +142,8 @@ int  h264dec_valid_param_sets(const H264Dec *d);
 /* conceal the current picture's missing MBs (conceal.c); returns their
  * number or -1 */
 int  h264dec_conceal(H264Dec *d, int is_i);
+/* wait until the backend no longer reads d->pb (H264Backend.records_wait) */
+void h264dec_pb_writable(H264Dec *d);
 /* ConcealMb's neighbour path for the MB at (row, col) of an I420 picture of
  * w x h MBs in host memory, reading the MBs flagged in dec (the host
  * restatement of k_conceal; conceal.c) */

@@ -361,7 +361,11 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
         const void *recs[1] = {pb->rec};
         const int16_t *coefs[1] = {pb->coef};
         uint32_t nc[1] = {pb->ncoef};
-        if (engine_decode_host(e, 1, &stream, &cur_slot, recs, coefs, nc, 2 * (int)pb->n_intra > pb->nmbs)) {
+        const int heavy = 2 * (int)pb->n_intra > pb->nmbs;
+        // the decoder's own picture is in pinned memory (hb_host_alloc): uploaded
+        // straight from it, the decoder waits (hb_records_wait) before reusing it
+        if (pb->pinned ? engine_decode_direct(e, stream, cur_slot, pb->rec, pb->coef, pb->ncoef, heavy)
+                       : engine_decode_host(e, 1, &stream, &cur_slot, recs, coefs, nc, heavy)) {
             (void)hipMemsetAsync(engine_err_words(e), 0, sizeof(unsigned), st);
             return -1;
         }
@@ -387,6 +391,14 @@ static int hb_decode(void *vctx, const PicBuild *pb, int cur_slot)
     // (a waiter gets the lock back long before SHARE_RC_RING more batches
     // launch: each later batch takes a picture or a 1 ms wait of another instance)
     return sh->rc_ring[mine % SHARE_RC_RING];
+}
+
+static int hb_records_wait(void *vctx)
+{
+    HipBackendCtx *c = (HipBackendCtx *)vctx;
+    // a shared engine's decode returns after its batch consumed the records
+    if (c->sh || !c->e) return 0;
+    return engine_records_wait(c->e);
 }
 
 static int hb_prefetch(void *vctx, int slot, uint8_t *dst)
@@ -605,6 +617,7 @@ extern "C" H264Backend h264mi_hip_backend_create(int device)
     be.read_rgba = hb_read_rgba;
     be.host_alloc = hb_host_alloc;
     be.host_free = hb_host_free;
+    be.records_wait = hb_records_wait;
     be.copy = hb_copy;
     // H264MI_HOST_CONCEAL=1: conceal on the host (a copy of the picture, conceal.c)
     be.conceal = getenv("H264MI_HOST_CONCEAL") && atoi(getenv("H264MI_HOST_CONCEAL")) ? NULL : hb_conceal;

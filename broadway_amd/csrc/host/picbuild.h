@@ -27,9 +27,18 @@ typedef struct PicBuild {
     int      is_p;         /* any P slice in the picture */
     uint64_t alg_ref_bytes;    /* algorithmic MC footprint bytes */
     uint32_t n_inter, n_intra, n_coded_blocks;
+    /* optional allocator of rec / coef (picbuild_init_alloc): the HIP
+     * backend's pinned host memory, which it uploads from directly (no staging
+     * copy); `pinned` = rec and coef came from it */
+    void  *(*halloc)(void *ctx, size_t bytes);
+    void   (*hfree)(void *ctx, void *p);
+    void    *hctx;
+    int      pinned;
 } PicBuild;
 
 int  picbuild_init(PicBuild *pb, int w_mbs, int h_mbs);
+int  picbuild_init_alloc(PicBuild *pb, int w_mbs, int h_mbs, void *(*halloc)(void *, size_t),
+                         void (*hfree)(void *, void *), void *hctx);
 void picbuild_free(PicBuild *pb);
 void picbuild_reset(PicBuild *pb, int cip);      /* start of a new picture */
 void picbuild_reuse(PicBuild *pb, int cip);      /* the next slice into a private PicBuild (slice ids count on) */

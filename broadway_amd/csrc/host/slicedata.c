@@ -18,14 +18,34 @@ static void picbuild_reset_counts(PicBuild *pb, int cip);
 
 int picbuild_init(PicBuild *pb, int w_mbs, int h_mbs)
 {
+    return picbuild_init_alloc(pb, w_mbs, h_mbs, NULL, NULL, NULL);
+}
+
+static void *pb_alloc(PicBuild *pb, size_t bytes)
+{
+    return pb->halloc ? pb->halloc(pb->hctx, bytes) : malloc(bytes);
+}
+static void pb_free(PicBuild *pb, void *p)
+{
+    if (pb->halloc) { if (p) pb->hfree(pb->hctx, p); }
+    else free(p);
+}
+
+int picbuild_init_alloc(PicBuild *pb, int w_mbs, int h_mbs, void *(*halloc)(void *, size_t),
+                        void (*hfree)(void *, void *), void *hctx)
+{
     memset(pb, 0, sizeof(*pb));
+    pb->halloc = halloc && hfree ? halloc : NULL;
+    pb->hfree = hfree; pb->hctx = hctx;
+    pb->pinned = pb->halloc != NULL;
     pb->w = w_mbs; pb->h = h_mbs; pb->nmbs = w_mbs * h_mbs;
-    pb->rec = (MbRec *)calloc((size_t)pb->nmbs, sizeof(MbRec));
+    pb->rec = (MbRec *)pb_alloc(pb, (size_t)pb->nmbs * sizeof(MbRec));
+    if (pb->rec) memset(pb->rec, 0, (size_t)pb->nmbs * sizeof(MbRec));
     pb->pc.mb = (MbInfo *)calloc((size_t)pb->nmbs, sizeof(MbInfo));
     pb->pc.slice = (uint16_t *)calloc((size_t)pb->nmbs, sizeof(uint16_t));
     pb->decoded = (uint8_t *)calloc((size_t)pb->nmbs, 1);
     pb->cap = (uint32_t)pb->nmbs * 8 + 64;
-    pb->coef = (int16_t *)malloc((size_t)pb->cap * 32);
+    pb->coef = (int16_t *)pb_alloc(pb, (size_t)pb->cap * 32);
     pb->pc.w = w_mbs; pb->pc.h = h_mbs;
     if (!pb->rec || !pb->pc.mb || !pb->pc.slice || !pb->coef || !pb->decoded) { picbuild_free(pb); return -1; }
     return 0;
@@ -33,7 +53,7 @@ int picbuild_init(PicBuild *pb, int w_mbs, int h_mbs)
 
 void picbuild_free(PicBuild *pb)
 {
-    free(pb->rec); free(pb->pc.mb); free(pb->pc.slice); free(pb->coef); free(pb->decoded);
+    pb_free(pb, pb->rec); free(pb->pc.mb); free(pb->pc.slice); pb_free(pb, pb->coef); free(pb->decoded);
     pb->rec = NULL; pb->pc.mb = NULL; pb->pc.slice = NULL; pb->coef = NULL; pb->decoded = NULL;
 }
 
@@ -77,8 +97,16 @@ int16_t *picbuild_coef_alloc(PicBuild *pb, uint32_t nblk)
     if (pb->ncoef + nblk > pb->cap) {
         uint32_t nc = pb->cap * 2;
         while (nc < pb->ncoef + nblk) nc *= 2;
-        int16_t *p = (int16_t *)realloc(pb->coef, (size_t)nc * 32);
-        if (!p) return NULL;
+        int16_t *p;
+        if (pb->halloc) {
+            p = (int16_t *)pb->halloc(pb->hctx, (size_t)nc * 32);
+            if (!p) return NULL;
+            memcpy(p, pb->coef, (size_t)pb->ncoef * 32);
+            pb->hfree(pb->hctx, pb->coef);
+        } else {
+            p = (int16_t *)realloc(pb->coef, (size_t)nc * 32);
+            if (!p) return NULL;
+        }
         pb->coef = p;
         pb->cap = nc;
     }

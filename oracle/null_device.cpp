@@ -194,6 +194,14 @@ int engine_decode_host(h264mi_engine *e, int npics, const int *stream, const int
     }
     return 0;
 }
+int engine_decode_direct(h264mi_engine *e, int stream, int cur_slot, const void *rec, const int16_t *coef,
+                         uint32_t ncoef, int intra_heavy)
+{
+    const void *recs[1] = {rec};
+    const int16_t *coefs[1] = {coef};
+    return engine_decode_host(e, 1, &stream, &cur_slot, recs, coefs, &ncoef, intra_heavy);
+}
+int engine_records_wait(h264mi_engine *e) { return e ? 0 : -1; }
 int engine_wait(h264mi_engine *e) { return e ? 0 : -1; }
 hipStream_t engine_stream(h264mi_engine *e) { return e->st; }
 unsigned *engine_err_words(h264mi_engine *e) { return e->err; }
