@@ -737,6 +737,7 @@ __device__ uint32_t i4_entry(int mode, int x, int y, int avtr)
 // its ring slot as they land there, not after it is complete.  LeftNb: that
 // slot's samples and progress words (MbRing::lprog / cprog, tagged with the
 // MB index) and this MB's own progress words.
+template <bool LDSM> __device__ __forceinline__ unsigned long long ld_granT(const unsigned long long *p);
 struct LeftNb {
     const uint8_t *lp;              // left MB's ring slot (samples), NULL when unavailable (no AV_A)
     const int *lprog, *cprog;       // its progress words
@@ -744,6 +745,13 @@ struct LeftNb {
     int ltag, mytag;                // (c - 1) << 4, c << 4
     unsigned *perr;
     bool chk;                       // dependency checker: the word must name the left MB
+    // intra_tile CDEF: the above-right MB's granule (read by I4x4 block 5
+    // only, step 3) is waited for there, not before the luma starts: lane
+    // 32's pointer, last value and the tag it must carry; cdef wave-uniform
+    const unsigned long long *cg;
+    unsigned long long cgr;
+    uint32_t ctag;
+    bool cdef;
 };
 __device__ __forceinline__ void prog_wait(const int *p, int want, int lane, unsigned *perr, bool chk = false)
 {
@@ -775,6 +783,7 @@ __device__ __forceinline__ void prog_set(int *p, int v, int lane)
 // phase before it uses any, so a phase costs one LDS round trip
 // (Intra16x16 :626-686, Intra4x4 :700-832, IntraChroma :844-914,
 // AddResidual :926-988).
+template <bool UPL = false, bool CDEF = false>
 __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint64_t i4, const int16_t *res, bool has_res,
                                            uint8_t *ty, uint8_t *tu, uint8_t *tv, const uint32_t *i4tab, uint8_t *junk,
                                            uint8_t *px, int lane, const LeftNb &N, int part = 3)
@@ -919,9 +928,24 @@ __device__ __forceinline__ void intra_tile(int mbtype, int avail, int pred, uint
             const int o0 = blk_y(b0) * 64 + blk_x(b0) * 4, o1 = blk_y(b1) * 64 + blk_x(b1) * 4;
             rv[s] = has_res ? (int)res[(slot ? o1 : o0) + py4 * 16 + px4] : 0;
         }
+        // CDEF: lane 32 re-reads the above-right granule now, so that the load
+        // has landed by step 3
+        unsigned long long cgv = CDEF ? N.cgr : 0ull;
+        if (CDEF && N.cdef && lane == 32 && (uint32_t)(cgv >> 32) != N.ctag) cgv = ld_granT<UPL>(N.cg);
 #pragma unroll
         for (int s = 0; s < 10; s++) {
             const int b0 = i4s0(s), b1 = i4s1(s);
+            if (CDEF && s == 3 && N.cdef) {     // block 5 reads the above-right MB's bottom row
+                const bool need = lane == 32;
+                unsigned spins = 0;
+                while (__builtin_amdgcn_ballot_w64(need && (uint32_t)(cgv >> 32) != N.ctag) != 0) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (++spins > (1u << 20)) { if (lane == 0) atomicOr(N.perr, 2u); break; }   // bounded wait
+                    if (need) cgv = ld_granT<UPL>(N.cg);
+                }
+                if (need) *(uint32_t *)&ty[TX0 + 16] = (uint32_t)cgv;
+                wave_sync();
+            }
             // a block in column 0 (steps 0, 2, 4, 6: blocks 0, 2, 8, 10) reads
             // the left MB's block beside it (5, 7, 13, 15: its steps 3, 5, 7, 9)
             if ((s & 1) == 0 && s <= 6 && aA) {
@@ -1354,7 +1378,10 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
                 if (mine_part) gr = ld_granT<UPL>(g);
             }
         };
-        if (need_top) top_wait(mine && lumal);
+        // the above-right granule (needC: I4x4 block 5 in modes 3 / 7) is
+        // taken before step 3 only (intra_tile CDEF)
+        const bool cdef = needC;
+        if (need_top) top_wait(mine && lumal && !(cdef && lane == 32));
         if (pst) st0 = (st0 & 0xFFFFFFFFull) | (wall_clock64() << 32);
         {   // luma tile halo: the row above (dwords), its top-left / top-right (the
             // left column is read from the left MB's slot as it lands, intra_tile)
@@ -1362,7 +1389,7 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
             if (lane >= 24 && lane < 28) {
                 if (aB) *(uint32_t *)&M.ty[TX0 + (lane - 24) * 4] = top;
             } else if (lane == 32) {
-                if (needC) *(uint32_t *)&M.ty[TX0 + 16] = top;
+                if (needC && !cdef) *(uint32_t *)&M.ty[TX0 + 16] = top;
             } else if (lane == 33) {
                 if (aD) M.ty[TX0 - 1] = (uint8_t)(top >> 24);
             }
@@ -1377,7 +1404,8 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
         N.ltag = (c - 1) << 4; N.mytag = c << 4;
         N.perr = perr;
         N.chk = CHK;
-        intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N, 1);
+        N.cg = g; N.cgr = gr; N.ctag = tag; N.cdef = cdef;
+        intra_tile<UPL, true>(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N, 1);
         if (pub && lane < 4)        // luma bottom row -> the row below (entry c, dwords 24..27)
             st_granT<MEL>(pub + 24 + lane, *(const uint32_t *)&px[240 + lane * 4], tag);
         if (need_top) top_wait(mine && !lumal);
