@@ -1331,12 +1331,14 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
     unsigned long long gr = need_top ? ld_granT<UPL>(g) : 0ull;
     if constexpr (!LF) {
         if (pst) st0 = wall_clock64();
+        // the above-right granule (needC) only before I4x4 step 3 (intra_tile CDEF)
+        const bool minew = mine && !(needC && lane == 32);
         if (need_top) {
             unsigned spins = 0;
-            while (__builtin_amdgcn_ballot_w64(mine && (uint32_t)(gr >> 32) != tag) != 0) {
+            while (__builtin_amdgcn_ballot_w64(minew && (uint32_t)(gr >> 32) != tag) != 0) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 20)) { if (lane == 0) atomicOr(perr, 2u); break; }   // bounded wait
-                if (mine) gr = ld_granT<UPL>(g);
+                if (minew) gr = ld_granT<UPL>(g);
             }
         }
         const uint32_t top = (uint32_t)gr;
@@ -1347,7 +1349,6 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
                 const int k = lane - 24;
                 if (aB) *(uint32_t *)(k < 4 ? &M.ty[TX0 + k * 4] : k < 6 ? &M.tu[TX0 + (k - 4) * 4] : &M.tv[TX0 + (k - 6) * 4]) = top;
             } else if (lane == 32) {
-                if (needC) *(uint32_t *)&M.ty[TX0 + 16] = top;
             } else if (lane < 36) {
                 if (aD) (lane == 33 ? M.ty[TX0 - 1] : lane == 34 ? M.tu[TX0 - 1] : M.tv[TX0 - 1]) = (uint8_t)(top >> 24);
             }
@@ -1362,7 +1363,8 @@ __device__ __attribute__((noinline)) void mc_intra(g_MbRec *mbrec, const unsigne
         N.ltag = (c - 1) << 4; N.mytag = c << 4;
         N.perr = perr;
         N.chk = CHK;
-        intra_tile(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
+        N.cg = g; N.cgr = gr; N.ctag = tag; N.cdef = needC;
+        intra_tile<UPL, true>(qtype, avail, pred, i4, M.res, cbits != 0, M.ty, M.tu, M.tv, i4tab, M.junk, px, lane, N);
     } else {
         if (pst) st0 = wall_clock64();
         // luma first: its top granules (B dwords 24..27, C, D's luma byte) are
